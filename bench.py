@@ -1,0 +1,161 @@
+"""Benchmark: hybrid rollout timesteps/sec (batched ICs) on MI355X.
+
+Workload (BASELINE.json configs[2], the north star's "4096-IC batch of 64-cell
+chains at 1 MI355X"): per GPU 4096 independent ICs x 64 cells, FluxGNN(4,128,4)
+float32 with the r=3 ablation checkpoint's architecture (weights from the
+committed 1-epoch fixture tests/golden/weights_W1_r3.npz), synthetic ICs from
+the reference IC generator (seeds 1000 + global IC index).  A step is one full
+hybrid timestep of the whole batch: GNN -> flux symmetrisation -> FV
+continuity + Burgers -> spectral Poisson; the rollout records every state
+(as HybridSolver.run does).  N GPUs: weak scaling, 4096 ICs per rank, no
+communication while stepping, one RCCL all_gather of per-IC metrics.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--ics-per-gpu B] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gnn-plasma-flux_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+GNN_FLOP_PER_CELL_STEP = 329_216   # input 1,024 + layers 262,144 + P/Q readout 66,048
+STATE_BYTES_PER_CELL_STEP = 24     # read (n,u,E) + write (n,u,E) float32
+PEAK_F32_MFMA_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+PEAK_HBM_GBS = 8000.0
+METRIC = "hybrid rollout timesteps/sec (batched ICs) at 1/2/4/8 MI355X"
+
+
+def cpu_baseline(weights, nx, T, n_ics, threads):
+    """Reference-faithful CPU hybrid solver (oracle port: one IC at a time,
+    torch-CPU FluxGNN + numpy FV/FFT, src/hybrid_solver.py:34-73) on a bounded
+    sample; plus the batched torch-CPU form for context."""
+    from oracle import hybrid_oracle as O
+    torch.set_num_threads(threads)
+    p = O.params_from(weights)
+    G = O.Grid(nx)
+    ics = np.stack([O.initial_condition(G, 1000 + i) for i in range(n_ics)])
+    O.hybrid_run_per_ic(p, G, ics[:1], 2)  # warm the allocator / BLAS
+    t0 = time.perf_counter()
+    O.hybrid_run_per_ic(p, G, ics, T)
+    alpha = n_ics * T / (time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    O.hybrid_run(p, G, ics, T)
+    beta = n_ics * T / (time.perf_counter() - t0)
+    return alpha, beta
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--ics-per-gpu", type=int, default=4096)
+    ap.add_argument("--nx", type=int, default=64)
+    ap.add_argument("--weights", default=os.path.join(ROOT, "tests", "golden", "weights_W1_r3.npz"))
+    ap.add_argument("--no-traj", action="store_true", help="do not record the state trajectory")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-ics", type=int, default=256)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from hybridflux import HybridSolver
+    from hybridflux.rollout import gather_ic_rows, shard_seeds
+
+    weights = dict(np.load(args.weights, allow_pickle=False))
+    B, nx, K, W = args.ics_per_gpu, args.nx, args.steps, args.warmup
+    n_total = B * world
+    solver = HybridSolver(weights, radius=3, nx=nx, device=dev)
+    ics = solver.baseline.initial_conditions(shard_seeds(1000, n_total, world, rank), as_tensor=True)
+    stream = torch.cuda.current_stream(dev)
+
+    # warmup: one rollout of W steps (compiles nothing; faults the code objects in)
+    solver.run_batch(ics, max(W, 1), traj=not args.no_traj, metrics=True)
+    torch.cuda.synchronize(dev)
+
+    # preallocate outputs so the timed region is launches only
+    final = torch.empty_like(ics)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    res = solver.run_batch(ics, K, traj=not args.no_traj, metrics=True, out=final)
+    ev1.record(stream)
+    gathered = gather_ic_rows(res["metrics"][:, -1], n_total)   # RCCL all_gather of final metrics
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1)
+
+    t_max = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    wall_max = float(t_max.item())
+    finite = float(gathered[:, 2].float().mean().item())
+
+    if rank == 0:
+        value = n_total * K / wall_max
+        flop = GNN_FLOP_PER_CELL_STEP * B * nx * K
+        achieved = flop / (kernel_ms * 1e-3) / 1e12
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            threads = min(16, os.cpu_count() or 1)
+            alpha, beta = cpu_baseline(weights, nx, 30, args.cpu_sample_ics, threads)
+            cpu = {"value": round(alpha, 1), "unit": "IC-steps/s", "cores": threads, "kind": "port",
+                   "sample": f"{args.cpu_sample_ics} ICs x 30 steps, one IC at a time (reference-faithful "
+                             f"HybridSolver loop: torch-CPU FluxGNN + numpy FV/FFT), nx={nx}",
+                   "batched_torch_cpu_value": round(beta, 1)}
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "IC-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(wall_max / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference IC generator seeds 1000.., fixture weights W1_r3 (1-epoch reference trainer)",
+            "config": {"workload": f"cfg3: {nx}-cell periodic chain, {B}-IC batch per GPU, FluxGNN(4,128,4) f32, "
+                                   f"{K}-step persistent rollout{'' if args.no_traj else ' recording every state'}",
+                       "nx": nx, "ics_per_gpu": B, "global_ics": n_total, "parallelism": f"ic-shard x{world}"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_MFMA_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
+                         "traffic": None,
+                         "kernel": "chain_rollout_kernel<4>", "kernel_ms": round(kernel_ms, 3),
+                         "flop_per_launch": flop,
+                         "hbm_state_frac": round(STATE_BYTES_PER_CELL_STEP * B * nx * K / (kernel_ms * 1e-3)
+                                                 / (PEAK_HBM_GBS * 1e9), 6)},
+            "cpu_baseline": cpu,
+            "finite_fraction": finite,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,407 @@
+// C ABI of libhybridflux (include/hybridflux.h): model handles, weight
+// packing into MFMA fragment order, argument validation, launch sequencing.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hf_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+int fail_hip(hipError_t e, const char *what) {
+  return fail(HF_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HF_CHECK_HIP(expr, what)                  \
+  do {                                            \
+    hipError_t _e = (expr);                       \
+    if (_e != hipSuccess) return fail_hip(_e, what); \
+  } while (0)
+
+}  // namespace
+
+struct hf_model {
+  int in_dim = 0, hidden = 0, layers = 0, wdtype = 0;
+  bool chain_ok = false;  // fused chain kernels need in_dim 4, hidden 128, f32
+  float *dev = nullptr;   // single device allocation holding every buffer
+  hf::ChainW chain{};
+  hf::GraphW graph{};
+};
+
+namespace {
+
+// Offsets of each parameter inside the reference-ordered flat array.
+struct Layout {
+  int64_t w_in, b_in, w_l, b_l, w_e, b_e, w_2, b_2, total;
+  Layout(int in, int H, int L) {
+    int64_t o = 0;
+    w_in = o; o += (int64_t)H * in;
+    b_in = o; o += H;
+    w_l = o;  // per layer: weight [H][2H] then bias [H]
+    b_l = -1;
+    o += (int64_t)L * ((int64_t)H * 2 * H + H);
+    w_e = o; o += (int64_t)H * 2 * H;
+    b_e = o; o += H;
+    w_2 = o; o += H;
+    b_2 = o; o += 1;
+    total = o;
+  }
+};
+
+// Pack the reference weights into the A-fragment order of chain_gnn.hip.
+//  k-step s of a 128-wide half, lane l: k = 16*(s>>2) + 4*(l>>4) + (s&3),
+//  output row n = 16*nt + (l&15).
+int kperm(int s, int lane) { return 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3); }
+
+void pack_chain_f32(const float *p, int L, std::vector<float> &out, int64_t &o_win, int64_t &o_bin,
+                    int64_t &o_wl, int64_t &o_bl, int64_t &o_we, int64_t &o_be, int64_t &o_w2,
+                    float &b2) {
+  using hf::kH;
+  using hf::kKS;
+  using hf::kNT;
+  const Layout lay(hf::kIn, kH, L);
+  out.clear();
+  o_win = (int64_t)out.size();
+  for (int lane = 0; lane < 64; ++lane)
+    for (int nt = 0; nt < kNT; ++nt)
+      out.push_back(p[lay.w_in + (int64_t)(16 * nt + (lane & 15)) * hf::kIn + (lane >> 4)]);
+  o_bin = (int64_t)out.size();
+  out.insert(out.end(), p + lay.b_in, p + lay.b_in + kH);
+  o_wl = (int64_t)out.size();
+  for (int l = 0; l < L; ++l) {
+    const float *W = p + lay.w_l + (int64_t)l * ((int64_t)kH * 2 * kH + kH);
+    for (int s = 0; s < 2 * kKS; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int nt = 0; nt < kNT; ++nt) {
+          const int k = (s < kKS ? 0 : kH) + kperm(s % kKS, lane);
+          out.push_back(W[(int64_t)(16 * nt + (lane & 15)) * 2 * kH + k]);
+        }
+  }
+  o_bl = (int64_t)out.size();
+  for (int l = 0; l < L; ++l) {
+    const float *bl = p + lay.w_l + (int64_t)l * ((int64_t)kH * 2 * kH + kH) + (int64_t)kH * 2 * kH;
+    out.insert(out.end(), bl, bl + kH);
+  }
+  o_we = (int64_t)out.size();
+  for (int ot = 0; ot < kNT; ++ot)
+    for (int s = 0; s < kKS; ++s)
+      for (int lane = 0; lane < 64; ++lane) {
+        const int64_t row = (int64_t)(16 * ot + (lane & 15)) * 2 * kH;
+        out.push_back(p[lay.w_e + row + kperm(s, lane)]);
+        out.push_back(p[lay.w_e + row + kH + kperm(s, lane)]);
+      }
+  o_be = (int64_t)out.size();
+  out.insert(out.end(), p + lay.b_e, p + lay.b_e + kH);
+  o_w2 = (int64_t)out.size();
+  out.insert(out.end(), p + lay.w_2, p + lay.w_2 + kH);
+  b2 = p[lay.b_2];
+}
+
+hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+bool fused_nx(int nx) { return nx == 16 || nx == 32 || nx == 48 || nx == 64; }
+
+constexpr int kMaxFvNx = 6144;  // LDS bound of fv_poisson.hip (20 B per cell)
+
+int check_device() {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(HF_EHIP, "no HIP device visible: libhybridflux has no CPU path");
+  return HF_OK;
+}
+
+int chain_usable(const hf_model *m) {
+  if (!m->chain_ok)
+    return fail(HF_EUNSUPPORTED,
+                "chain kernels are specialised to FluxGNN(input_dim=4, hidden_dim=128) float32 "
+                "(src/config.py:19-23); use hf_graph_flux for other widths");
+  return HF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *hf_version(void) { return "hybridflux 0.1 gfx950"; }
+
+const char *hf_last_error(void) { return g_err.c_str(); }
+
+int hf_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int64_t hf_model_param_count(int in_dim, int hidden, int layers) {
+  if (in_dim <= 0 || hidden <= 0 || layers < 0) return -1;
+  return Layout(in_dim, hidden, layers).total;
+}
+
+int hf_model_create(const float *host_params, int in_dim, int hidden, int layers, int wdtype,
+                    hf_model_t *out) {
+  if (!out) return fail(HF_EINVAL, "hf_model_create: out is NULL");
+  *out = nullptr;
+  if (!host_params) return fail(HF_EINVAL, "hf_model_create: host_params is NULL");
+  if (in_dim <= 0 || hidden <= 0 || layers < 0)
+    return fail(HF_EINVAL, "hf_model_create: dimensions must be positive");
+  if (wdtype != HF_WDTYPE_F32)
+    return fail(HF_EUNSUPPORTED, "hf_model_create: only HF_WDTYPE_F32 is implemented in this build");
+  if (int rc = check_device()) return rc;
+
+  const Layout lay(in_dim, hidden, layers);
+  hf_model *m = new hf_model();
+  m->in_dim = in_dim;
+  m->hidden = hidden;
+  m->layers = layers;
+  m->wdtype = wdtype;
+  m->chain_ok = (in_dim == hf::kIn && hidden == hf::kH);
+
+  // natural copy (graph path) followed by the packed copy (chain path)
+  std::vector<float> packed;
+  int64_t o_win = 0, o_bin = 0, o_wl = 0, o_bl = 0, o_we = 0, o_be = 0, o_w2 = 0;
+  float b2 = 0.f;
+  if (m->chain_ok) pack_chain_f32(host_params, layers, packed, o_win, o_bin, o_wl, o_bl, o_we, o_be, o_w2, b2);
+  // natural layer weights are split into contiguous [L][H][2H] and [L][H]
+  std::vector<float> nat((size_t)lay.total);
+  {
+    int64_t o = 0;
+    auto put = [&](int64_t src, int64_t n) {
+      std::memcpy(nat.data() + o, host_params + src, sizeof(float) * n);
+      o += n;
+    };
+    put(lay.w_in, (int64_t)hidden * in_dim);
+    put(lay.b_in, hidden);
+    for (int l = 0; l < layers; ++l)
+      put(lay.w_l + (int64_t)l * ((int64_t)hidden * 2 * hidden + hidden), (int64_t)hidden * 2 * hidden);
+    for (int l = 0; l < layers; ++l)
+      put(lay.w_l + (int64_t)l * ((int64_t)hidden * 2 * hidden + hidden) + (int64_t)hidden * 2 * hidden,
+          hidden);
+    put(lay.w_e, (int64_t)hidden * 2 * hidden);
+    put(lay.b_e, hidden);
+    put(lay.w_2, hidden);
+    put(lay.b_2, 1);
+  }
+  const size_t nat_pad = (nat.size() + 63) & ~size_t(63);
+  const size_t bytes = sizeof(float) * (nat_pad + packed.size());
+  hipError_t e = hipMalloc(&m->dev, bytes);
+  if (e != hipSuccess) {
+    delete m;
+    return fail(HF_ENOMEM, std::string("hf_model_create: hipMalloc: ") + hipGetErrorString(e));
+  }
+  e = hipMemcpy(m->dev, nat.data(), sizeof(float) * nat.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !packed.empty())
+    e = hipMemcpy(m->dev + nat_pad, packed.data(), sizeof(float) * packed.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(m->dev);
+    delete m;
+    return fail_hip(e, "hf_model_create: upload");
+  }
+  {
+    const float *d = m->dev;
+    int64_t o = 0;
+    hf::GraphW &g = m->graph;
+    g.in_dim = in_dim;
+    g.hidden = hidden;
+    g.layers = layers;
+    g.w_in = d + o; o += (int64_t)hidden * in_dim;
+    g.b_in = d + o; o += hidden;
+    g.w_l = d + o; o += (int64_t)layers * hidden * 2 * hidden;
+    g.b_l = d + o; o += (int64_t)layers * hidden;
+    g.w_e = d + o; o += (int64_t)hidden * 2 * hidden;
+    g.b_e = d + o; o += hidden;
+    g.w_2 = d + o; o += hidden;
+    g.b_2 = d + o;
+  }
+  if (m->chain_ok) {
+    const float *d = m->dev + nat_pad;
+    hf::ChainW &c = m->chain;
+    c.win = d + o_win;
+    c.bin = d + o_bin;
+    c.wl = d + o_wl;
+    c.bl = d + o_bl;
+    c.we = d + o_we;
+    c.be = d + o_be;
+    c.w2 = d + o_w2;
+    c.b2 = b2;
+    c.layers = layers;
+  }
+  *out = m;
+  return HF_OK;
+}
+
+void hf_model_destroy(hf_model_t model) {
+  if (!model) return;
+  if (model->dev) (void)hipFree(model->dev);
+  delete model;
+}
+
+int hf_chain_flux(hf_model_t m, const float *nf, int B, int nx, float *fe, float *ff, void *stream) {
+  if (!m || !nf) return fail(HF_EINVAL, "hf_chain_flux: NULL model or node features");
+  if (B < 0 || nx < 1) return fail(HF_EINVAL, "hf_chain_flux: need B >= 0 and nx >= 1");
+  if (int rc = chain_usable(m)) return rc;
+  if (!fe && !ff) return HF_OK;
+  HF_CHECK_HIP(hf::launch_chain_flux(m->chain, nf, nullptr, 0, nullptr, B, nx, fe, ff, as_stream(stream)),
+               "hf_chain_flux");
+  return HF_OK;
+}
+
+int64_t hf_graph_workspace_bytes(hf_model_t m, int64_t N, int64_t E) {
+  if (!m || N < 0 || E < 0) return -1;
+  return hf::graph_workspace_bytes(m->graph, N, E);
+}
+
+int hf_graph_flux(hf_model_t m, const float *nf, int64_t N, const int64_t *ei, int64_t E,
+                  float *flux, void *ws, void *stream) {
+  if (!m) return fail(HF_EINVAL, "hf_graph_flux: NULL model");
+  if (N < 0 || E < 0) return fail(HF_EINVAL, "hf_graph_flux: negative size");
+  if (E == 0) return HF_OK;
+  if (N == 0) return fail(HF_EINVAL, "hf_graph_flux: edges without nodes");
+  if (!nf || !ei || !flux || !ws) return fail(HF_EINVAL, "hf_graph_flux: NULL pointer");
+  if (N > 0x7fffffffLL || E > 0x7fffffffLL) return fail(HF_EUNSUPPORTED, "hf_graph_flux: > 2^31 nodes/edges");
+  HF_CHECK_HIP(hf::launch_graph_flux(m->graph, nf, N, ei, E, flux, ws, as_stream(stream)), "hf_graph_flux");
+  return HF_OK;
+}
+
+int hf_poisson_coeffs(int nx, double length, double *c) {
+  if (nx < 1 || !(length > 0) || !c) return fail(HF_EINVAL, "hf_poisson_coeffs: bad argument");
+  // E = Re(ifft(i fft(rho)/k)), k_q = 2 pi q'/L over the signed fftfreq q'
+  // (src/baseline_solver.py:26).  Pairing +-q' gives
+  //   c[d] = -(L / (pi nx)) * sum_{q'=1}^{ceil(nx/2)-1} sin(2 pi q' d / nx) / q'
+  // and the Nyquist mode (even nx) contributes nothing to the real part.
+  const double pi = 3.14159265358979323846264338327950288;
+  const int qmax = (nx - 1) / 2;
+  for (int d = 0; d < nx; ++d) {
+    long double acc = 0.0L;
+    for (int q = 1; q <= qmax; ++q) {
+      const long long r = ((long long)q * d) % nx;
+      acc += sinl(2.0L * (long double)pi * (long double)r / (long double)nx) / (long double)q;
+    }
+    c[d] = (double)(-(long double)length / ((long double)pi * nx) * acc);
+  }
+  return HF_OK;
+}
+
+int hf_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B, int nx,
+               void *stream) {
+  if (!n || !E || !pc) return fail(HF_EINVAL, "hf_poisson: NULL pointer");
+  if (B < 0 || nx < 1 || ld_n < nx || ld_E < nx) return fail(HF_EINVAL, "hf_poisson: bad shape");
+  if (nx > 2 * kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_poisson: nx too large for the LDS solve");
+  HF_CHECK_HIP(hf::launch_poisson(n, ld_n, E, ld_E, pc, B, nx, as_stream(stream)), "hf_poisson");
+  return HF_OK;
+}
+
+int hf_step(hf_model_t m, const float *in, float *out, const float *x, const double *pc, int B, int nx,
+            float c, float dt, float nu, float dx2, float *ff, float *metrics, void *stream) {
+  if (!in || !out || !pc) return fail(HF_EINVAL, "hf_step: NULL state or Poisson coefficients");
+  if (in == out) return fail(HF_EINVAL, "hf_step: state_in and state_out must not alias");
+  if (B < 0 || nx < 1) return fail(HF_EINVAL, "hf_step: need B >= 0, nx >= 1");
+  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_step: nx too large for the LDS solve");
+  hipStream_t s = as_stream(stream);
+  if (B == 0) return HF_OK;
+  if (!m) {  // BaselineSolver.step
+    HF_CHECK_HIP(hf::launch_fv_step(in, 3LL * nx, out, 3LL * nx, nullptr, pc, B, nx, c, dt, nu, dx2, ff,
+                                    nx, metrics, HF_NUM_METRICS, s),
+                 "hf_step(classical)");
+    return HF_OK;
+  }
+  if (!x) return fail(HF_EINVAL, "hf_step: NULL x");
+  if (int rc = chain_usable(m)) return rc;
+  if (fused_nx(nx)) {
+    HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, in, out, x, pc, B, nx, 1, c, dt, nullptr, ff, nullptr, s),
+                 "hf_step(hybrid fused)");
+    if (metrics)
+      HF_CHECK_HIP(hf::launch_state_metrics(out, 3LL * nx, B, nx, metrics, HF_NUM_METRICS, s), "hf_step metrics");
+    return HF_OK;
+  }
+  float *F = ff;
+  if (!F) HF_CHECK_HIP(hipMallocAsync((void **)&F, sizeof(float) * (size_t)B * nx, s), "hf_step scratch");
+  hipError_t e = hf::launch_chain_flux(m->chain, nullptr, in, 3LL * nx, x, B, nx, nullptr, F, s);
+  if (e == hipSuccess)
+    e = hf::launch_fv_step(in, 3LL * nx, out, 3LL * nx, F, pc, B, nx, c, dt, nu, dx2, nullptr, nx, metrics,
+                           HF_NUM_METRICS, s);
+  if (!ff) (void)hipFreeAsync(F, s);
+  HF_CHECK_HIP(e, "hf_step(hybrid)");
+  return HF_OK;
+}
+
+int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B,
+           int nx, int T, float c, float dt, float nu, float dx2, float *traj, float *flux_traj,
+           float *metrics, void *stream) {
+  if (!state0 || !state_final || !pc) return fail(HF_EINVAL, "hf_run: NULL state or Poisson coefficients");
+  if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run: need B >= 0, nx >= 1, T >= 0");
+  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run: nx too large for the LDS solve");
+  if (m && !x) return fail(HF_EINVAL, "hf_run: NULL x");
+  if (m) {
+    if (int rc = chain_usable(m)) return rc;
+  }
+  hipStream_t s = as_stream(stream);
+  if (B == 0) return HF_OK;
+  const int64_t S = 3LL * nx;  // floats per state
+  if (m && fused_nx(nx)) {  // state0 may alias state_final: read whole before written
+    HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, state0, state_final, x, pc, B, nx, T, c, dt, traj,
+                                          flux_traj, metrics, s),
+                 "hf_run(hybrid fused)");
+    return HF_OK;
+  }
+  // Generic sequencing: [chain flux ->] FV+Poisson per step.
+  if (state0 == state_final && T > 0 && !traj)
+    return fail(HF_EINVAL, "hf_run: state0 and state_final may alias only in the fused path");
+  const int64_t ldT = (T + 1) * S, ldM = (int64_t)(T + 1) * HF_NUM_METRICS;
+  if (traj)
+    HF_CHECK_HIP(hipMemcpy2DAsync(traj, sizeof(float) * ldT, state0, sizeof(float) * S, sizeof(float) * S, B,
+                                  hipMemcpyDeviceToDevice, s),
+                 "hf_run traj[0]");
+  if (metrics) HF_CHECK_HIP(hf::launch_state_metrics(state0, S, B, nx, metrics, ldM, s), "hf_run metrics[0]");
+  if (T == 0) {
+    HF_CHECK_HIP(hipMemcpyAsync(state_final, state0, sizeof(float) * B * S, hipMemcpyDeviceToDevice, s),
+                 "hf_run copy");
+    return HF_OK;
+  }
+  float *scratch = nullptr, *F = nullptr;
+  if (!traj) HF_CHECK_HIP(hipMallocAsync((void **)&scratch, sizeof(float) * (size_t)B * S, s), "hf_run scratch");
+  if (m && hipMallocAsync((void **)&F, sizeof(float) * (size_t)B * nx, s) != hipSuccess) {
+    if (scratch) (void)hipFreeAsync(scratch, s);
+    return fail(HF_ENOMEM, "hf_run: face-flux scratch");
+  }
+  hipError_t e = hipSuccess;
+  const float *cur = state0;
+  int64_t ld_cur = S;
+  for (int t = 0; t < T && e == hipSuccess; ++t) {
+    float *dst;
+    int64_t ld_dst;
+    if (traj) {
+      dst = traj + (int64_t)(t + 1) * S;
+      ld_dst = ldT;
+    } else {
+      dst = ((T - 1 - t) % 2 == 0) ? state_final : scratch;
+      ld_dst = S;
+    }
+    if (m) e = hf::launch_chain_flux(m->chain, nullptr, cur, ld_cur, x, B, nx, nullptr, F, s);
+    if (e == hipSuccess)
+      e = hf::launch_fv_step(cur, ld_cur, dst, ld_dst, F, pc, B, nx, c, dt, nu, dx2,
+                             flux_traj ? flux_traj + (int64_t)t * nx : nullptr, (int64_t)T * nx,
+                             metrics ? metrics + (int64_t)(t + 1) * HF_NUM_METRICS : nullptr, ldM, s);
+    cur = dst;
+    ld_cur = ld_dst;
+  }
+  if (e == hipSuccess && traj)
+    e = hipMemcpy2DAsync(state_final, sizeof(float) * S, cur, sizeof(float) * ldT, sizeof(float) * S, B,
+                         hipMemcpyDeviceToDevice, s);
+  if (scratch) (void)hipFreeAsync(scratch, s);
+  if (F) (void)hipFreeAsync(F, s);
+  HF_CHECK_HIP(e, "hf_run");
+  return HF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,79 @@
+// Internal declarations shared by the HIP translation units of libhybridflux.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hybridflux.h"
+
+namespace hf {
+
+// Width of the fused chain kernels: MODEL_CONFIG (src/config.py:19-23) is
+// input_dim 4, hidden 128, 4 layers.  16x16x4 f32 MFMA tiles => 8 feature
+// tiles of 16 and 32 k-steps of 4 per 128-wide half of a [h ; agg] input.
+constexpr int kIn = 4;
+constexpr int kH = 128;
+constexpr int kNT = kH / 16;
+constexpr int kKS = kH / 4;
+
+// Window geometry of the halo-recompute chain kernel (any nx): a wave owns
+// 64 consecutive cells; L=4 layers + the 1-hop edge readout invalidate 4
+// cells at each window edge, so faces [4, 58] of the window are exact.
+constexpr int kWinCells = 64;
+constexpr int kWinHalo = 4;
+constexpr int kWinFaces = kWinCells - 2 * kWinHalo - 1;  // 55
+
+// Packed float32 weights (device) in MFMA A-fragment order; see capi.cpp
+// pack_chain_f32 for the exact index maps.
+struct ChainW {
+  const float *win;  // [64 lanes][kNT]             input layer A fragments
+  const float *bin;  // [kH]
+  const float *wl;   // [L][2*kKS][64][kNT]         update MLP A fragments
+  const float *bl;   // [L][kH]
+  const float *we;   // [kNT][kKS][64][2]           edge MLP (P,Q) A fragments
+  const float *be;   // [kH]
+  const float *w2;   // [kH]
+  float b2;
+  int layers;
+};
+
+// Natural-layout float32 weights (device) for the generic-graph path.
+struct GraphW {
+  const float *w_in, *b_in;        // [H][in], [H]
+  const float *w_l, *b_l;          // [L][H][2H], [L][H]
+  const float *w_e, *b_e;          // [H][2H], [H]
+  const float *w_2, *b_2;          // [H], [1]
+  int in_dim, hidden, layers;
+};
+
+// Chain flux.  Feature source: AoS node features [B*nx][4] (nf != nullptr)
+// or SoA state [B][3][nx] with IC stride ld_state floats + x[nx].
+hipError_t launch_chain_flux(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
+                             const float *x, int B, int nx, float *flux_edge, float *flux_face,
+                             hipStream_t s);
+
+// Persistent fused rollout for nx in {16,32,48,64}.
+hipError_t launch_chain_rollout(const ChainW &w, const float *state0, float *state_final,
+                                const float *x, const double *pc, int B, int nx, int T, float c,
+                                float dt, float *traj, float *flux_traj, float *metrics,
+                                hipStream_t s);
+
+// One FV + Poisson update (any nx).  face_flux != nullptr => hybrid update
+// with that F; nullptr => classical (F = n*u, viscosity).  IC strides in floats.
+hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld_out,
+                          const float *face_flux, const double *pc, int B, int nx, float c,
+                          float dt, float nu, float dx2, float *flux_out, int64_t ld_flux,
+                          float *metrics, int64_t ld_metrics, hipStream_t s);
+
+// Metrics of a state batch (used for t=0 of non-fused rollouts).
+hipError_t launch_state_metrics(const float *st, int64_t ld, int B, int nx, float *metrics,
+                                int64_t ld_metrics, hipStream_t s);
+
+hipError_t launch_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B,
+                          int nx, hipStream_t s);
+
+int64_t graph_workspace_bytes(const GraphW &w, int64_t N, int64_t E);
+hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei,
+                             int64_t E, float *flux, void *ws, hipStream_t s);
+
+}  // namespace hf

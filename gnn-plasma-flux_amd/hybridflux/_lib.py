@@ -1,0 +1,83 @@
+"""ctypes binding of libhybridflux.so (include/hybridflux.h).
+
+The shared library is built in-tree by `__graft_entry__.build()` (or `make -C
+gnn-plasma-flux_amd/csrc`).  There is deliberately no fallback: if the library
+is missing or no gfx950 device is visible, every compute call raises.
+"""
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_void_p
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libhybridflux.so")
+
+HF_OK = 0
+HF_EINVAL = -1
+HF_EUNSUPPORTED = -2
+HF_EHIP = -3
+HF_ENOMEM = -4
+HF_WDTYPE_F32 = 0
+HF_WDTYPE_BF16 = 1
+HF_NUM_METRICS = 4
+
+# name -> (restype, argtypes); mirrors include/hybridflux.h exactly.
+SIGNATURES = {
+    "hf_version": (c_char_p, []),
+    "hf_last_error": (c_char_p, []),
+    "hf_device_count": (c_int, []),
+    "hf_model_param_count": (c_int64, [c_int, c_int, c_int]),
+    "hf_model_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "hf_model_destroy": (None, [c_void_p]),
+    "hf_chain_flux": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "hf_graph_workspace_bytes": (c_int64, [c_void_p, c_int64, c_int64]),
+    "hf_graph_flux": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                              c_void_p]),
+    "hf_poisson_coeffs": (c_int, [c_int, c_double, c_void_p]),
+    "hf_poisson": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "hf_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                        c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    "hf_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                       c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+class HybridFluxError(RuntimeError):
+    """A libhybridflux call failed; carries the library's return code."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"libhybridflux error {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the .so is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is not built. Run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or `make -C gnn-plasma-flux_amd/csrc` (hipcc, gfx950). hybridflux has no CPU path.")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc):
+    if rc != HF_OK:
+        msg = lib().hf_last_error()
+        raise HybridFluxError(rc, msg.decode() if msg else "unknown error")
+    return rc
+
+
+def ptr(t):
+    """Device (or host) address of a tensor / ndarray, or None."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return c_void_p(t.data_ptr())
+    return t.ctypes.data_as(c_void_p)

@@ -1,0 +1,197 @@
+"""Device-side engine: owns the libhybridflux model handles and per-grid
+device constants, and launches the hot path on torch's current HIP stream.
+
+Everything here takes and returns torch tensors that already live on a HIP
+device; the reference-shaped numpy API (HybridSolver / BaselineSolver) sits
+on top of it.  Scalars follow the reference's rounding: the Python floats
+dt/dx, dt, nu and dx**2 are rounded to float32 once on the host, exactly as
+numpy does when it mixes them with float32 arrays (src/hybrid_solver.py:52,
+56-57; src/baseline_solver.py:86,91,94).
+"""
+import math
+from ctypes import c_void_p
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import HF_NUM_METRICS, check, lib, ptr
+
+PARAM_ORDER_DOC = "input_mlp.0.{weight,bias}, update_mlps.<l>.0.{weight,bias}, edge_mlp.0.*, edge_mlp.2.*"
+
+
+def require_device(t, what="tensor"):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise RuntimeError(
+            f"hybridflux: {what} must be a torch tensor on a HIP (cuda) device; this engine has no CPU "
+            f"path (got {type(t).__name__}{'' if not isinstance(t, torch.Tensor) else ' on ' + str(t.device)})")
+    return t
+
+
+def stream_of(device):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def flatten_params(sd, layers):
+    """Reference state dict (src/flux_gnn.py:17-38 keys) -> flat float32 array in
+    the order include/hybridflux.h documents for hf_model_create."""
+    def arr(k):
+        v = sd[k]
+        if isinstance(v, torch.Tensor):
+            v = v.detach().to("cpu", torch.float32).numpy()
+        return np.ascontiguousarray(np.asarray(v, dtype=np.float32)).reshape(-1)
+
+    parts = [arr("input_mlp.0.weight"), arr("input_mlp.0.bias")]
+    for l in range(layers):
+        parts += [arr(f"update_mlps.{l}.0.weight"), arr(f"update_mlps.{l}.0.bias")]
+    parts += [arr("edge_mlp.0.weight"), arr("edge_mlp.0.bias"), arr("edge_mlp.2.weight"), arr("edge_mlp.2.bias")]
+    return np.ascontiguousarray(np.concatenate(parts))
+
+
+def dims_of(sd):
+    w_in = sd["input_mlp.0.weight"]
+    hidden, in_dim = int(w_in.shape[0]), int(w_in.shape[1])
+    layers = sum(1 for k in sd if k.startswith("update_mlps.") and k.endswith(".0.weight"))
+    return in_dim, hidden, layers
+
+
+class DeviceModel:
+    """A packed, read-only copy of FluxGNN weights on one device (hf_model_t)."""
+
+    def __init__(self, state_dict, device):
+        self.in_dim, self.hidden, self.layers = dims_of(state_dict)
+        self.device = torch.device(device)
+        flat = flatten_params(state_dict, self.layers)
+        want = lib().hf_model_param_count(self.in_dim, self.hidden, self.layers)
+        if flat.size != want:
+            raise ValueError(f"state dict has {flat.size} parameters, expected {want}")
+        self.handle = c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().hf_model_create(flat.ctypes.data_as(c_void_p), self.in_dim, self.hidden,
+                                        self.layers, _lib.HF_WDTYPE_F32, self.handle))
+
+    @property
+    def chain_ok(self):
+        return self.in_dim == 4 and self.hidden == 128
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            lib().hf_model_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+
+class Grid:
+    """Geometry + time-step constants (src/baseline_solver.py:7-27) and their
+    device copies: cell centres x (float32) and the circulant Poisson column."""
+
+    def __init__(self, nx=64, length=2 * math.pi, dt=5e-3, nu=1e-3):
+        self.nx, self.length, self.dt, self.nu = int(nx), float(length), float(dt), float(nu)
+        self.dx = self.length / self.nx
+        self.x = np.linspace(0.5 * self.dx, self.length - 0.5 * self.dx, self.nx)
+        self.c32 = float(np.float32(self.dt / self.dx))
+        self.dt32 = float(np.float32(self.dt))
+        self.nu32 = float(np.float32(self.nu))
+        self.dx2_32 = float(np.float32(self.dx ** 2))
+        pc = np.empty(self.nx, dtype=np.float64)
+        check(lib().hf_poisson_coeffs(self.nx, self.length, pc.ctypes.data_as(c_void_p)))
+        self.poisson_c = pc
+        self._dev = {}
+
+    def on(self, device):
+        device = torch.device(device)
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = (torch.as_tensor(self.x.astype(np.float32), device=device),
+                              torch.as_tensor(self.poisson_c, device=device))
+        return self._dev[key]
+
+
+def _state(t, nx):
+    require_device(t, "state")
+    if t.dtype != torch.float32 or t.dim() != 3 or t.shape[1] != 3 or t.shape[2] != nx:
+        raise ValueError(f"state must be float32 [B,3,{nx}], got {tuple(t.shape)} {t.dtype}")
+    return t.contiguous()
+
+
+def step(model, grid, state, flux_face=False, metrics=False):
+    """One hybrid (model) or classical (model=None) step for state [B,3,nx]."""
+    state = _state(state, grid.nx)
+    B, dev = state.shape[0], state.device
+    out = torch.empty_like(state)
+    F = torch.empty(B, grid.nx, device=dev) if flux_face else None
+    M = torch.empty(B, HF_NUM_METRICS, device=dev) if metrics else None
+    x, pc = grid.on(dev)
+    with torch.cuda.device(dev):
+        check(lib().hf_step(model.handle if model else None, ptr(state), ptr(out), ptr(x), ptr(pc), B,
+                            grid.nx, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(F), ptr(M),
+                            stream_of(dev)))
+    return out, F, M
+
+
+def run(model, grid, state0, T, traj=True, flux=False, metrics=False, out=None):
+    """T-step rollout; returns dict(final, traj [B,T+1,3,nx], flux [B,T,nx], metrics [B,T+1,4])."""
+    state0 = _state(state0, grid.nx)
+    B, dev = state0.shape[0], state0.device
+    T = int(T)
+    final = torch.empty_like(state0) if out is None else out
+    tr = torch.empty(B, T + 1, 3, grid.nx, device=dev) if traj else None
+    fl = torch.empty(B, T, grid.nx, device=dev) if flux else None
+    me = torch.empty(B, T + 1, HF_NUM_METRICS, device=dev) if metrics else None
+    x, pc = grid.on(dev)
+    with torch.cuda.device(dev):
+        check(lib().hf_run(model.handle if model else None, ptr(state0), ptr(final), ptr(x), ptr(pc), B,
+                           grid.nx, T, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(tr), ptr(fl),
+                           ptr(me), stream_of(dev)))
+    return {"final": final, "traj": tr, "flux": fl, "metrics": me}
+
+
+def chain_flux(model, node_features, B, nx):
+    """FluxGNN.forward on B disjoint periodic chains of nx cells -> [B*2nx]."""
+    require_device(node_features, "node_features")
+    nf = node_features.contiguous()
+    if nf.dtype != torch.float32 or nf.shape != (B * nx, 4):
+        raise ValueError(f"node_features must be float32 [{B * nx},4], got {tuple(nf.shape)} {nf.dtype}")
+    fe = torch.empty(B * 2 * nx, device=nf.device)
+    with torch.cuda.device(nf.device):
+        check(lib().hf_chain_flux(model.handle, ptr(nf), B, nx, ptr(fe), None, stream_of(nf.device)))
+    return fe
+
+
+def graph_flux(model, node_features, edge_index):
+    """FluxGNN.forward on an arbitrary graph (generic path) -> [E]."""
+    require_device(node_features, "node_features")
+    nf = node_features.to(torch.float32).contiguous()
+    ei = edge_index.to(device=nf.device, dtype=torch.int64).contiguous()
+    N, E = nf.shape[0], ei.shape[1]
+    if nf.dim() != 2 or nf.shape[1] != model.in_dim:
+        raise ValueError(f"node_features must be [N,{model.in_dim}], got {tuple(nf.shape)}")
+    flux = torch.empty(E, device=nf.device)
+    if E == 0:
+        return flux
+    lo, hi = int(ei.min()), int(ei.max())  # reference raises IndexError on these too
+    if lo < 0 or hi >= N:
+        raise IndexError(f"edge_index entries must lie in [0, {N}), got [{lo}, {hi}]")
+    ws = torch.empty(int(lib().hf_graph_workspace_bytes(model.handle, N, E)), dtype=torch.uint8,
+                     device=nf.device)
+    with torch.cuda.device(nf.device):
+        check(lib().hf_graph_flux(model.handle, ptr(nf), N, ptr(ei), E, ptr(flux), ptr(ws),
+                                  stream_of(nf.device)))
+    return flux
+
+
+def poisson(grid, n):
+    """Spectral Poisson E for densities n [B,nx] (src/baseline_solver.py:59-68)."""
+    require_device(n, "n")
+    n = n.to(torch.float32).contiguous()
+    B = n.shape[0]
+    E = torch.empty_like(n)
+    _, pc = grid.on(n.device)
+    with torch.cuda.device(n.device):
+        check(lib().hf_poisson(ptr(n), grid.nx, ptr(E), grid.nx, ptr(pc), B, grid.nx, stream_of(n.device)))
+    return E

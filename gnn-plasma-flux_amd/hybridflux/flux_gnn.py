@@ -1,0 +1,101 @@
+"""FluxGNN with the reference's module tree and forward signature
+(src/flux_gnn.py:6-67), executed by the MI355X kernels of libhybridflux.
+
+The nn.Module layout (input_mlp / update_mlps / edge_mlp Sequentials) is kept
+so reference checkpoints load with `load_state_dict` unchanged.  forward()
+never runs these Linear layers itself: the parameters are packed (once per
+change) into a device weight handle and the edge fluxes come from
+  * the fused chain kernel (chain_gnn.hip) when edge_index is a periodic chain
+    — tagged by graph_constructor, or recognised by content — and the model
+    has MODEL_CONFIG's width (in 4, hidden 128);
+  * the generic-graph kernels (graph.hip) for any other edge_index
+    (examples/smoke_test.py:53 passes a random one) or width.
+There is no CPU path: CPU inputs raise.  Backward kernels are not part of this
+engine yet, so autograd through forward() raises at backward time.
+"""
+import torch
+import torch.nn as nn
+
+from . import engine
+from .graph_constructor import chain_edge_index, chain_tag
+
+
+class _NoBackward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flux, *params):
+        return flux.view_as(flux)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError(
+            "hybridflux FluxGNN has no backward kernels yet (differentiable hybrid step is the next "
+            "component, SURVEY.md 8f rank 2); train with the reference trainer and load the state dict")
+
+
+class FluxGNN(nn.Module):
+    """Message-passing GNN predicting one flux per directed edge."""
+
+    def __init__(self, input_dim=2, hidden_dim=32, num_layers=2):
+        super().__init__()
+        self.input_dim = input_dim
+        self.hidden_dim = hidden_dim
+        self.num_layers = num_layers
+        self.input_mlp = nn.Sequential(nn.Linear(input_dim, hidden_dim), nn.ReLU())
+        self.update_mlps = nn.ModuleList(
+            [nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU()) for _ in range(num_layers)])
+        self.edge_mlp = nn.Sequential(nn.Linear(2 * hidden_dim, hidden_dim), nn.ReLU(),
+                                      nn.Linear(hidden_dim, 1))
+        self._packed = {}
+
+    # -- weights -------------------------------------------------------------
+    def _signature(self):
+        return tuple((p.data_ptr(), p._version, str(p.device)) for p in self.parameters())
+
+    def device_model(self, device):
+        """The packed libhybridflux weight handle for `device` (rebuilt when any
+        parameter changes)."""
+        device = torch.device(device)
+        key = str(device)
+        sig = self._signature()
+        hit = self._packed.get(key)
+        if hit is None or hit[0] != sig:
+            if hit is not None:
+                hit[1].close()
+            sd = {k: v for k, v in self.state_dict().items()}
+            self._packed[key] = (sig, engine.DeviceModel(sd, device))
+        return self._packed[key][1]
+
+    def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate packed copies
+        out = super()._apply(fn, *args, **kwargs)
+        for _, (_, dm) in list(self._packed.items()):
+            dm.close()
+        self._packed = {}
+        return out
+
+    # -- forward -------------------------------------------------------------
+    @staticmethod
+    def _chain_geometry(node_features, edge_index):
+        N = node_features.shape[0]
+        tag = chain_tag(edge_index)
+        if tag is not None:
+            B, nx = tag
+            return (B, nx) if B * nx == N else None
+        if edge_index.dim() == 2 and edge_index.shape[0] == 2 and edge_index.shape[1] == 2 * N and N > 0:
+            ref = chain_edge_index(N, 1, edge_index.device)
+            if torch.equal(edge_index.to(torch.long), ref):
+                return 1, N
+        return None
+
+    def forward(self, node_features, edge_index):
+        """node_features [N, input_dim] float32, edge_index [2, E] int64 -> flux [E]."""
+        engine.require_device(node_features, "node_features")
+        dm = self.device_model(node_features.device)
+        geom = self._chain_geometry(node_features, edge_index)
+        if geom is not None and dm.chain_ok:
+            flux = engine.chain_flux(dm, node_features.to(torch.float32), geom[0], geom[1])
+        else:
+            flux = engine.graph_flux(dm, node_features, edge_index)
+        if torch.is_grad_enabled() and (node_features.requires_grad or
+                                        any(p.requires_grad for p in self.parameters())):
+            return _NoBackward.apply(flux, *[p for p in self.parameters() if p.requires_grad])
+        return flux

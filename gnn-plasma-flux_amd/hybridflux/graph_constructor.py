@@ -1,0 +1,71 @@
+"""Chain-graph construction with the reference's API (src/graph_constructor.py:6-39).
+
+The MI355X kernels never materialise this graph — the chain's +-1 neighbours
+are lane shifts inside chain_gnn.hip — but FluxGNN.forward keeps the
+(node_features, edge_index) signature, so these builders produce exactly the
+reference tensors and TAG the edge index so FluxGNN can dispatch to the chain
+kernel without inspecting its contents.
+"""
+import numpy as np
+import torch
+
+CHAIN_TAG = "_hf_chain"
+
+
+def chain_edge_index(nx, batch=1, device=None):
+    """Edge list of `batch` disjoint periodic chains of nx cells.  Per IC b the
+    2*nx edges are (i -> i+1) for i < nx, then (i+1 -> i) — the order of
+    src/graph_constructor.py:34-38 — offset by b*nx nodes."""
+    src = torch.arange(nx, dtype=torch.long, device=device)
+    dst = (src + 1) % nx
+    row = torch.cat([src, dst])
+    col = torch.cat([dst, src])
+    if batch > 1:
+        off = (torch.arange(batch, dtype=torch.long, device=device) * nx).unsqueeze(1)
+        row = (row.unsqueeze(0) + off).reshape(-1)
+        col = (col.unsqueeze(0) + off).reshape(-1)
+    ei = torch.stack([row, col])
+    tag_chain(ei, batch, nx)
+    return ei
+
+
+def tag_chain(edge_index, batch, nx):
+    setattr(edge_index, CHAIN_TAG, (int(batch), int(nx), edge_index._version))
+    return edge_index
+
+
+def chain_tag(edge_index):
+    """(batch, nx) if edge_index is an unmodified tagged chain, else None."""
+    tag = getattr(edge_index, CHAIN_TAG, None)
+    if tag is None or tag[2] != edge_index._version:
+        return None
+    return tag[0], tag[1]
+
+
+def build_chain_graph(full_state, x, device=None):
+    """full_state [3,nx] (numpy or torch: n,u,E), x [nx] ->
+    node_features [nx,4] float32 (n,u,E,x) and edge_index [2,2nx] int64."""
+    if isinstance(full_state, np.ndarray):
+        n, u, E = (torch.from_numpy(full_state[i].astype(np.float32)) for i in range(3))
+    else:
+        n, u, E = full_state[0], full_state[1], full_state[2]
+    if device is None:
+        device = n.device
+    else:
+        n, u, E = n.to(device), u.to(device), E.to(device)
+    x_t = torch.as_tensor(x, dtype=torch.float32, device=device)
+    node_features = torch.stack([n, u, E, x_t], dim=-1)
+    return node_features, chain_edge_index(n.shape[0], 1, device)
+
+
+def build_chain_graph_batch(states, x, device=None):
+    """Batched form: states [B,3,nx] -> node_features [B*nx,4], edge_index [2,B*2nx]
+    (IC b owns nodes b*nx.. and edges b*2nx..)."""
+    if isinstance(states, np.ndarray):
+        states = torch.from_numpy(np.ascontiguousarray(states, dtype=np.float32))
+    if device is not None:
+        states = states.to(device)
+    B, _, nx = states.shape
+    x_t = torch.as_tensor(x, dtype=torch.float32, device=states.device).expand(B, nx)
+    nf = torch.stack([states[:, 0], states[:, 1], states[:, 2], x_t], dim=-1).reshape(B * nx, 4)
+    return nf, chain_edge_index(nx, B, states.device)

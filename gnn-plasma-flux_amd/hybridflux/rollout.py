@@ -1,0 +1,57 @@
+"""Multi-GPU batched rollout: independent initial conditions sharded across
+ranks (one process per GPU), zero communication while stepping, and ONE
+collective at the end — an all_gather of the per-IC rollout metrics over
+RCCL/xGMI (backend "nccl" on ROCm), or gloo on CPU for tests.
+
+This is the reference's multi-IC evaluation loop
+(scripts/evaluation/evaluate_multi_ic.py:106-138: seeds 1000.., one IC at a
+time) turned into a data-parallel job: IC j of rank r is seed
+`seed0 + start(r) + j`, so the union over ranks is the same seed range at any
+world size.  A 64-cell chain never shards spatially (BASELINE.json north star).
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n_total, world, rank):
+    """Contiguous [start, stop) of IC indices owned by `rank`; ragged totals
+    give the first n_total % world ranks one extra IC."""
+    base, rem = divmod(int(n_total), int(world))
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def shard_seeds(seed0, n_total, world, rank):
+    a, b = shard_bounds(n_total, world, rank)
+    return list(range(seed0 + a, seed0 + b))
+
+
+def gather_ic_rows(local, n_total, group=None):
+    """all_gather a per-IC tensor [b_local, ...] into [n_total, ...] on every
+    rank (ragged shards are padded to the largest shard for the collective)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return local
+    rank = dist.get_rank(group)
+    counts = [shard_bounds(n_total, world, r)[1] - shard_bounds(n_total, world, r)[0] for r in range(world)]
+    assert local.shape[0] == counts[rank], (local.shape, counts)
+    cap = max(counts)
+    pad = local.new_zeros((cap,) + tuple(local.shape[1:]))
+    pad[: local.shape[0]] = local
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad.contiguous(), group=group)
+    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+
+
+def sharded_rollout(run_local, make_ics, seed0, n_total, T, group=None):
+    """Run this rank's shard and gather every IC's metrics.
+
+    run_local(ics, T) -> dict with 'metrics' [b, T+1, K] (device tensor) and 'final'.
+    make_ics(seeds) -> [b, 3, nx] states for those seeds.
+    Returns (local_result, global_metrics [n_total, T+1, K]).
+    """
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    ics = make_ics(shard_seeds(seed0, n_total, world, rank))
+    res = run_local(ics, T)
+    return res, gather_ic_rows(res["metrics"], n_total, group)

@@ -1,0 +1,154 @@
+/*
+ * hybridflux.h — C ABI of the MI355X hybrid-rollout engine (libhybridflux.so).
+ *
+ * Drop-in boundary for the hot path of shanedirksen/gnn-plasma-flux: the
+ * per-timestep loop  FluxGNN message passing on the periodic 1-D chain
+ * -> flux symmetrisation -> finite-volume continuity + Burgers update ->
+ * spectral Poisson solve.  The reference has no FFI of its own (it is pure
+ * Python); each entry point below names the reference function it replaces
+ * (paths relative to the reference root).  The Python host layer
+ * (gnn-plasma-flux_amd/hybridflux) binds these through ctypes; INTEGRATION.md
+ * shows the binding.
+ *
+ * Conventions
+ *  - Every pointer named dev_* is a device (HBM) pointer; host_* are host.
+ *  - Layouts: state [B][3][nx] float32 (n,u,E per IC, channel-major, the
+ *    reference's [3,nx] per IC); node features [N][in_dim] float32 (AoS, as
+ *    FluxGNN.forward receives them); edge fluxes [B][2*nx] in the reference
+ *    edge order (edges i->i+1 first, then i+1->i).
+ *  - Work is enqueued on `stream` (a hipStream_t, NULL = default stream) and
+ *    is asynchronous: nothing here synchronises the host.
+ *  - Return 0 on success, a negative HF_E* code on failure; the message is
+ *    available from hf_last_error() (thread-local).  Nothing throws across
+ *    the ABI.  There is NO CPU fallback: without a usable gfx950 device every
+ *    compute entry point fails with HF_EHIP.
+ *  - Ownership: the caller owns every state/flux/trajectory/metric buffer.
+ *    A model handle owns only its packed, read-only device weights, so
+ *    concurrent calls on one handle from different streams are safe.
+ */
+#ifndef HYBRIDFLUX_H
+#define HYBRIDFLUX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HF_OK 0
+#define HF_EINVAL (-1)      /* bad argument (shape, NULL pointer, size)        */
+#define HF_EUNSUPPORTED (-2)/* configuration this build does not implement    */
+#define HF_EHIP (-3)        /* HIP runtime error (no device, launch failure)  */
+#define HF_ENOMEM (-4)      /* device allocation failed                       */
+
+#define HF_WDTYPE_F32 0     /* weights and arithmetic in float32 (parity mode) */
+#define HF_WDTYPE_BF16 1    /* bf16 MLP weights/activations, f32 accumulate    */
+
+/* Number of per-(IC, step) rollout metrics written by hf_run / hf_fv_step:
+ * [0] energy 0.5*mean(u^2+E^2)  [1] charge mean(n)  [2] 1.0 if every state
+ * value is finite else 0.0  [3] max |n-1| over the chain.
+ * (scripts/evaluation/evaluate_all.py:324-334, evaluate_long_rollout.py:331) */
+#define HF_NUM_METRICS 4
+
+typedef struct hf_model *hf_model_t;
+
+/* Library version string, e.g. "hybridflux 0.1 gfx950". */
+const char *hf_version(void);
+
+/* Thread-local message describing the last failure on this thread. */
+const char *hf_last_error(void);
+
+/* Number of visible HIP devices (0 when none); never fails. */
+int hf_device_count(void);
+
+/*
+ * Replaces: FluxGNN.__init__ + load_state_dict (src/flux_gnn.py:11-38,
+ * src/hybrid_solver.py:22-28).
+ * host_params: every parameter of the reference state dict, float32,
+ * concatenated in this order (row-major, shapes as nn.Linear stores them):
+ *   input_mlp.0.weight [H][in_dim], input_mlp.0.bias [H],
+ *   for l in 0..layers-1: update_mlps.l.0.weight [H][2H], update_mlps.l.0.bias [H],
+ *   edge_mlp.0.weight [H][2H], edge_mlp.0.bias [H],
+ *   edge_mlp.2.weight [1][H], edge_mlp.2.bias [1].
+ * The handle packs them into the MFMA fragment order of the fused chain
+ * kernels (when in_dim==4 && H==128) and keeps the natural layout for the
+ * generic-graph path.  wdtype: HF_WDTYPE_F32 or HF_WDTYPE_BF16.
+ */
+int hf_model_create(const float *host_params, int in_dim, int hidden, int layers,
+                    int wdtype, hf_model_t *out);
+void hf_model_destroy(hf_model_t model);
+/* Total float count host_params must hold for these dimensions. */
+int64_t hf_model_param_count(int in_dim, int hidden, int layers);
+
+/*
+ * Replaces: FluxGNN.forward (src/flux_gnn.py:40-67) applied to the batched
+ * chain graph of build_chain_graph (src/graph_constructor.py:6-39).
+ * dev_node_features [B*nx][4]; dev_flux_edge [B][2nx] (may be NULL);
+ * dev_flux_face [B][nx] = 0.5*(edge i + edge nx+i) (may be NULL;
+ * src/hybrid_solver.py:45-48).  Any nx >= 1.
+ */
+int hf_chain_flux(hf_model_t model, const float *dev_node_features, int B, int nx,
+                  float *dev_flux_edge, float *dev_flux_face, void *stream);
+
+/*
+ * Replaces: FluxGNN.forward on an ARBITRARY graph (examples/smoke_test.py:45-56
+ * calls it with a random edge_index).  dev_edge_index [2][E] int64.
+ * dev_workspace must hold hf_graph_workspace_bytes(model, N, E) bytes.
+ */
+int64_t hf_graph_workspace_bytes(hf_model_t model, int64_t N, int64_t E);
+int hf_graph_flux(hf_model_t model, const float *dev_node_features, int64_t N,
+                  const int64_t *dev_edge_index, int64_t E, float *dev_flux,
+                  void *dev_workspace, void *stream);
+
+/*
+ * Host helper (no device work): first column c[0..nx) of the real circulant
+ * matrix equal to the reference's spectral Poisson operator
+ * E = Re(ifft(1j*fft(n-1)/k)), k=0 mode zeroed (src/baseline_solver.py:26,59-68):
+ * E[i] = sum_j c[(i-j) mod nx] * (n[j]-1).  Computed in float64.
+ */
+int hf_poisson_coeffs(int nx, double length, double *host_c);
+
+/* Replaces: BaselineSolver.solve_poisson (src/baseline_solver.py:59-68), batched.
+ * dev_n, dev_E: [B][nx] float32 (row stride ld_n / ld_E floats);
+ * dev_c: device copy of hf_poisson_coeffs. */
+int hf_poisson(const float *dev_n, int ld_n, float *dev_E, int ld_E,
+               const double *dev_c, int B, int nx, void *stream);
+
+/*
+ * One timestep for B ICs (state_in -> state_out, may not alias).
+ * model != NULL: HybridSolver.step (src/hybrid_solver.py:34-64):
+ *   GNN flux -> symmetrise -> FV continuity -> Burgers u (no viscosity) -> Poisson.
+ * model == NULL: BaselineSolver.step (src/baseline_solver.py:80-101):
+ *   F=n*u -> FV continuity -> Burgers u + dt*(E + nu*lap u) -> Poisson.
+ * Scalars are the reference's Python floats rounded to float32 on the host:
+ *   c = f32(dt/dx), dt = f32(dt), nu = f32(nu), dx2 = f32(dx*dx).
+ * dev_x [nx]: float32 cell centres (node feature x); dev_c: Poisson coeffs.
+ * dev_flux_face [B][nx] (may be NULL): the F used this step (F_n classically).
+ * dev_metrics [B][HF_NUM_METRICS] (may be NULL) for state_out.
+ */
+int hf_step(hf_model_t model, const float *dev_state_in, float *dev_state_out,
+            const float *dev_x, const double *dev_c, int B, int nx,
+            float c, float dt, float nu, float dx2,
+            float *dev_flux_face, float *dev_metrics, void *stream);
+
+/*
+ * T-step rollout (HybridSolver.run src/hybrid_solver.py:66-73 when model !=
+ * NULL, BaselineSolver.run src/baseline_solver.py:103-118 when NULL), batched.
+ * dev_state0 [B][3][nx] -> dev_state_final [B][3][nx].
+ * dev_traj [B][T+1][3][nx] (may be NULL) receives every state incl. t=0.
+ * dev_flux_traj [B][T][nx] (may be NULL) receives the face flux of each step
+ *   (the classical run's `fluxes`).
+ * dev_metrics [B][T+1][HF_NUM_METRICS] (may be NULL).
+ * For nx in {16,32,48,64} with model != NULL the whole rollout is ONE
+ * persistent kernel (state resident on-chip across steps).
+ */
+int hf_run(hf_model_t model, const float *dev_state0, float *dev_state_final,
+           const float *dev_x, const double *dev_c, int B, int nx, int T,
+           float c, float dt, float nu, float dx2,
+           float *dev_traj, float *dev_flux_traj, float *dev_metrics, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HYBRIDFLUX_H */

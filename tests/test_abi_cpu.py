@@ -1,0 +1,77 @@
+"""CPU-side checks of the C ABI: the library loads, exports every entry point
+include/hybridflux.h declares, and its host-only helpers are correct.  No
+kernel is launched here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+from hybridflux import _lib
+
+HEADER = os.path.join(ROOT, "include", "hybridflux.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(hf_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 12
+    lib = _lib.lib()
+    for n in names:
+        assert hasattr(lib, n), f"libhybridflux.so does not export {n}"
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
+
+
+def test_version_and_codes():
+    lib = _lib.lib()
+    assert b"gfx950" in lib.hf_version()
+    text = open(HEADER).read()
+    for name in ("HF_OK", "HF_EINVAL", "HF_EUNSUPPORTED", "HF_EHIP", "HF_ENOMEM", "HF_NUM_METRICS"):
+        val = int(re.search(rf"#define {name} \(?(-?\d+)\)?", text).group(1))
+        assert getattr(_lib, name) == val
+
+
+def test_param_count_matches_reference_model():
+    lib = _lib.lib()
+    w = golden("weights_W0.npz")
+    assert lib.hf_model_param_count(4, 128, 4) == sum(w[k].size for k in w.files) == 165249
+    assert lib.hf_model_param_count(4, 64, 3) == 4 * 64 + 64 + 3 * (64 * 128 + 64) + 64 * 128 + 64 + 64 + 1
+    assert lib.hf_model_param_count(0, 64, 3) == -1
+
+
+@pytest.mark.parametrize("nx", [16, 32, 48, 64, 1024])
+def test_poisson_coefficients_reproduce_spectral_solve(nx):
+    """The circulant column from hf_poisson_coeffs applied in float64 equals the
+    reference FFT solve (src/baseline_solver.py:59-68) to < 1e-7."""
+    lib = _lib.lib()
+    c = np.empty(nx)
+    _lib.check(lib.hf_poisson_coeffs(nx, 2 * np.pi, c.ctypes.data_as(ctypes.c_void_p)))
+    g = golden("poisson.npz")
+    rho = g[f"n_nx{nx}"].astype(np.float64) - 1.0
+    idx = (np.arange(nx)[:, None] - np.arange(nx)[None, :]) % nx
+    E = (rho @ c[idx].T).astype(np.float32)
+    assert np.abs(E - g[f"E_nx{nx}"]).max() < 1e-7
+
+
+def test_poisson_coefficients_errors():
+    lib = _lib.lib()
+    c = np.empty(4)
+    assert lib.hf_poisson_coeffs(0, 1.0, c.ctypes.data_as(ctypes.c_void_p)) == _lib.HF_EINVAL
+    assert b"hf_poisson_coeffs" in lib.hf_last_error()
+
+
+def test_no_device_fails_loudly():
+    lib = _lib.lib()
+    if lib.hf_device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    w = np.zeros(lib.hf_model_param_count(4, 128, 4), dtype=np.float32)
+    h = ctypes.c_void_p()
+    rc = lib.hf_model_create(w.ctypes.data_as(ctypes.c_void_p), 4, 128, 4, 0, ctypes.byref(h))
+    assert rc == _lib.HF_EHIP and b"no CPU path" in lib.hf_last_error()

@@ -1,0 +1,272 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden vectors of
+the reference and against the CPU oracle on the same seeded inputs.
+
+Tolerances (float32 everywhere; the kernels sum in a different order than
+the CPU BLAS, which the reference itself differs from fp64 by ~4e-7):
+  edge / face fluxes, one evaluation ............ atol 2e-6
+  Poisson E ..................................... atol 1e-7
+  classical FV update (n, u), one step ........... bit-exact
+  states after a 30-step rollout ................. atol 1e-5 + rtol 1e-5
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import hybrid_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FLUX_ATOL = 2e-6
+E_ATOL = 1e-7
+ROLL_ATOL, ROLL_RTOL = 1e-5, 1e-5
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def hf():
+    import hybridflux
+    from hybridflux import _lib
+    assert _lib.lib().hf_device_count() > 0, "GPU tests need a visible HIP device"
+    return hybridflux
+
+
+def weights(name):
+    return dict(golden(f"weights_{name}.npz"))
+
+
+def model(hf, name):
+    m = hf.FluxGNN(4, 128, 4)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in weights(name).items()})
+    return m.to(DEV).eval()
+
+
+def close(a, b, atol, rtol=0.0):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = np.abs(a.astype(np.float64) - b)
+    lim = atol + rtol * np.abs(b)
+    assert np.isfinite(a).all()
+    assert (err <= lim).all(), f"max err {err.max():.3e} (limit {atol:.1e}+{rtol:.1e}|ref|)"
+
+
+# ------------------------------------------------------------------- FluxGNN
+@pytest.mark.parametrize("w", ["W0", "W1_r1", "W1_r2", "W1_r3"])
+def test_chain_flux_vs_reference_every_step(hf, w):
+    """Edge fluxes at every state of the reference's own 30-step trajectories."""
+    h = golden(f"hybrid_{w}_nx64.npz")
+    states = h["states"][:, :30]                     # [16, 30, 3, 64] inputs
+    B = states.shape[0] * states.shape[1]
+    m = model(hf, w)
+    x = hf.BaselineSolver(64, device=DEV).x
+    nf, ei = hf.build_chain_graph_batch(states.reshape(B, 3, 64), x, DEV)
+    with torch.no_grad():
+        fe = m(nf, ei).cpu().numpy().reshape(16, 30, 128)
+    close(fe, h["flux_edge"], FLUX_ATOL)
+
+
+def test_chain_flux_untagged_single_chain(hf):
+    """A plain reference-style call: build the edge_index by hand (no tag)."""
+    h = golden("hybrid_W1_r1_nx64.npz")
+    m = model(hf, "W1_r1")
+    x = hf.BaselineSolver(64, device=DEV).x
+    st = h["states"][3, 7]
+    nf = torch.as_tensor(np.stack([st[0], st[1], st[2], x.astype(np.float32)], -1), device=DEV)
+    ei = O.chain_edges(64, 1).to(DEV)
+    with torch.no_grad():
+        fe = m(nf, ei).cpu().numpy()
+    close(fe, h["flux_edge"][3, 7], FLUX_ATOL)
+
+
+def test_generic_graph_path_vs_reference(hf):
+    g = golden("fluxgnn_random.npz")
+    small = hf.FluxGNN(4, 64, 3)
+    small.load_state_dict({k[6:]: torch.from_numpy(g[k]) for k in g.files if k.startswith("small.")})
+    small = small.to(DEV)
+    with torch.no_grad():
+        f = small(torch.as_tensor(g["small_nf"], device=DEV), torch.as_tensor(g["small_ei"], device=DEV))
+    assert f.shape == (128,)                        # examples/smoke_test.py:55-56
+    close(f.cpu().numpy(), g["small_flux"], 2e-6, 1e-5)
+    big = model(hf, "W0")
+    with torch.no_grad():
+        f = big(torch.as_tensor(g["big_nf"], device=DEV), torch.as_tensor(g["big_ei"], device=DEV))
+    close(f.cpu().numpy(), g["big_flux"], 2e-6, 1e-5)
+
+
+def test_generic_graph_isolated_nodes_and_bad_index(hf):
+    m = hf.FluxGNN(4, 32, 2).to(DEV)
+    p = O.params_from({k: v.cpu() for k, v in m.state_dict().items()})
+    nf = torch.randn(10, 4, generator=torch.Generator().manual_seed(3))
+    ei = torch.tensor([[0, 0, 0, 5, 5], [1, 2, 9, 0, 0]])   # nodes 1-4, 6-9 receive nothing
+    want = O.flux_gnn_forward(p, nf, ei).detach().numpy()
+    with torch.no_grad():
+        got = m(nf.to(DEV), ei.to(DEV)).cpu().numpy()
+    close(got, want, 2e-6, 1e-5)
+    with pytest.raises(IndexError):
+        m(nf.to(DEV), torch.tensor([[0, 11], [1, 2]], device=DEV))
+
+
+def test_forward_autograd_is_loud(hf):
+    m = model(hf, "W0")
+    nf, ei = hf.build_chain_graph(golden("ics.npz")["ics_nx64"][0], np.linspace(0, 1, 64), DEV)
+    out = m(nf, ei)                                  # grad enabled: forward works
+    assert out.requires_grad and out.shape == (128,)
+    with pytest.raises(NotImplementedError):
+        out.sum().backward()
+
+
+# ------------------------------------------------------------------- Poisson
+@pytest.mark.parametrize("nx", [16, 32, 48, 64, 1024])
+def test_poisson_vs_reference(hf, nx):
+    g = golden("poisson.npz")
+    s = hf.BaselineSolver(nx, device=DEV)
+    close(s.solve_poisson(g[f"n_nx{nx}"]), g[f"E_nx{nx}"], E_ATOL)
+
+
+def test_initial_conditions_vs_reference(hf):
+    g = golden("ics.npz")
+    s = hf.BaselineSolver(64, device=DEV)
+    ics = s.initial_conditions([int(v) for v in g["seeds_nx64"]])
+    assert np.array_equal(ics[:, :2], g["ics_nx64"][:, :2])     # host RNG modes: bit-exact
+    close(ics[:, 2], g["ics_nx64"][:, 2], E_ATOL)
+
+
+# ------------------------------------------------------------------- classical
+def test_classical_step_bitwise_fv(hf):
+    g = golden("classical.npz")
+    s = hf.BaselineSolver(64, device=DEV)
+    st = g["b16_states"]
+    out, F, _ = s.step_batch(st[:, 0], return_flux=True)
+    out = out.cpu().numpy()
+    assert np.array_equal(out[:, :2], st[:, 1, :2])      # n, u: identical float32 ops
+    assert np.array_equal(F.cpu().numpy(), g["b16_fluxes"][:, 0])
+    close(out[:, 2], st[:, 1, 2], E_ATOL)
+
+
+def test_classical_run_vs_reference(hf):
+    g = golden("classical.npz")
+    s = hf.BaselineSolver(64, device=DEV)
+    states, fluxes = s.run(g["seed0_states"][0], n_steps=30)    # config 1 path
+    close(states, g["seed0_states"], ROLL_ATOL, ROLL_RTOL)
+    close(fluxes, g["seed0_fluxes"], ROLL_ATOL, ROLL_RTOL)
+    r = s.run_batch(g["b16_states"][:, 0], 30, flux=True)
+    close(r["traj"].cpu().numpy(), g["b16_states"], ROLL_ATOL, ROLL_RTOL)
+    s1k = hf.BaselineSolver(1024, dt=3.125e-4, device=DEV)
+    r = s1k.run_batch(g["nx1024_states"][:, 0], 30)
+    close(r["traj"].cpu().numpy(), g["nx1024_states"], ROLL_ATOL, ROLL_RTOL)
+
+
+# ------------------------------------------------------------------- hybrid
+@pytest.mark.parametrize("w", ["W0", "W1_r1", "W1_r2", "W1_r3"])
+def test_hybrid_rollout_vs_reference(hf, w):
+    h = golden(f"hybrid_{w}_nx64.npz")
+    r = int(w[-1]) if w != "W0" else 1
+    solver = hf.HybridSolver(weights(w), radius=r, device=DEV)
+    out = solver.run_batch(h["states"][:, 0], 30, flux=True, metrics=True)
+    traj = out["traj"].cpu().numpy()
+    close(traj, h["states"], ROLL_ATOL, ROLL_RTOL)
+    # flux of step t is the symmetrised GNN flux of the reference state t
+    F_ref = 0.5 * (h["flux_edge"][..., :64] + h["flux_edge"][..., 64:]).astype(np.float32)
+    close(out["flux"].cpu().numpy(), F_ref, 5e-6, 1e-5)
+    energy, charge, finite = O.rollout_metrics(traj)
+    m = out["metrics"].cpu().numpy()
+    close(m[..., 0], energy, 1e-6, 1e-6)
+    close(m[..., 1], charge, 1e-6, 1e-6)
+    assert (m[..., 2] == finite).all()
+
+
+def test_hybrid_numpy_api_step_and_run(hf):
+    h = golden("hybrid_W1_r1_nx64.npz")
+    solver = hf.HybridSolver(weights("W1_r1"), radius=1, device=DEV)
+    s1 = solver.step(h["states"][0, 0])
+    assert s1.shape == (3, 64) and s1.dtype == np.float32
+    close(s1, h["states"][0, 1], 1e-6, 1e-6)
+    traj = solver.run(h["states"][0, 0], n_steps=30)
+    assert traj.shape == (31, 3, 64)
+    close(traj, h["states"][0], ROLL_ATOL, ROLL_RTOL)
+    assert solver.radius == 1 and solver.baseline.nx == 64
+
+
+def test_hybrid_step_matches_fused_run(hf):
+    """hf_step (T=1 launches) chained == one persistent hf_run, bit for bit."""
+    h = golden("hybrid_W1_r2_nx64.npz")
+    solver = hf.HybridSolver(weights("W1_r2"), radius=2, device=DEV)
+    st = torch.as_tensor(h["states"][:, 0], device=DEV)
+    cur = st
+    for _ in range(5):
+        cur = solver.step_batch(cur)
+    run = solver.run_batch(st, 5, traj=False)["final"]
+    assert torch.equal(cur, run)
+
+
+def test_hybrid_nx1024_windowed_vs_reference(hf):
+    h = golden("hybrid_W1_r2_nx1024.npz")
+    solver = hf.HybridSolver(weights("W1_r2"), radius=2, nx=1024, dt=3.125e-4, device=DEV)
+    m = solver.model
+    nf, ei = hf.build_chain_graph_batch(h["states"][:, :4].reshape(16, 3, 1024), solver.baseline.x, DEV)
+    with torch.no_grad():
+        fe = m(nf, ei).cpu().numpy().reshape(4, 4, 2048)
+    close(fe, h["flux_edge"], FLUX_ATOL)
+    out = solver.run_batch(h["states"][:, 0], 30)
+    close(out["traj"].cpu().numpy(), h["states"], ROLL_ATOL, ROLL_RTOL)
+
+
+@pytest.mark.parametrize("nx", [1, 2, 7, 16, 32, 48, 50, 55, 56, 100, 130])
+def test_hybrid_any_nx_vs_oracle(hf, nx):
+    """Fused (16/32/48/64) and windowed (others) chain kernels against the oracle
+    on seeded ICs, incl. chains shorter than the 5-cell receptive field."""
+    w = weights("W1_r3")
+    G = O.Grid(nx, dt=5e-3 * min(1.0, nx / 64.0))
+    ics = np.stack([O.initial_condition(G, s) for s in (5, 6, 7)])
+    want, fe_want = O.hybrid_run(O.params_from(w), G, ics, 4)
+    solver = hf.HybridSolver(w, radius=3, nx=nx, dt=G.dt, device=DEV)
+    got = solver.run_batch(ics, 4)["traj"].cpu().numpy()
+    close(got, want, ROLL_ATOL, ROLL_RTOL)
+    nf, ei = hf.build_chain_graph_batch(ics, G.x, DEV)
+    with torch.no_grad():
+        fe = solver.model(nf, ei).cpu().numpy().reshape(3, 2 * nx)
+    close(fe, fe_want[:, 0], FLUX_ATOL)
+
+
+@pytest.mark.parametrize("B", [0, 1, 3, 5, 33])
+def test_ragged_batches(hf, B):
+    w = weights("W1_r1")
+    G = O.Grid(64)
+    ics = np.stack([O.initial_condition(G, s) for s in range(100, 100 + B)]) if B else np.zeros((0, 3, 64), np.float32)
+    solver = hf.HybridSolver(w, radius=1, device=DEV)
+    out = solver.run_batch(ics, 3)
+    assert out["traj"].shape == (B, 4, 3, 64)
+    if B:
+        want, _ = O.hybrid_run(O.params_from(w), G, ics, 3)
+        close(out["traj"].cpu().numpy(), want, ROLL_ATOL, ROLL_RTOL)
+
+
+def test_zero_steps(hf):
+    ics = golden("ics.npz")["ics_nx64"][:4]
+    solver = hf.HybridSolver(weights("W0"), radius=1, device=DEV)
+    out = solver.run_batch(ics, 0, metrics=True)
+    assert np.array_equal(out["traj"].cpu().numpy()[:, 0], ics)
+    assert np.array_equal(out["final"].cpu().numpy(), ics)
+
+
+# ------------------------------------------------------- full-size properties
+def test_full_batch_properties(hf):
+    """BASELINE config 3 size (4096 ICs x 64 cells): determinism, batch
+    invariance, charge conservation, finiteness, and a sampled oracle check."""
+    w = weights("W1_r2")
+    solver = hf.HybridSolver(w, radius=2, device=DEV)
+    seeds = list(range(1000, 1000 + 4096))
+    ics = solver.baseline.initial_conditions(seeds, as_tensor=True)
+    a = solver.run_batch(ics, 30, traj=False, metrics=True)
+    b = solver.run_batch(ics, 30, traj=False)
+    assert torch.equal(a["final"], b["final"])                       # deterministic
+    sub = [0, 1, 777, 2048, 4095]
+    alone = solver.run_batch(ics[sub], 30, traj=False)["final"]
+    assert torch.equal(alone, a["final"][sub])                       # batch invariant
+    m = a["metrics"].cpu().numpy()
+    assert (m[..., 2] == 1).all()
+    drift = np.abs(m[:, -1, 1] - m[:, 0, 1]).max()                   # FV telescopes: mean(n) conserved
+    assert drift < 1e-5, drift
+    pick = np.random.RandomState(0).choice(4096, 24, replace=False)
+    want, _ = O.hybrid_run(O.params_from(w), O.Grid(64), ics[pick].cpu().numpy(), 30)
+    close(a["final"][pick].cpu().numpy(), want[:, -1], ROLL_ATOL, ROLL_RTOL)

@@ -1,0 +1,72 @@
+"""Pins the CPU oracle (oracle/hybrid_oracle.py) to the golden vectors that
+tests/golden/make_golden.py produced by running the reference itself.
+Every comparison here is bit-exact."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import hybrid_oracle as O
+
+WEIGHTS = ["W0", "W1_r1", "W1_r2", "W1_r3"]
+
+
+def test_initial_conditions_bitwise():
+    g = golden("ics.npz")
+    G = O.Grid(64)
+    got = np.stack([O.initial_condition(G, int(s)) for s in g["seeds_nx64"]])
+    assert np.array_equal(got, g["ics_nx64"])
+    G1k = O.Grid(1024, dt=3.125e-4)
+    got = np.stack([O.initial_condition(G1k, int(s)) for s in g["seeds_nx1024"]])
+    assert np.array_equal(got, g["ics_nx1024"])
+    assert np.array_equal(G.x, g["x_nx64"]) and np.array_equal(G1k.x, g["x_nx1024"])
+
+
+@pytest.mark.parametrize("nx", [16, 32, 48, 64, 1024])
+def test_poisson_bitwise(nx):
+    g = golden("poisson.npz")
+    assert np.array_equal(O.solve_poisson(O.Grid(nx), g[f"n_nx{nx}"]), g[f"E_nx{nx}"])
+
+
+def test_classical_bitwise():
+    g = golden("classical.npz")
+    S, F = O.classical_run(O.Grid(64), g["seed0_states"][0], 30)
+    assert np.array_equal(S, g["seed0_states"]) and np.array_equal(F, g["seed0_fluxes"])
+    S, F = O.classical_run(O.Grid(64), g["b16_states"][:, 0], 30)
+    assert np.array_equal(S, g["b16_states"]) and np.array_equal(F, g["b16_fluxes"])
+    S, F = O.classical_run(O.Grid(1024, dt=3.125e-4), g["nx1024_states"][:, 0], 30)
+    assert np.array_equal(S, g["nx1024_states"]) and np.array_equal(F, g["nx1024_fluxes"])
+
+
+@pytest.mark.parametrize("w", WEIGHTS)
+def test_hybrid_rollout_bitwise(w):
+    p = O.params_from(dict(golden(f"weights_{w}.npz")))
+    h = golden(f"hybrid_{w}_nx64.npz")
+    S, FE = O.hybrid_run(p, O.Grid(64), h["states"][:, 0], 30)
+    assert np.array_equal(S, h["states"])
+    assert np.array_equal(FE, h["flux_edge"])
+
+
+def test_hybrid_per_ic_bitwise():
+    p = O.params_from(dict(golden("weights_W1_r1.npz")))
+    h = golden("hybrid_W1_r1_nx64.npz")
+    S = O.hybrid_run_per_ic(p, O.Grid(64), h["states"][:3, 0], 30)
+    assert np.array_equal(S, h["states"][:3])
+
+
+def test_hybrid_nx1024_first_steps():
+    p = O.params_from(dict(golden("weights_W1_r2.npz")))
+    h = golden("hybrid_W1_r2_nx1024.npz")
+    S, FE = O.hybrid_run(p, O.Grid(1024, dt=3.125e-4), h["states"][:2, 0], 4)
+    assert np.array_equal(S, h["states"][:2, :5])
+    assert np.array_equal(FE, h["flux_edge"][:2])
+
+
+def test_random_graph_forward():
+    g = golden("fluxgnn_random.npz")
+    small = O.params_from({k[len("small."):]: g[k] for k in g.files if k.startswith("small.")})
+    import torch
+    got = O.flux_gnn_forward(small, torch.from_numpy(g["small_nf"]), torch.from_numpy(g["small_ei"]))
+    assert np.array_equal(got.detach().numpy(), g["small_flux"])
+    big = O.params_from(dict(golden("weights_W0.npz")))
+    got = O.flux_gnn_forward(big, torch.from_numpy(g["big_nf"]), torch.from_numpy(g["big_ei"]))
+    assert np.array_equal(got.detach().numpy(), g["big_flux"])
