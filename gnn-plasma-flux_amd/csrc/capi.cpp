@@ -247,8 +247,10 @@ void hf_model_destroy(hf_model_t model) {
 }
 
 int hf_chain_flux(hf_model_t m, const float *nf, int B, int nx, float *fe, float *ff, void *stream) {
-  if (!m || !nf) return fail(HF_EINVAL, "hf_chain_flux: NULL model or node features");
+  if (!m) return fail(HF_EINVAL, "hf_chain_flux: NULL model");
   if (B < 0 || nx < 1) return fail(HF_EINVAL, "hf_chain_flux: need B >= 0 and nx >= 1");
+  if (B == 0) return HF_OK;
+  if (!nf) return fail(HF_EINVAL, "hf_chain_flux: NULL node features");
   if (int rc = chain_usable(m)) return rc;
   if (!fe && !ff) return HF_OK;
   HF_CHECK_HIP(hf::launch_chain_flux(m->chain, nf, nullptr, 0, nullptr, B, nx, fe, ff, as_stream(stream)),
@@ -294,8 +296,9 @@ int hf_poisson_coeffs(int nx, double length, double *c) {
 
 int hf_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B, int nx,
                void *stream) {
-  if (!n || !E || !pc) return fail(HF_EINVAL, "hf_poisson: NULL pointer");
   if (B < 0 || nx < 1 || ld_n < nx || ld_E < nx) return fail(HF_EINVAL, "hf_poisson: bad shape");
+  if (B == 0) return HF_OK;
+  if (!n || !E || !pc) return fail(HF_EINVAL, "hf_poisson: NULL pointer");
   if (nx > 2 * kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_poisson: nx too large for the LDS solve");
   HF_CHECK_HIP(hf::launch_poisson(n, ld_n, E, ld_E, pc, B, nx, as_stream(stream)), "hf_poisson");
   return HF_OK;
@@ -303,9 +306,10 @@ int hf_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, i
 
 int hf_step(hf_model_t m, const float *in, float *out, const float *x, const double *pc, int B, int nx,
             float c, float dt, float nu, float dx2, float *ff, float *metrics, void *stream) {
+  if (B < 0 || nx < 1) return fail(HF_EINVAL, "hf_step: need B >= 0, nx >= 1");
+  if (B == 0) return HF_OK;
   if (!in || !out || !pc) return fail(HF_EINVAL, "hf_step: NULL state or Poisson coefficients");
   if (in == out) return fail(HF_EINVAL, "hf_step: state_in and state_out must not alias");
-  if (B < 0 || nx < 1) return fail(HF_EINVAL, "hf_step: need B >= 0, nx >= 1");
   if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_step: nx too large for the LDS solve");
   hipStream_t s = as_stream(stream);
   if (B == 0) return HF_OK;
@@ -338,8 +342,9 @@ int hf_step(hf_model_t m, const float *in, float *out, const float *x, const dou
 int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B,
            int nx, int T, float c, float dt, float nu, float dx2, float *traj, float *flux_traj,
            float *metrics, void *stream) {
-  if (!state0 || !state_final || !pc) return fail(HF_EINVAL, "hf_run: NULL state or Poisson coefficients");
   if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run: need B >= 0, nx >= 1, T >= 0");
+  if (B == 0) return HF_OK;
+  if (!state0 || !state_final || !pc) return fail(HF_EINVAL, "hf_run: NULL state or Poisson coefficients");
   if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run: nx too large for the LDS solve");
   if (m && !x) return fail(HF_EINVAL, "hf_run: NULL x");
   if (m) {

@@ -6,6 +6,11 @@
 // (src/hybrid_solver.py:45-58, src/baseline_solver.py:70-94).
 #pragma once
 
+// HIP's __f*_rn helpers are plain operators unless OCML_BASIC_ROUNDED_OPERATIONS
+// is set, and hipcc contracts a*b+c into FMA by default: turn contraction off
+// for every TU that includes this header (explicit fmaf / MFMA are unaffected).
+#pragma clang fp contract(off)
+
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>

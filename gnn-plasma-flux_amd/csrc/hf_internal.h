@@ -23,16 +23,23 @@ constexpr int kWinCells = 64;
 constexpr int kWinHalo = 4;
 constexpr int kWinFaces = kWinCells - 2 * kWinHalo - 1;  // 55
 
-// Packed float32 weights (device) in MFMA A-fragment order; see capi.cpp
-// pack_chain_f32 for the exact index maps.
+// Packed float32 weights (device) for the chain kernels; see capi.cpp
+// pack_chain_f32 for the exact index maps.  The big matrices form ONE stream
+// of 8 KiB chunks, consumed in order through an LDS ring:
+//   chunk c <  16L : update layer l = c/16, k-steps 4*(c%16) .. +3, all 8 output tiles
+//   chunk c >= 16L : edge readout tile ot = (c-16L)/2, k-steps 16*((c-16L)%2) .. +15, P and Q
+// Each chunk is [j 8][lane 64][4] floats, so one wave instruction moves 1 KiB.
+constexpr int kChunkFloats = 8 * 64 * 4;
+constexpr int kMaxChainLayers = 8;
+__host__ __device__ inline int chain_chunks(int layers) { return 16 * layers + 2 * kNT; }
+
 struct ChainW {
-  const float *win;  // [64 lanes][kNT]             input layer A fragments
-  const float *bin;  // [kH]
-  const float *wl;   // [L][2*kKS][64][kNT]         update MLP A fragments
-  const float *bl;   // [L][kH]
-  const float *we;   // [kNT][kKS][64][2]           edge MLP (P,Q) A fragments
-  const float *be;   // [kH]
-  const float *w2;   // [kH]
+  const float *stream;  // [chain_chunks(L)][8][64][4]
+  const float *win;     // [2][64][4]   input layer A fragments
+  const float *bin;     // [kH]
+  const float *bl;      // [L][kH]
+  const float *be;      // [kH]
+  const float *w2;      // [kH]
   float b2;
   int layers;
 };
