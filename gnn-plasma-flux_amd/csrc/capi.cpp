@@ -63,48 +63,60 @@ struct Layout {
 //  output row n = 16*nt + (l&15).
 int kperm(int s, int lane) { return 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3); }
 
-void pack_chain_f32(const float *p, int L, std::vector<float> &out, int64_t &o_win, int64_t &o_bin,
-                    int64_t &o_wl, int64_t &o_bl, int64_t &o_we, int64_t &o_be, int64_t &o_w2,
-                    float &b2) {
+// Chain-kernel packing (chain_gnn.hip):
+//  * `stream`: chain_chunks(L) chunks of [j 8][lane 64][4] floats (see
+//    hf_internal.h).  Update-layer chunk (l, gi): k-step s = 4gi + (j>>1),
+//    output tile nt = 4(j&1) + c, k = (s < 32 ? 0 : 128) + kperm(s % 32, lane).
+//    Readout chunk (ot, hh): k-step s = 16hh + 2j + (c>>1), c&1 selects
+//    P = W_e[:, :H] or Q = W_e[:, H:].  Row n = 16*tile + (lane&15).
+//  * `win`: [j 2][lane][4], tile nt = 4j + c, column k = lane>>4.
+//  * biases, w2 in natural order; b2 as a scalar.
+struct ChainPack {
+  std::vector<float> buf;
+  int64_t o_stream = 0, o_win = 0, o_bin = 0, o_bl = 0, o_be = 0, o_w2 = 0;
+  float b2 = 0.f;
+};
+
+void pack_chain_f32(const float *p, int L, ChainPack &P) {
   using hf::kH;
   using hf::kKS;
   using hf::kNT;
   const Layout lay(hf::kIn, kH, L);
+  std::vector<float> &out = P.buf;
   out.clear();
-  o_win = (int64_t)out.size();
-  for (int lane = 0; lane < 64; ++lane)
-    for (int nt = 0; nt < kNT; ++nt)
-      out.push_back(p[lay.w_in + (int64_t)(16 * nt + (lane & 15)) * hf::kIn + (lane >> 4)]);
-  o_bin = (int64_t)out.size();
-  out.insert(out.end(), p + lay.b_in, p + lay.b_in + kH);
-  o_wl = (int64_t)out.size();
-  for (int l = 0; l < L; ++l) {
-    const float *W = p + lay.w_l + (int64_t)l * ((int64_t)kH * 2 * kH + kH);
-    for (int s = 0; s < 2 * kKS; ++s)
+  auto layer_w = [&](int l) { return p + lay.w_l + (int64_t)l * ((int64_t)kH * 2 * kH + kH); };
+  P.o_stream = 0;
+  for (int c = 0; c < hf::chain_chunks(L); ++c)
+    for (int j = 0; j < 8; ++j)
       for (int lane = 0; lane < 64; ++lane)
-        for (int nt = 0; nt < kNT; ++nt) {
-          const int k = (s < kKS ? 0 : kH) + kperm(s % kKS, lane);
-          out.push_back(W[(int64_t)(16 * nt + (lane & 15)) * 2 * kH + k]);
+        for (int cc = 0; cc < 4; ++cc) {
+          if (c < 16 * L) {
+            const int l = c / 16, gi = c % 16;
+            const int s = 4 * gi + (j >> 1), nt = 4 * (j & 1) + cc;
+            const int k = (s < kKS ? 0 : kH) + kperm(s % kKS, lane);
+            out.push_back(layer_w(l)[(int64_t)(16 * nt + (lane & 15)) * 2 * kH + k]);
+          } else {
+            const int r = c - 16 * L, ot = r / 2, hh = r % 2;
+            const int s = 16 * hh + 2 * j + (cc >> 1), pq = cc & 1;
+            out.push_back(p[lay.w_e + (int64_t)(16 * ot + (lane & 15)) * 2 * kH + pq * kH + kperm(s, lane)]);
+          }
         }
-  }
-  o_bl = (int64_t)out.size();
-  for (int l = 0; l < L; ++l) {
-    const float *bl = p + lay.w_l + (int64_t)l * ((int64_t)kH * 2 * kH + kH) + (int64_t)kH * 2 * kH;
-    out.insert(out.end(), bl, bl + kH);
-  }
-  o_we = (int64_t)out.size();
-  for (int ot = 0; ot < kNT; ++ot)
-    for (int s = 0; s < kKS; ++s)
-      for (int lane = 0; lane < 64; ++lane) {
-        const int64_t row = (int64_t)(16 * ot + (lane & 15)) * 2 * kH;
-        out.push_back(p[lay.w_e + row + kperm(s, lane)]);
-        out.push_back(p[lay.w_e + row + kH + kperm(s, lane)]);
+  P.o_win = (int64_t)out.size();
+  for (int j = 0; j < 2; ++j)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int cc = 0; cc < 4; ++cc) {
+        const int nt = 4 * j + cc;
+        out.push_back(p[lay.w_in + (int64_t)(16 * nt + (lane & 15)) * hf::kIn + (lane >> 4)]);
       }
-  o_be = (int64_t)out.size();
+  P.o_bin = (int64_t)out.size();
+  out.insert(out.end(), p + lay.b_in, p + lay.b_in + kH);
+  P.o_bl = (int64_t)out.size();
+  for (int l = 0; l < L; ++l) out.insert(out.end(), layer_w(l) + (int64_t)kH * 2 * kH, layer_w(l) + (int64_t)kH * 2 * kH + kH);
+  P.o_be = (int64_t)out.size();
   out.insert(out.end(), p + lay.b_e, p + lay.b_e + kH);
-  o_w2 = (int64_t)out.size();
+  P.o_w2 = (int64_t)out.size();
   out.insert(out.end(), p + lay.w_2, p + lay.w_2 + kH);
-  b2 = p[lay.b_2];
+  P.b2 = p[lay.b_2];
 }
 
 hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
@@ -124,7 +136,7 @@ int check_device() {
 int chain_usable(const hf_model *m) {
   if (!m->chain_ok)
     return fail(HF_EUNSUPPORTED,
-                "chain kernels are specialised to FluxGNN(input_dim=4, hidden_dim=128) float32 "
+                "chain kernels are specialised to FluxGNN(input_dim=4, hidden_dim=128, num_layers<=8) float32 "
                 "(src/config.py:19-23); use hf_graph_flux for other widths");
   return HF_OK;
 }
@@ -165,13 +177,12 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
   m->hidden = hidden;
   m->layers = layers;
   m->wdtype = wdtype;
-  m->chain_ok = (in_dim == hf::kIn && hidden == hf::kH);
+  m->chain_ok = (in_dim == hf::kIn && hidden == hf::kH && layers <= hf::kMaxChainLayers);
 
   // natural copy (graph path) followed by the packed copy (chain path)
-  std::vector<float> packed;
-  int64_t o_win = 0, o_bin = 0, o_wl = 0, o_bl = 0, o_we = 0, o_be = 0, o_w2 = 0;
-  float b2 = 0.f;
-  if (m->chain_ok) pack_chain_f32(host_params, layers, packed, o_win, o_bin, o_wl, o_bl, o_we, o_be, o_w2, b2);
+  ChainPack pk;
+  if (m->chain_ok) pack_chain_f32(host_params, layers, pk);
+  const std::vector<float> &packed = pk.buf;
   // natural layer weights are split into contiguous [L][H][2H] and [L][H]
   std::vector<float> nat((size_t)lay.total);
   {
@@ -226,14 +237,13 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
   if (m->chain_ok) {
     const float *d = m->dev + nat_pad;
     hf::ChainW &c = m->chain;
-    c.win = d + o_win;
-    c.bin = d + o_bin;
-    c.wl = d + o_wl;
-    c.bl = d + o_bl;
-    c.we = d + o_we;
-    c.be = d + o_be;
-    c.w2 = d + o_w2;
-    c.b2 = b2;
+    c.stream = d + pk.o_stream;
+    c.win = d + pk.o_win;
+    c.bin = d + pk.o_bin;
+    c.bl = d + pk.o_bl;
+    c.be = d + pk.o_be;
+    c.w2 = d + pk.o_w2;
+    c.b2 = pk.b2;
     c.layers = layers;
   }
   *out = m;

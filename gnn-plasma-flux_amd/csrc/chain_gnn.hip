@@ -18,6 +18,15 @@
 //   from the adjacent m-tile by row_ror (periodic wrap inside the IC).
 //   The edge MLP uses the P/Q split: z(i->j) = W_a h_i + W_b h_j + b, so P and
 //   Q are per-node GEMMs (K=128) and each edge only adds a shifted pair.
+//
+// Weight stream: a workgroup is 4 waves (4 ICs, one per SIMD) that consume the
+// same 640 KiB weight stream in lockstep.  The stream is cut into 8 KiB chunks
+// (4 k-steps of an update layer, or 16 k-steps of the readout) and staged
+// through a 4-slot LDS ring by global_load_lds (LDS-DMA, no registers in
+// flight): chunk p+2 is issued while chunk p feeds the MFMAs, each wave moving
+// a quarter of every chunk.  Per chunk: counted vmcnt for the wave's own DMA,
+// one s_barrier, issue p+2, ds_read_b128 the fragments.  Each weight byte
+// leaves L2 once per workgroup instead of once per wave.
 #include "hf_device.h"
 #include "hf_internal.h"
 
@@ -25,6 +34,7 @@ namespace hf {
 namespace {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -66,118 +76,201 @@ __device__ __forceinline__ void left_nb(const float (&v)[MT], float (&l)[MT]) {
   for (int mt = 0; mt < MT; ++mt) l[mt] = dpp_over<kRowShr1>(rot[(mt + MT - 1) % MT], v[mt]);
 }
 
-__device__ __forceinline__ f4 relu4(f4 v) {
-  return f4{relu(v.x), relu(v.y), relu(v.z), relu(v.w)};
-}
+__device__ __forceinline__ f4 relu4(f4 v) { return f4{relu(v.x), relu(v.y), relu(v.z), relu(v.w)}; }
 
 __device__ __forceinline__ f4 ldf4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
 
-// A fragments of one k-step for all kNT output tiles: 8 consecutive floats per lane.
-__device__ __forceinline__ void load_afrag(const float *p, float (&a)[kNT]) {
-  f4 a0 = ldf4(p), a1 = ldf4(p + 4);
-  a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w;
-  a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+// Orders this wave's LDS traffic (the compiler may otherwise reorder a ds_read
+// of another lane's word above the ds_write that produced it).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// ------------------------------------------------------------------ LDS plan
+constexpr int kWaves = 4;                               // one IC (item) per wave
+constexpr int kRingSlots = 4;
+constexpr int kRingFloats = kRingSlots * kChunkFloats;  // 32 KiB
+constexpr int kSmallFloats = 512 + kH * (3 + kMaxChainLayers);  // win, bin, be, w2, bl[L]
+constexpr int kWaveScratchFloats = 6 * 64 + 2 * 64;     // n,u,E,x,F,rho (+ 64 doubles)
+constexpr int kLdsFloats = kRingFloats + kSmallFloats + kWaves * kWaveScratchFloats;
+
+struct Small {  // LDS copies of the small weight arrays
+  const float *win, *bin, *bl, *be, *w2;
+};
+
+// Stage the small arrays into LDS (all threads of the workgroup) and return views.
+__device__ __forceinline__ Small stage_small(const ChainW &W, float *s) {
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) s[i] = W.win[i];
+  for (int i = threadIdx.x; i < kH; i += blockDim.x) {
+    s[512 + i] = W.bin[i];
+    s[512 + kH + i] = W.be[i];
+    s[512 + 2 * kH + i] = W.w2[i];
+  }
+  for (int i = threadIdx.x; i < W.layers * kH; i += blockDim.x) s[512 + 3 * kH + i] = W.bl[i];
+  return Small{s, s + 512, s + 512 + 3 * kH, s + 512 + kH, s + 512 + 2 * kH};
+}
+
+// ----------------------------------------------------------------- the ring
+struct Ring {
+  const float *src;  // packed weight stream (global)
+  float *lds;        // 4 slots
+  int chunks;        // chunks per forward pass
+  int wave, lane;
+  int pos;           // stream position being consumed (slot = pos & 3)
+  int ahead;         // chunk id of stream position pos + 2
+
+  __device__ __forceinline__ void issue(int chunk, int slot) const {
+    const float *g = src + (size_t)chunk * kChunkFloats + lane * 4;
+    float *d = lds + slot * kChunkFloats;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * wave + jj;  // this wave's quarter of the chunk
+      __builtin_amdgcn_global_load_lds(g + j * 256, (lds_void *)(d + j * 256), 16, 0, 0);
+    }
+  }
+  // Start the stream at chunk 0 (positions 0 and 1 in flight).
+  __device__ __forceinline__ void prime() {
+    pos = 0;
+    issue(0, 0);
+    issue(1 % chunks, 1);
+    ahead = 2 % chunks;
+  }
+  // Wait for chunk `pos`, keep two chunks in flight, return its slot.
+  __device__ __forceinline__ const float *next() {
+    // own DMA for `pos` done (only pos+1's two instructions may remain), every
+    // ds_read of this wave retired, then every wave has passed: the slot of
+    // pos-2, which pos+2 is about to overwrite, is no longer read by anyone.
+    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(ahead, (pos + 2) & (kRingSlots - 1));
+    ahead = ahead + 1 == chunks ? 0 : ahead + 1;
+    const float *slot = lds + (pos & (kRingSlots - 1)) * kChunkFloats;
+    ++pos;
+    return slot;
+  }
+  __device__ __forceinline__ void drain() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+};
+
+__device__ __forceinline__ void read_chunk(const float *slot, int lane, f4 (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = ldf4(slot + (j * 64 + lane) * 4);
+}
+
+// One update-layer chunk: k-steps s = 4*gi + q.  The first 8 chunks of a layer
+// read h itself, the last 8 the neighbour mean (h[i+1] + h[i-1]) / 2.
+template <int MT, int GI>
+__device__ __forceinline__ void layer_chunk(Ring &R, const f4 (&h)[MT][kNT], f4 (&acc)[MT][kNT]) {
+  f4 v[8];
+  read_chunk(R.next(), R.lane, v);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    constexpr int kHalf = kKS / 4;
+    const int s = (GI % kHalf) * 4 + q;  // k-step within its 128-wide half
+    float b[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) b[mt] = h[mt][s >> 2][s & 3];
+    if (GI >= kHalf) {
+      float bl[MT], br[MT];
+      left_nb<MT>(b, bl);
+      right_nb<MT>(b, br);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) b[mt] = __fmul_rn(__fadd_rn(br[mt], bl[mt]), 0.5f);  // index_add_ h[i+1], h[i-1]; / deg 2
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = mfma4(v[2 * q + (nt >> 2)][nt & 3], b[mt], acc[mt][nt]);
+  }
+}
+
+// One readout chunk: k-steps s = 16*HH + qq for P (W_e[:, :H]) and Q (W_e[:, H:]).
+template <int MT, int HH>
+__device__ __forceinline__ void read_chunk_pq(Ring &R, const f4 (&h)[MT][kNT], f4 (&P)[MT], f4 (&Q)[MT]) {
+  f4 v[8];
+  read_chunk(R.next(), R.lane, v);
+#pragma unroll
+  for (int qq = 0; qq < 16; ++qq) {
+    const int s = 16 * HH + qq;
+    const float ap = v[qq >> 1][2 * (qq & 1)], aq = v[qq >> 1][2 * (qq & 1) + 1];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const float b = h[mt][s >> 2][s & 3];
+      P[mt] = mfma4(ap, b, P[mt]);
+      Q[mt] = mfma4(aq, b, Q[mt]);
+    }
+  }
 }
 
 // FluxGNN forward for the MT*16 cells of this wave.  feat[mt] is the lane's
 // input feature (index l>>4 of [n,u,E,x]) of cell 16*mt + (l&15).  Returns the
 // edge fluxes of (i -> i+1) in ffwd and of (i+1 -> i) in fbwd for cell i, on
-// every lane of the cell's column.
+// every lane of the cell's column.  Consumes exactly one pass of the stream.
 template <int MT>
-__device__ __forceinline__ void gnn_chain(const ChainW &W, const float (&feat)[MT],
+__device__ __forceinline__ void gnn_chain(const ChainW &W, const Small &S, Ring &R, const float (&feat)[MT],
                                           float (&ffwd)[MT], float (&fbwd)[MT]) {
-  const int lane = threadIdx.x & 63;
+  const int lane = R.lane;
   const int g4 = 4 * (lane >> 4);
   f4 h[MT][kNT];
 
   // input MLP: h0 = ReLU(W_in x + b_in), K = 4 = one MFMA per tile   (src/flux_gnn.py:49)
   {
-    float a[kNT];
-    load_afrag(W.win + lane * kNT, a);
+    const f4 a0 = ldf4(S.win + lane * 4), a1 = ldf4(S.win + 256 + lane * 4);
 #pragma unroll
     for (int nt = 0; nt < kNT; ++nt) {
-      const f4 bias = ldf4(W.bin + 16 * nt + g4);
+      const f4 bias = ldf4(S.bin + 16 * nt + g4);
+      const float a = nt < 4 ? a0[nt & 3] : a1[nt & 3];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) h[mt][nt] = relu4(mfma4(a[nt], feat[mt], bias));
+      for (int mt = 0; mt < MT; ++mt) h[mt][nt] = relu4(mfma4(a, feat[mt], bias));
     }
   }
 
   // message passing: h = ReLU(W_l [h ; (h[i+1]+h[i-1])/2] + b_l)        (src/flux_gnn.py:53-60)
   for (int l = 0; l < W.layers; ++l) {
-    const float *wl = W.wl + (size_t)l * (2 * kKS * 64 * kNT) + lane * kNT;
-    const float *bl = W.bl + l * kH + g4;
     f4 acc[MT][kNT];
-#pragma unroll
-    for (int nt = 0; nt < kNT; ++nt) {
-      const f4 bias = ldf4(bl + 16 * nt);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = bias;
-    }
-#pragma unroll
-    for (int s = 0; s < kKS; ++s) {  // self half of the input, k = 16*(s>>2) + 4g + (s&3)
-      float a[kNT];
-      load_afrag(wl + s * (64 * kNT), a);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const float b = h[mt][s >> 2][s & 3];
-#pragma unroll
-        for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = mfma4(a[nt], b, acc[mt][nt]);
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < kKS; ++s) {  // aggregated half, k = 128 + same order
-      float a[kNT];
-      load_afrag(wl + (kKS + s) * (64 * kNT), a);
-      float v[MT], vl[MT], vr[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) v[mt] = h[mt][s >> 2][s & 3];
-      left_nb<MT>(v, vl);
-      right_nb<MT>(v, vr);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        // index_add_ of h[i+1] then h[i-1], divided by deg = 2 (exact)
-        const float b = __fmul_rn(__fadd_rn(vr[mt], vl[mt]), 0.5f);
-#pragma unroll
-        for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = mfma4(a[nt], b, acc[mt][nt]);
-      }
-    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < kNT; ++nt) h[mt][nt] = relu4(acc[mt][nt]);
+      for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+    layer_chunk<MT, 0>(R, h, acc);
+    layer_chunk<MT, 1>(R, h, acc);
+    layer_chunk<MT, 2>(R, h, acc);
+    layer_chunk<MT, 3>(R, h, acc);
+    layer_chunk<MT, 4>(R, h, acc);
+    layer_chunk<MT, 5>(R, h, acc);
+    layer_chunk<MT, 6>(R, h, acc);
+    layer_chunk<MT, 7>(R, h, acc);
+    layer_chunk<MT, 8>(R, h, acc);
+    layer_chunk<MT, 9>(R, h, acc);
+    layer_chunk<MT, 10>(R, h, acc);
+    layer_chunk<MT, 11>(R, h, acc);
+    layer_chunk<MT, 12>(R, h, acc);
+    layer_chunk<MT, 13>(R, h, acc);
+    layer_chunk<MT, 14>(R, h, acc);
+    layer_chunk<MT, 15>(R, h, acc);
+#pragma unroll
+    for (int nt = 0; nt < kNT; ++nt) {
+      const f4 bias = ldf4(S.bl + l * kH + 16 * nt + g4);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) h[mt][nt] = relu4(acc[mt][nt] + bias);
+    }
   }
 
   // edge readout, P/Q split: z_fwd(i) = P(i) + Q(i+1), z_bwd(i) = P(i+1) + Q(i),
-  // P = W_e[:, :H] h + b_e, Q = W_e[:, H:] h; flux = w2 . ReLU(z) + b2   (src/flux_gnn.py:62-66)
+  // P = W_e[:, :H] h, Q = W_e[:, H:] h; flux = w2 . ReLU(z + b_e) + b2    (src/flux_gnn.py:62-66)
   float pf[MT], pb[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
   for (int ot = 0; ot < kNT; ++ot) {
     f4 P[MT], Q[MT];
-    const f4 be = ldf4(W.be + 16 * ot + g4);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      P[mt] = be;
-      Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
-    }
-    const float *we = W.we + (size_t)ot * (kKS * 64 * 2) + lane * 2;
-#pragma unroll
-    for (int s = 0; s < kKS; ++s) {
-      const float2 a = *reinterpret_cast<const float2 *>(we + s * 128);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const float b = h[mt][s >> 2][s & 3];
-        P[mt] = mfma4(a.x, b, P[mt]);
-        Q[mt] = mfma4(a.y, b, Q[mt]);
-      }
-    }
-    const f4 w2 = ldf4(W.w2 + 16 * ot + g4);
+    for (int mt = 0; mt < MT; ++mt) P[mt] = Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
+    read_chunk_pq<MT, 0>(R, h, P, Q);
+    read_chunk_pq<MT, 1>(R, h, P, Q);
+    const f4 be = ldf4(S.be + 16 * ot + g4);
+    const f4 w2 = ldf4(S.w2 + 16 * ot + g4);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float pv[MT], qv[MT], pr[MT], qr[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        pv[mt] = P[mt][r];
+        pv[mt] = __fadd_rn(P[mt][r], be[r]);
         qv[mt] = Q[mt][r];
       }
       right_nb<MT>(pv, pr);
@@ -201,39 +294,59 @@ __device__ __forceinline__ void gnn_chain(const ChainW &W, const float (&feat)[M
   }
 }
 
+__device__ __forceinline__ Ring make_ring(const ChainW &W, float *ring_lds) {
+  Ring R;
+  R.src = W.stream;
+  R.lds = ring_lds;
+  R.chunks = chain_chunks(W.layers);
+  R.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  R.lane = threadIdx.x & 63;
+  R.pos = 0;
+  R.ahead = 0;
+  return R;
+}
+
 // ---------------------------------------------------------------------------
-// FluxGNN.forward on B chains, one wave per (IC, window).
+// FluxGNN.forward on B chains; items = (IC, window), one wave per item,
+// 4 items per workgroup.
 //  EXACT: nx == 16*MT, the wave owns the whole periodic IC, every face exact.
 //  else : MT == 4 window of 64 cells starting at w*55-4 (mod nx); faces
 //         [4,58] of the window (55 per window) are exact, the rest discarded.
 template <int MT, bool EXACT>
-__global__ __launch_bounds__(64, 1) void chain_flux_kernel(ChainW W, const float *__restrict__ nf,
-                                                           const float *__restrict__ state,
-                                                           int64_t ld_state,
-                                                           const float *__restrict__ x, int nx,
-                                                           int nwin, float *__restrict__ fe,
-                                                           float *__restrict__ ff) {
-  const int lane = threadIdx.x;
-  const int j = lane & 15, g = lane >> 4;
-  const int b = blockIdx.x / nwin;
-  const int w = blockIdx.x - b * nwin;
+__global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const float *__restrict__ nf,
+                                                            const float *__restrict__ state,
+                                                            int64_t ld_state,
+                                                            const float *__restrict__ x, int nx,
+                                                            int nwin, int64_t items,
+                                                            float *__restrict__ fe,
+                                                            float *__restrict__ ff) {
+  __shared__ f4 lds4[kLdsFloats / 4];
+  float *lds = reinterpret_cast<float *>(lds4);
+  const Small S = stage_small(W, lds + kRingFloats);
+  Ring R = make_ring(W, lds);
+  const int lane = R.lane, j = lane & 15, g = lane >> 4;
+  const int64_t item_raw = (int64_t)blockIdx.x * kWaves + R.wave;
+  const bool live = item_raw < items;
+  const int64_t item = live ? item_raw : items - 1;  // idle waves mirror a real item, write nothing
+  const int64_t b = item / nwin;
+  const int w = (int)(item - b * nwin);
   const int start = EXACT ? 0 : w * kWinFaces - kWinHalo;
   float feat[MT];
   int cell[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    int cidx = start + 16 * mt + j;
-    cidx %= nx;
+    int cidx = (start + 16 * mt + j) % nx;
     if (cidx < 0) cidx += nx;
     cell[mt] = cidx;
-    if (nf) {
-      feat[mt] = nf[((int64_t)b * nx + cidx) * kIn + g];
-    } else {
-      feat[mt] = g < 3 ? state[(int64_t)b * ld_state + (int64_t)g * nx + cidx] : x[cidx];
-    }
+    feat[mt] = nf ? nf[(b * nx + cidx) * kIn + g]
+                  : (g < 3 ? state[b * ld_state + (int64_t)g * nx + cidx] : x[cidx]);
   }
+  __syncthreads();  // small weights staged (no DMA in flight yet)
+  R.prime();
   float f_fwd[MT], f_bwd[MT];
-  gnn_chain<MT>(W, feat, f_fwd, f_bwd);
+  gnn_chain<MT>(W, S, R, feat, f_fwd, f_bwd);
+  R.drain();
+  if (!live) return;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int wc = 16 * mt + j;
@@ -244,90 +357,112 @@ __global__ __launch_bounds__(64, 1) void chain_flux_kernel(ChainW W, const float
       ok = wc >= kWinHalo && wc < kWinHalo + kWinFaces && face < nx;
     }
     if (!ok) continue;
-    if (fe && g == 0) fe[(int64_t)b * 2 * nx + face] = f_fwd[mt];
-    if (fe && g == 1) fe[(int64_t)b * 2 * nx + nx + face] = f_bwd[mt];
-    if (ff && g == 2) ff[(int64_t)b * nx + face] = face_flux(f_fwd[mt], f_bwd[mt]);
+    if (fe && g == 0) fe[b * 2 * nx + face] = f_fwd[mt];
+    if (fe && g == 1) fe[b * 2 * nx + nx + face] = f_bwd[mt];
+    if (ff && g == 2) ff[b * nx + face] = face_flux(f_fwd[mt], f_bwd[mt]);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Persistent hybrid rollout, one wave per IC, nx = 16*MT: T steps of
-// GNN -> symmetrise -> continuity -> Burgers -> spectral Poisson with the
-// state held in LDS (src/hybrid_solver.py:34-73).
+// Persistent hybrid rollout, one wave per IC (4 ICs per workgroup), nx = 16*MT:
+// T steps of GNN -> symmetrise -> continuity -> Burgers -> spectral Poisson
+// with the IC's state in LDS (src/hybrid_solver.py:34-73).  The weight stream
+// runs continuously across steps.
 template <int MT>
-__global__ __launch_bounds__(64, 1) void chain_rollout_kernel(
+__global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
     ChainW W, const float *__restrict__ state0, float *__restrict__ state_final,
-    const float *__restrict__ x, const double *__restrict__ pc, int T, float c, float dt,
+    const float *__restrict__ x, const double *__restrict__ pc, int B, int T, float c, float dt,
     float *__restrict__ traj, float *__restrict__ flux_traj, float *__restrict__ metrics) {
   constexpr int NX = 16 * MT;
-  __shared__ float s_st[4 * NX];  // n | u | E | x
-  __shared__ float s_F[NX];
-  __shared__ float s_rho[NX];
-  __shared__ double s_c[NX];
-  const int lane = threadIdx.x;
-  const int j = lane & 15, g = lane >> 4;
-  const int64_t b = blockIdx.x;
+  __shared__ f4 lds4[kLdsFloats / 4];
+  float *lds = reinterpret_cast<float *>(lds4);
+  const Small S = stage_small(W, lds + kRingFloats);
+  Ring R = make_ring(W, lds);
+  const int lane = R.lane, j = lane & 15, g = lane >> 4;
+  float *scratch = lds + kRingFloats + kSmallFloats + R.wave * kWaveScratchFloats;
+  float *s_st = scratch;          // n | u | E | x   (4 x 64)
+  float *s_F = scratch + 4 * 64;
+  float *s_rho = scratch + 5 * 64;
+  double *s_c = reinterpret_cast<double *>(scratch + 6 * 64);
+  const int b_raw = blockIdx.x * kWaves + R.wave;
+  const bool live = b_raw < B;
+  const int64_t b = live ? b_raw : B - 1;
   const float *st0 = state0 + b * 3 * NX;
-  for (int i = lane; i < 3 * NX; i += 64) s_st[i] = st0[i];
+  for (int i = lane; i < 3 * NX; i += 64) s_st[(i / NX) * 64 + i % NX] = st0[i];
   if (lane < NX) {
-    s_st[3 * NX + lane] = x[lane];
+    s_st[3 * 64 + lane] = x[lane];
     s_c[lane] = pc[lane];
   }
-  __syncthreads();
-  float *tj = traj ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
-  float *mt_out = metrics ? metrics + b * (int64_t)(T + 1) * HF_NUM_METRICS : nullptr;
+  __syncthreads();  // small weights + per-wave state visible (no DMA in flight yet)
+  float *tj = (traj && live) ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
+  float *mt_out = (metrics && live) ? metrics + b * (int64_t)(T + 1) * HF_NUM_METRICS : nullptr;
+  float *ftj = (flux_traj && live) ? flux_traj + b * (int64_t)T * NX : nullptr;
   auto emit = [&](int t) {
     if (tj)
-      for (int i = lane; i < 3 * NX; i += 64) tj[(int64_t)t * 3 * NX + i] = s_st[i];
+      for (int i = lane; i < 3 * NX; i += 64) tj[(int64_t)t * 3 * NX + i] = s_st[(i / NX) * 64 + i % NX];
     if (mt_out) {
       MetricAcc m;
       m.init();
-      if (lane < NX) m.add(s_st[lane], s_st[NX + lane], s_st[2 * NX + lane]);
+      if (lane < NX) m.add(s_st[lane], s_st[64 + lane], s_st[128 + lane]);
       m.wave_reduce();
       if (lane == 0) m.store(mt_out + t * HF_NUM_METRICS, NX);
     }
   };
   emit(0);
+  R.prime();
   for (int t = 0; t < T; ++t) {
     float feat[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) feat[mt] = s_st[g * NX + 16 * mt + j];
+    for (int mt = 0; mt < MT; ++mt) feat[mt] = s_st[g * 64 + 16 * mt + j];
     float f_fwd[MT], f_bwd[MT];
-    gnn_chain<MT>(W, feat, f_fwd, f_bwd);
+    gnn_chain<MT>(W, S, R, feat, f_fwd, f_bwd);
     if (g == 0) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) s_F[16 * mt + j] = face_flux(f_fwd[mt], f_bwd[mt]);
     }
-    __syncthreads();
+    wave_lds_sync();
     float n_new = 0.f, u_new = 0.f;
     if (lane < NX) {
       const int im = lane == 0 ? NX - 1 : lane - 1;
       const float F = s_F[lane];
       n_new = continuity(s_st[lane], F, s_F[im], c);
-      u_new = velocity_hybrid(s_st[NX + lane], s_st[NX + im], s_st[2 * NX + lane], c, dt);
+      u_new = velocity_hybrid(s_st[64 + lane], s_st[64 + im], s_st[128 + lane], c, dt);
       s_rho[lane] = __fsub_rn(n_new, 1.0f);
-      if (flux_traj) flux_traj[(b * T + t) * NX + lane] = F;
+      if (ftj) ftj[(int64_t)t * NX + lane] = F;
     }
-    __syncthreads();
+    wave_lds_sync();
     if (lane < NX) {
       const float E_new = poisson_cell(s_rho, s_c, lane, NX);
       s_st[lane] = n_new;
-      s_st[NX + lane] = u_new;
-      s_st[2 * NX + lane] = E_new;
+      s_st[64 + lane] = u_new;
+      s_st[128 + lane] = E_new;
     }
-    __syncthreads();
+    wave_lds_sync();
     emit(t + 1);
   }
+  R.drain();
+  if (!live) return;
   float *out = state_final + b * 3 * NX;
-  for (int i = lane; i < 3 * NX; i += 64) out[i] = s_st[i];
+  for (int i = lane; i < 3 * NX; i += 64) out[i] = s_st[(i / NX) * 64 + i % NX];
+}
+
+template <int MT, bool EXACT>
+hipError_t flux_launch(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
+                       int nx, int nwin, int64_t items, float *fe, float *ff, hipStream_t s) {
+  const int64_t blocks = (items + kWaves - 1) / kWaves;
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((chain_flux_kernel<MT, EXACT>), dim3((unsigned)blocks), dim3(64 * kWaves), 0, s, w, nf,
+                     state, ld_state, x, nx, nwin, items, fe, ff);
+  return hipGetLastError();
 }
 
 template <int MT>
 hipError_t rollout_mt(const ChainW &w, const float *state0, float *state_final, const float *x,
                       const double *pc, int B, int T, float c, float dt, float *traj,
                       float *flux_traj, float *metrics, hipStream_t s) {
-  hipLaunchKernelGGL(chain_rollout_kernel<MT>, dim3(B), dim3(64), 0, s, w, state0, state_final, x,
-                     pc, T, c, dt, traj, flux_traj, metrics);
+  const int blocks = (B + kWaves - 1) / kWaves;
+  hipLaunchKernelGGL(chain_rollout_kernel<MT>, dim3(blocks), dim3(64 * kWaves), 0, s, w, state0, state_final,
+                     x, pc, B, T, c, dt, traj, flux_traj, metrics);
   return hipGetLastError();
 }
 
@@ -338,29 +473,14 @@ hipError_t launch_chain_flux(const ChainW &w, const float *nf, const float *stat
                              hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (nx) {
-    case 16:
-      hipLaunchKernelGGL((chain_flux_kernel<1, true>), dim3(B), dim3(64), 0, s, w, nf, state,
-                         ld_state, x, nx, 1, flux_edge, flux_face);
-      return hipGetLastError();
-    case 32:
-      hipLaunchKernelGGL((chain_flux_kernel<2, true>), dim3(B), dim3(64), 0, s, w, nf, state,
-                         ld_state, x, nx, 1, flux_edge, flux_face);
-      return hipGetLastError();
-    case 48:
-      hipLaunchKernelGGL((chain_flux_kernel<3, true>), dim3(B), dim3(64), 0, s, w, nf, state,
-                         ld_state, x, nx, 1, flux_edge, flux_face);
-      return hipGetLastError();
-    case 64:
-      hipLaunchKernelGGL((chain_flux_kernel<4, true>), dim3(B), dim3(64), 0, s, w, nf, state,
-                         ld_state, x, nx, 1, flux_edge, flux_face);
-      return hipGetLastError();
+    case 16: return flux_launch<1, true>(w, nf, state, ld_state, x, nx, 1, B, flux_edge, flux_face, s);
+    case 32: return flux_launch<2, true>(w, nf, state, ld_state, x, nx, 1, B, flux_edge, flux_face, s);
+    case 48: return flux_launch<3, true>(w, nf, state, ld_state, x, nx, 1, B, flux_edge, flux_face, s);
+    case 64: return flux_launch<4, true>(w, nf, state, ld_state, x, nx, 1, B, flux_edge, flux_face, s);
     default: {
       const int nwin = (nx + kWinFaces - 1) / kWinFaces;
-      const int64_t blocks = (int64_t)B * nwin;
-      if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((chain_flux_kernel<4, false>), dim3((unsigned)blocks), dim3(64), 0, s, w,
-                         nf, state, ld_state, x, nx, nwin, flux_edge, flux_face);
-      return hipGetLastError();
+      return flux_launch<4, false>(w, nf, state, ld_state, x, nx, nwin, (int64_t)B * nwin, flux_edge,
+                                   flux_face, s);
     }
   }
 }
