@@ -53,6 +53,20 @@ def cpu_baseline(weights, nx, T, n_ics, threads):
     return alpha, beta
 
 
+def pmc_traffic(K, B, nx, traj):
+    """HBM bytes per launch from the committed PMC passes of this same bench
+    command (tools/gpu_pmc.sh + tools/pmc_traffic.py), if they match."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if (t.get("steps"), t.get("ics_per_gpu"), t.get("nx"), t.get("traj")) != (K, B, nx, traj):
+        return None
+    return t
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,6 +78,10 @@ def main():
     ap.add_argument("--no-traj", action="store_true", help="do not record the state trajectory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-ics", type=int, default=256)
+    ap.add_argument("--precision", default="f32", choices=["f32", "f16x3", "bf16"],
+                    help="chain-kernel arithmetic of the headline line (f32 = exact float32 MFMA)")
+    ap.add_argument("--also", default="f16x3",
+                    help="comma list of other precisions to time in the same process (reported under 'alt'); '' = none")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -83,7 +101,7 @@ def main():
     weights = dict(np.load(args.weights, allow_pickle=False))
     B, nx, K, W = args.ics_per_gpu, args.nx, args.steps, args.warmup
     n_total = B * world
-    solver = HybridSolver(weights, radius=3, nx=nx, device=dev)
+    solver = HybridSolver(weights, radius=3, nx=nx, device=dev, precision=args.precision)
     ics = solver.baseline.initial_conditions(shard_seeds(1000, n_total, world, rank), as_tensor=True)
     stream = torch.cuda.current_stream(dev)
 
@@ -108,6 +126,25 @@ def main():
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1)
 
+    # other precisions, same ICs / K / warmup, timed the same way (reported, not the headline)
+    alt = {}
+    for prec in [p for p in args.also.split(",") if p and p != args.precision]:
+        s2 = HybridSolver(weights, radius=3, nx=nx, device=dev, precision=prec)
+        s2.run_batch(ics, max(W, 1), traj=not args.no_traj)
+        torch.cuda.synchronize(dev)
+        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ta = time.perf_counter()
+        a0.record(stream)
+        r2 = s2.run_batch(ics, K, traj=not args.no_traj, metrics=True)
+        a1.record(stream)
+        torch.cuda.synchronize(dev)
+        wall2 = time.perf_counter() - ta
+        dev_err = float((r2["final"] - final).abs().max().item())
+        alt[prec] = {"value": round(B * K / wall2, 1), "ms_per_step": round(wall2 / K * 1e3, 4),
+                     "kernel_ms": round(a0.elapsed_time(a1), 3),
+                     "max_abs_diff_vs_headline_final_state": dev_err}
+        del s2, r2
+
     t_max = torch.tensor([wall], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -115,6 +152,7 @@ def main():
     finite = float(gathered[:, 2].float().mean().item())
 
     if rank == 0:
+        traffic = pmc_traffic(K, B, nx, not args.no_traj)
         value = n_total * K / wall_max
         flop = GNN_FLOP_PER_CELL_STEP * B * nx * K
         achieved = flop / (kernel_ms * 1e-3) / 1e12
@@ -137,20 +175,23 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": {"f32": "f32", "f16x3": "f16x3 (fp32-accurate split: 3 fp16 MFMA products, f32 accumulate)",
+                      "bf16": "bf16 (f32 accumulate)"}[args.precision],
             "data": "synthetic: reference IC generator seeds 1000.., fixture weights W1_r3 (1-epoch reference trainer)",
-            "config": {"workload": f"cfg3: {nx}-cell periodic chain, {B}-IC batch per GPU, FluxGNN(4,128,4) f32, "
+            "config": {"workload": f"cfg3: {nx}-cell periodic chain, {B}-IC batch per GPU, FluxGNN(4,128,4) {args.precision}, "
                                    f"{K}-step persistent rollout{'' if args.no_traj else ' recording every state'}",
                        "nx": nx, "ics_per_gpu": B, "global_ics": n_total, "parallelism": f"ic-shard x{world}"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_MFMA_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
-                         "traffic": None,
+                         "traffic": traffic["traffic_bytes"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
                          "kernel": "chain_rollout_kernel<4>", "kernel_ms": round(kernel_ms, 3),
                          "flop_per_launch": flop,
                          "hbm_state_frac": round(STATE_BYTES_PER_CELL_STEP * B * nx * K / (kernel_ms * 1e-3)
                                                  / (PEAK_HBM_GBS * 1e9), 6)},
             "cpu_baseline": cpu,
             "finite_fraction": finite,
+            "alt": alt or None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -63,59 +64,129 @@ struct Layout {
 //  output row n = 16*nt + (l&15).
 int kperm(int s, int lane) { return 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3); }
 
-// Chain-kernel packing (chain_gnn.hip):
-//  * `stream`: chain_chunks(L) chunks of [j 8][lane 64][4] floats (see
-//    hf_internal.h).  Update-layer chunk (l, gi): k-step s = 4gi + (j>>1),
-//    output tile nt = 4(j&1) + c, k = (s < 32 ? 0 : 128) + kperm(s % 32, lane).
-//    Readout chunk (ot, hh): k-step s = 16hh + 2j + (c>>1), c&1 selects
-//    P = W_e[:, :H] or Q = W_e[:, H:].  Row n = 16*tile + (lane&15).
-//  * `win`: [j 2][lane][4], tile nt = 4j + c, column k = lane>>4.
-//  * biases, w2 in natural order; b2 as a scalar.
+// Chain-kernel packing (chain_f32.hip / chain_k32.hip; layouts in hf_internal.h).
+//  f32 `stream`: chain_chunks chunks of [j 8][lane 64][4] floats.  Update-layer
+//    chunk (l, gi): k-step s = 4gi + (j>>1), output tile nt = 4(j&1) + c,
+//    k = (s < 32 ? 0 : 128) + kperm(s % 32, lane).  Readout chunk (ot, hh):
+//    k-step s = 16hh + 2j + (c>>1), c&1 selects P = W_e[:, :H] or Q = W_e[:, H:].
+//  k32 `stream`: per layer chunks (nth, kb) for nth = 0..1, kb = 0..3, each
+//    [j = 2*ntl + (W_a|W_b)][term][lane][e 0..7] 16-bit values with output tile
+//    nt = 4nth + ntl and k = (W_b ? 128 : 0) + 16(2kb + (e>>2)) + 4(lane>>4) + (e&3);
+//    then per readout tile ot one chunk [j = 2kb + (P|Q)][term][lane][e].
+//    f16x3: term 0 = fp16(w), term 1 = fp16(w - term0); bf16: one bf16(w) term.
+//  Row n = 16*tile + (lane&15) throughout.
+//  small (f32): win [j 2][lane][4] (tile nt = 4j + c, column k = lane>>4), then
+//    b_in, b_l[L], b_e, w2; b2 as a scalar.  In bf16 mode every weight matrix
+//    (incl. W_in, w2) is rounded to bf16 values; biases stay f32.
+uint16_t to_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+float bf16_to_f32(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+uint16_t f16_bits(_Float16 h) {
+  uint16_t b;
+  std::memcpy(&b, &h, 2);
+  return b;
+}
+
 struct ChainPack {
-  std::vector<float> buf;
-  int64_t o_stream = 0, o_win = 0, o_bin = 0, o_bl = 0, o_be = 0, o_w2 = 0;
+  std::vector<unsigned char> stream;
+  std::vector<float> small;
+  int64_t o_win = 0, o_bin = 0, o_bl = 0, o_be = 0, o_w2 = 0;
   float b2 = 0.f;
 };
 
-void pack_chain_f32(const float *p, int L, ChainPack &P) {
+template <class T>
+void put(std::vector<unsigned char> &out, T v) {
+  const unsigned char *b = reinterpret_cast<const unsigned char *>(&v);
+  out.insert(out.end(), b, b + sizeof(T));
+}
+
+void pack_chain(const float *p, int L, int prec, ChainPack &P) {
   using hf::kH;
   using hf::kKS;
   using hf::kNT;
   const Layout lay(hf::kIn, kH, L);
-  std::vector<float> &out = P.buf;
-  out.clear();
   auto layer_w = [&](int l) { return p + lay.w_l + (int64_t)l * ((int64_t)kH * 2 * kH + kH); };
-  P.o_stream = 0;
-  for (int c = 0; c < hf::chain_chunks(L); ++c)
-    for (int j = 0; j < 8; ++j)
-      for (int lane = 0; lane < 64; ++lane)
-        for (int cc = 0; cc < 4; ++cc) {
-          if (c < 16 * L) {
-            const int l = c / 16, gi = c % 16;
-            const int s = 4 * gi + (j >> 1), nt = 4 * (j & 1) + cc;
-            const int k = (s < kKS ? 0 : kH) + kperm(s % kKS, lane);
-            out.push_back(layer_w(l)[(int64_t)(16 * nt + (lane & 15)) * 2 * kH + k]);
-          } else {
-            const int r = c - 16 * L, ot = r / 2, hh = r % 2;
-            const int s = 16 * hh + 2 * j + (cc >> 1), pq = cc & 1;
-            out.push_back(p[lay.w_e + (int64_t)(16 * ot + (lane & 15)) * 2 * kH + pq * kH + kperm(s, lane)]);
+  auto q = [&](float v) { return prec == hf::kPrecBF16 ? bf16_to_f32(to_bf16(v)) : v; };
+  std::vector<unsigned char> &out = P.stream;
+  out.clear();
+  if (prec == hf::kPrecF32) {
+    for (int c = 0; c < hf::chain_chunks(L, prec); ++c)
+      for (int j = 0; j < 8; ++j)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int cc = 0; cc < 4; ++cc) {
+            float v;
+            if (c < 16 * L) {
+              const int l = c / 16, gi = c % 16;
+              const int s = 4 * gi + (j >> 1), nt = 4 * (j & 1) + cc;
+              const int k = (s < kKS ? 0 : kH) + kperm(s % kKS, lane);
+              v = layer_w(l)[(int64_t)(16 * nt + (lane & 15)) * 2 * kH + k];
+            } else {
+              const int r = c - 16 * L, ot = r / 2, hh = r % 2;
+              const int s = 16 * hh + 2 * j + (cc >> 1), pq = cc & 1;
+              v = p[lay.w_e + (int64_t)(16 * ot + (lane & 15)) * 2 * kH + pq * kH + kperm(s, lane)];
+            }
+            put(out, v);
           }
+  } else {
+    const int terms = prec == hf::kPrecF16x3 ? 2 : 1;
+    // one 16-byte fragment (8 values) of row `row`, k-block kb, column offset kbase
+    auto frag = [&](const float *W, int64_t ld, int row, int kbase, int kb, int lane, int term) {
+      for (int e = 0; e < 8; ++e) {
+        const int k = kbase + 16 * (2 * kb + (e >> 2)) + 4 * (lane >> 4) + (e & 3);
+        const float w = W[(int64_t)row * ld + k];
+        if (prec == hf::kPrecBF16) {
+          put(out, to_bf16(w));
+        } else {
+          const _Float16 hi = (_Float16)w;
+          const _Float16 lo = (_Float16)(w - (float)hi);
+          put(out, f16_bits(term == 0 ? hi : lo));
         }
-  P.o_win = (int64_t)out.size();
+      }
+    };
+    for (int l = 0; l < L; ++l)
+      for (int nth = 0; nth < 2; ++nth)
+        for (int kb = 0; kb < 4; ++kb)
+          for (int j = 0; j < 8; ++j)
+            for (int t = 0; t < terms; ++t)
+              for (int lane = 0; lane < 64; ++lane) {
+                const int nt = 4 * nth + (j >> 1), ab = j & 1;
+                frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, t);
+              }
+    for (int ot = 0; ot < kNT; ++ot)
+      for (int j = 0; j < 8; ++j)
+        for (int t = 0; t < terms; ++t)
+          for (int lane = 0; lane < 64; ++lane) {
+            const int kb = j >> 1, pq = j & 1;
+            frag(p + lay.w_e, 2 * kH, 16 * ot + (lane & 15), pq * kH, kb, lane, t);
+          }
+  }
+  std::vector<float> &sm = P.small;
+  sm.clear();
+  P.o_win = 0;
   for (int j = 0; j < 2; ++j)
     for (int lane = 0; lane < 64; ++lane)
       for (int cc = 0; cc < 4; ++cc) {
         const int nt = 4 * j + cc;
-        out.push_back(p[lay.w_in + (int64_t)(16 * nt + (lane & 15)) * hf::kIn + (lane >> 4)]);
+        sm.push_back(q(p[lay.w_in + (int64_t)(16 * nt + (lane & 15)) * hf::kIn + (lane >> 4)]));
       }
-  P.o_bin = (int64_t)out.size();
-  out.insert(out.end(), p + lay.b_in, p + lay.b_in + kH);
-  P.o_bl = (int64_t)out.size();
-  for (int l = 0; l < L; ++l) out.insert(out.end(), layer_w(l) + (int64_t)kH * 2 * kH, layer_w(l) + (int64_t)kH * 2 * kH + kH);
-  P.o_be = (int64_t)out.size();
-  out.insert(out.end(), p + lay.b_e, p + lay.b_e + kH);
-  P.o_w2 = (int64_t)out.size();
-  out.insert(out.end(), p + lay.w_2, p + lay.w_2 + kH);
+  P.o_bin = (int64_t)sm.size();
+  sm.insert(sm.end(), p + lay.b_in, p + lay.b_in + kH);
+  P.o_bl = (int64_t)sm.size();
+  for (int l = 0; l < L; ++l) sm.insert(sm.end(), layer_w(l) + (int64_t)kH * 2 * kH, layer_w(l) + (int64_t)kH * 2 * kH + kH);
+  P.o_be = (int64_t)sm.size();
+  sm.insert(sm.end(), p + lay.b_e, p + lay.b_e + kH);
+  P.o_w2 = (int64_t)sm.size();
+  for (int i = 0; i < kH; ++i) sm.push_back(q(p[lay.w_2 + i]));
   P.b2 = p[lay.b_2];
 }
 
@@ -167,8 +238,8 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
   if (!host_params) return fail(HF_EINVAL, "hf_model_create: host_params is NULL");
   if (in_dim <= 0 || hidden <= 0 || layers < 0)
     return fail(HF_EINVAL, "hf_model_create: dimensions must be positive");
-  if (wdtype != HF_WDTYPE_F32)
-    return fail(HF_EUNSUPPORTED, "hf_model_create: only HF_WDTYPE_F32 is implemented in this build");
+  if (wdtype != HF_WDTYPE_F32 && wdtype != HF_WDTYPE_BF16 && wdtype != HF_WDTYPE_F16X3)
+    return fail(HF_EINVAL, "hf_model_create: unknown wdtype");
   if (int rc = check_device()) return rc;
 
   const Layout lay(in_dim, hidden, layers);
@@ -181,8 +252,7 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
 
   // natural copy (graph path) followed by the packed copy (chain path)
   ChainPack pk;
-  if (m->chain_ok) pack_chain_f32(host_params, layers, pk);
-  const std::vector<float> &packed = pk.buf;
+  if (m->chain_ok) pack_chain(host_params, layers, wdtype, pk);
   // natural layer weights are split into contiguous [L][H][2H] and [L][H]
   std::vector<float> nat((size_t)lay.total);
   {
@@ -203,16 +273,21 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
     put(lay.w_2, hidden);
     put(lay.b_2, 1);
   }
-  const size_t nat_pad = (nat.size() + 63) & ~size_t(63);
-  const size_t bytes = sizeof(float) * (nat_pad + packed.size());
+  const size_t nat_bytes = (sizeof(float) * nat.size() + 255) & ~size_t(255);
+  const size_t stream_bytes = (pk.stream.size() + 255) & ~size_t(255);
+  const size_t bytes = nat_bytes + stream_bytes + sizeof(float) * pk.small.size();
   hipError_t e = hipMalloc(&m->dev, bytes);
   if (e != hipSuccess) {
     delete m;
     return fail(HF_ENOMEM, std::string("hf_model_create: hipMalloc: ") + hipGetErrorString(e));
   }
-  e = hipMemcpy(m->dev, nat.data(), sizeof(float) * nat.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess && !packed.empty())
-    e = hipMemcpy(m->dev + nat_pad, packed.data(), sizeof(float) * packed.size(), hipMemcpyHostToDevice);
+  char *base = reinterpret_cast<char *>(m->dev);
+  e = hipMemcpy(base, nat.data(), sizeof(float) * nat.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !pk.stream.empty())
+    e = hipMemcpy(base + nat_bytes, pk.stream.data(), pk.stream.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !pk.small.empty())
+    e = hipMemcpy(base + nat_bytes + stream_bytes, pk.small.data(), sizeof(float) * pk.small.size(),
+                  hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(m->dev);
     delete m;
@@ -235,9 +310,10 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
     g.b_2 = d + o;
   }
   if (m->chain_ok) {
-    const float *d = m->dev + nat_pad;
+    const float *d = reinterpret_cast<const float *>(base + nat_bytes + stream_bytes);
     hf::ChainW &c = m->chain;
-    c.stream = d + pk.o_stream;
+    c.stream = base + nat_bytes;
+    c.prec = wdtype;
     c.win = d + pk.o_win;
     c.bin = d + pk.o_bin;
     c.bl = d + pk.o_bl;

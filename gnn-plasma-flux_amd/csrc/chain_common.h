@@ -1,37 +1,28 @@
-// Fused FluxGNN message passing on the periodic 1-D chain, float32 MFMA.
+// Shared machinery of the chain kernels (chain_f32.hip, chain_k32.hip):
+// lane-shift neighbours, the LDS weight ring, and the two kernel bodies
+// (FluxGNN.forward on B chains; the persistent hybrid rollout) written once
+// over a precision "core" that supplies the GNN forward.
 //
-// Reference: src/flux_gnn.py:40-67 (forward), src/graph_constructor.py:34-38
-// (chain edges), src/hybrid_solver.py:34-73 (the step / rollout it feeds).
+// Layout conventions shared by every core (one wave = 64 cells of one IC):
+//   A 16x16 MFMA accumulator tile of a transposed GEMM Out^T = W X^T holds, in
+//   lane l, cell m = 16*mt + (l&15) and features n = 16*nt + 4*(l>>4) + r,
+//   r = 0..3.  Cells therefore lie along the 16 lanes of a DPP row: the chain
+//   neighbours m-1 / m+1 are row_shr:1 / row_shl:1, with the lane that falls
+//   off the row patched from the adjacent m-tile by row_ror (periodic wrap).
 //
-// Mapping (one wave = 64 cells of one IC, hidden state resident in VGPRs):
-//   Every GEMM is computed transposed, Out^T[n][m] = sum_k W[n][k] X[m][k], on
-//   v_mfma_f32_16x16x4_f32 tiles with A = weights (rows n), B = activations
-//   (columns m = cells).  Lane l of a 16x16 accumulator then holds cell
-//   m = 16*mt + (l&15) and features n = 16*nt + 4*(l>>4) + r, r = 0..3 — which
-//   is directly the B-operand fragment of the next layer if the k order of a
-//   k-step is (nt, r) -> k = 16*nt + 4*(l>>4) + r.  The weight A fragments are
-//   packed on the host in that permuted k order (capi.cpp), so activations
-//   never leave registers between layers.
-//   Cells lie along the 16 lanes of a DPP row, so the chain neighbours i-1 /
-//   i+1 of the mean aggregation (deg = 2 on the chain, src/flux_gnn.py:55-59)
-//   are row_shr:1 / row_shl:1, with the lane that falls off the row patched
-//   from the adjacent m-tile by row_ror (periodic wrap inside the IC).
-//   The edge MLP uses the P/Q split: z(i->j) = W_a h_i + W_b h_j + b, so P and
-//   Q are per-node GEMMs (K=128) and each edge only adds a shifted pair.
-//
-// Weight stream: a workgroup is 4 waves (4 ICs, one per SIMD) that consume the
-// same 640 KiB weight stream in lockstep.  The stream is cut into 8 KiB chunks
-// (4 k-steps of an update layer, or 16 k-steps of the readout) and staged
-// through a 4-slot LDS ring by global_load_lds (LDS-DMA, no registers in
-// flight): chunk p+2 is issued while chunk p feeds the MFMAs, each wave moving
-// a quarter of every chunk.  Per chunk: counted vmcnt for the wave's own DMA,
-// one s_barrier, issue p+2, ds_read_b128 the fragments.  Each weight byte
-// leaves L2 once per workgroup instead of once per wave.
+// Weight ring: a workgroup is 4 waves (4 ICs or windows, one per SIMD) that
+// consume the same packed weight stream in lockstep.  The stream is a list of
+// equal chunks staged through a 4-slot LDS ring by global_load_lds (LDS-DMA,
+// no registers in flight): chunk p+2 is issued while chunk p feeds the MFMAs,
+// each wave moving a quarter of every chunk.  Per chunk: counted vmcnt for the
+// wave's own DMA, one s_barrier, issue p+2, ds_read_b128 the fragments.
+#pragma once
+
 #include "hf_device.h"
 #include "hf_internal.h"
 
 namespace hf {
-namespace {
+namespace chain {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
@@ -85,12 +76,10 @@ __device__ __forceinline__ f4 ldf4(const float *p) { return *reinterpret_cast<co
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ------------------------------------------------------------------ LDS plan
-constexpr int kWaves = 4;                               // one IC (item) per wave
+constexpr int kWaves = 4;  // one IC (item) per wave
 constexpr int kRingSlots = 4;
-constexpr int kRingFloats = kRingSlots * kChunkFloats;  // 32 KiB
 constexpr int kSmallFloats = 512 + kH * (3 + kMaxChainLayers);  // win, bin, be, w2, bl[L]
-constexpr int kWaveScratchFloats = 6 * 64 + 2 * 64;     // n,u,E,x,F,rho (+ 64 doubles)
-constexpr int kLdsFloats = kRingFloats + kSmallFloats + kWaves * kWaveScratchFloats;
+constexpr int kWaveScratchFloats = 6 * 64 + 2 * 64;           // n,u,E,x,F,rho (+ 64 doubles)
 
 struct Small {  // LDS copies of the small weight arrays
   const float *win, *bin, *bl, *be, *w2;
@@ -109,7 +98,10 @@ __device__ __forceinline__ Small stage_small(const ChainW &W, float *s) {
 }
 
 // ----------------------------------------------------------------- the ring
+// CF = chunk size in floats (2048 = 8 KiB or 4096 = 16 KiB).
+template <int CF>
 struct Ring {
+  static constexpr int kPerWave = CF / (kWaves * 256);  // 1 KiB DMA instructions per wave per chunk
   const float *src;  // packed weight stream (global)
   float *lds;        // 4 slots
   int chunks;        // chunks per forward pass
@@ -118,11 +110,11 @@ struct Ring {
   int ahead;         // chunk id of stream position pos + 2
 
   __device__ __forceinline__ void issue(int chunk, int slot) const {
-    const float *g = src + (size_t)chunk * kChunkFloats + lane * 4;
-    float *d = lds + slot * kChunkFloats;
+    const float *g = src + (size_t)chunk * CF + lane * 4;
+    float *d = lds + slot * CF;
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = 2 * wave + jj;  // this wave's quarter of the chunk
+    for (int jj = 0; jj < kPerWave; ++jj) {
+      const int j = kPerWave * wave + jj;  // this wave's quarter of the chunk
       __builtin_amdgcn_global_load_lds(g + j * 256, (lds_void *)(d + j * 256), 16, 0, 0);
     }
   }
@@ -135,175 +127,90 @@ struct Ring {
   }
   // Wait for chunk `pos`, keep two chunks in flight, return its slot.
   __device__ __forceinline__ const float *next() {
-    // own DMA for `pos` done (only pos+1's two instructions may remain), every
+    // own DMA for `pos` done (only pos+1's instructions may remain), every
     // ds_read of this wave retired, then every wave has passed: the slot of
     // pos-2, which pos+2 is about to overwrite, is no longer read by anyone.
-    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (kPerWave == 2)
+      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     issue(ahead, (pos + 2) & (kRingSlots - 1));
     ahead = ahead + 1 == chunks ? 0 : ahead + 1;
-    const float *slot = lds + (pos & (kRingSlots - 1)) * kChunkFloats;
+    const float *slot = lds + (pos & (kRingSlots - 1)) * CF;
     ++pos;
     return slot;
   }
   __device__ __forceinline__ void drain() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 };
 
-__device__ __forceinline__ void read_chunk(const float *slot, int lane, f4 (&v)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = ldf4(slot + (j * 64 + lane) * 4);
+template <class Core>
+__device__ __forceinline__ Ring<Core::kChunkFloats> make_ring(const ChainW &W, float *ring_lds) {
+  Ring<Core::kChunkFloats> R;
+  R.src = static_cast<const float *>(W.stream);
+  R.lds = ring_lds;
+  R.chunks = chain_chunks(W.layers, W.prec);
+  R.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  R.lane = threadIdx.x & 63;
+  R.pos = 0;
+  R.ahead = 0;
+  return R;
 }
 
-// One update-layer chunk: k-steps s = 4*gi + q.  The first 8 chunks of a layer
-// read h itself, the last 8 the neighbour mean (h[i+1] + h[i-1]) / 2.
-template <int MT, int GI>
-__device__ __forceinline__ void layer_chunk(Ring &R, const f4 (&h)[MT][kNT], f4 (&acc)[MT][kNT]) {
-  f4 v[8];
-  read_chunk(R.next(), R.lane, v);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    constexpr int kHalf = kKS / 4;
-    const int s = (GI % kHalf) * 4 + q;  // k-step within its 128-wide half
-    float b[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) b[mt] = h[mt][s >> 2][s & 3];
-    if (GI >= kHalf) {
-      float bl[MT], br[MT];
-      left_nb<MT>(b, bl);
-      right_nb<MT>(b, br);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) b[mt] = __fmul_rn(__fadd_rn(br[mt], bl[mt]), 0.5f);  // index_add_ h[i+1], h[i-1]; / deg 2
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = mfma4(v[2 * q + (nt >> 2)][nt & 3], b[mt], acc[mt][nt]);
-  }
+template <class Core>
+constexpr int lds_floats() {
+  return kRingSlots * Core::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats;
 }
 
-// One readout chunk: k-steps s = 16*HH + qq for P (W_e[:, :H]) and Q (W_e[:, H:]).
-template <int MT, int HH>
-__device__ __forceinline__ void read_chunk_pq(Ring &R, const f4 (&h)[MT][kNT], f4 (&P)[MT], f4 (&Q)[MT]) {
-  f4 v[8];
-  read_chunk(R.next(), R.lane, v);
+// Readout epilogue for one output tile ot: z_fwd(i) = P(i)+b + Q(i+1),
+// z_bwd(i) = P(i+1)+b + Q(i); flux partial += w2 . ReLU(z)     (src/flux_gnn.py:62-66)
+template <int MT>
+__device__ __forceinline__ void readout_epilogue(const f4 (&P)[MT], const f4 (&Q)[MT], const f4 be, const f4 w2,
+                                                 float (&pf)[MT], float (&pb)[MT]) {
 #pragma unroll
-  for (int qq = 0; qq < 16; ++qq) {
-    const int s = 16 * HH + qq;
-    const float ap = v[qq >> 1][2 * (qq & 1)], aq = v[qq >> 1][2 * (qq & 1) + 1];
+  for (int r = 0; r < 4; ++r) {
+    float pv[MT], qv[MT], pr[MT], qr[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const float b = h[mt][s >> 2][s & 3];
-      P[mt] = mfma4(ap, b, P[mt]);
-      Q[mt] = mfma4(aq, b, Q[mt]);
+      pv[mt] = __fadd_rn(P[mt][r], be[r]);
+      qv[mt] = Q[mt][r];
+    }
+    right_nb<MT>(pv, pr);
+    right_nb<MT>(qv, qr);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      pf[mt] = fmaf(w2[r], relu(__fadd_rn(pv[mt], qr[mt])), pf[mt]);
+      pb[mt] = fmaf(w2[r], relu(__fadd_rn(pr[mt], qv[mt])), pb[mt]);
     }
   }
 }
 
-// FluxGNN forward for the MT*16 cells of this wave.  feat[mt] is the lane's
-// input feature (index l>>4 of [n,u,E,x]) of cell 16*mt + (l&15).  Returns the
-// edge fluxes of (i -> i+1) in ffwd and of (i+1 -> i) in fbwd for cell i, on
-// every lane of the cell's column.  Consumes exactly one pass of the stream.
+// The 128-feature dot product is split over the 4 lane groups of a column.
 template <int MT>
-__device__ __forceinline__ void gnn_chain(const ChainW &W, const Small &S, Ring &R, const float (&feat)[MT],
-                                          float (&ffwd)[MT], float (&fbwd)[MT]) {
-  const int lane = R.lane;
-  const int g4 = 4 * (lane >> 4);
-  f4 h[MT][kNT];
-
-  // input MLP: h0 = ReLU(W_in x + b_in), K = 4 = one MFMA per tile   (src/flux_gnn.py:49)
-  {
-    const f4 a0 = ldf4(S.win + lane * 4), a1 = ldf4(S.win + 256 + lane * 4);
-#pragma unroll
-    for (int nt = 0; nt < kNT; ++nt) {
-      const f4 bias = ldf4(S.bin + 16 * nt + g4);
-      const float a = nt < 4 ? a0[nt & 3] : a1[nt & 3];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) h[mt][nt] = relu4(mfma4(a, feat[mt], bias));
-    }
-  }
-
-  // message passing: h = ReLU(W_l [h ; (h[i+1]+h[i-1])/2] + b_l)        (src/flux_gnn.py:53-60)
-  for (int l = 0; l < W.layers; ++l) {
-    f4 acc[MT][kNT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
-    layer_chunk<MT, 0>(R, h, acc);
-    layer_chunk<MT, 1>(R, h, acc);
-    layer_chunk<MT, 2>(R, h, acc);
-    layer_chunk<MT, 3>(R, h, acc);
-    layer_chunk<MT, 4>(R, h, acc);
-    layer_chunk<MT, 5>(R, h, acc);
-    layer_chunk<MT, 6>(R, h, acc);
-    layer_chunk<MT, 7>(R, h, acc);
-    layer_chunk<MT, 8>(R, h, acc);
-    layer_chunk<MT, 9>(R, h, acc);
-    layer_chunk<MT, 10>(R, h, acc);
-    layer_chunk<MT, 11>(R, h, acc);
-    layer_chunk<MT, 12>(R, h, acc);
-    layer_chunk<MT, 13>(R, h, acc);
-    layer_chunk<MT, 14>(R, h, acc);
-    layer_chunk<MT, 15>(R, h, acc);
-#pragma unroll
-    for (int nt = 0; nt < kNT; ++nt) {
-      const f4 bias = ldf4(S.bl + l * kH + 16 * nt + g4);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) h[mt][nt] = relu4(acc[mt][nt] + bias);
-    }
-  }
-
-  // edge readout, P/Q split: z_fwd(i) = P(i) + Q(i+1), z_bwd(i) = P(i+1) + Q(i),
-  // P = W_e[:, :H] h, Q = W_e[:, H:] h; flux = w2 . ReLU(z + b_e) + b2    (src/flux_gnn.py:62-66)
-  float pf[MT], pb[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
-  for (int ot = 0; ot < kNT; ++ot) {
-    f4 P[MT], Q[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) P[mt] = Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
-    read_chunk_pq<MT, 0>(R, h, P, Q);
-    read_chunk_pq<MT, 1>(R, h, P, Q);
-    const f4 be = ldf4(S.be + 16 * ot + g4);
-    const f4 w2 = ldf4(S.w2 + 16 * ot + g4);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float pv[MT], qv[MT], pr[MT], qr[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        pv[mt] = __fadd_rn(P[mt][r], be[r]);
-        qv[mt] = Q[mt][r];
-      }
-      right_nb<MT>(pv, pr);
-      right_nb<MT>(qv, qr);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        pf[mt] = fmaf(w2[r], relu(__fadd_rn(pv[mt], qr[mt])), pf[mt]);
-        pb[mt] = fmaf(w2[r], relu(__fadd_rn(pr[mt], qv[mt])), pb[mt]);
-      }
-    }
-  }
-  // the 128-feature dot product is split over the 4 lane groups of a column
+__device__ __forceinline__ void readout_finish(float (&pf)[MT], float (&pb)[MT], float b2, float (&ffwd)[MT],
+                                               float (&fbwd)[MT]) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     pf[mt] += __shfl_xor(pf[mt], 16, 64);
     pf[mt] += __shfl_xor(pf[mt], 32, 64);
     pb[mt] += __shfl_xor(pb[mt], 16, 64);
     pb[mt] += __shfl_xor(pb[mt], 32, 64);
-    ffwd[mt] = pf[mt] + W.b2;
-    fbwd[mt] = pb[mt] + W.b2;
+    ffwd[mt] = pf[mt] + b2;
+    fbwd[mt] = pb[mt] + b2;
   }
 }
 
-__device__ __forceinline__ Ring make_ring(const ChainW &W, float *ring_lds) {
-  Ring R;
-  R.src = W.stream;
-  R.lds = ring_lds;
-  R.chunks = chain_chunks(W.layers);
-  R.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  R.lane = threadIdx.x & 63;
-  R.pos = 0;
-  R.ahead = 0;
-  return R;
+// Input MLP: h0 = ReLU(W_in x + b_in), K = 4 = one f32 MFMA per tile  (src/flux_gnn.py:49)
+template <int MT>
+__device__ __forceinline__ void input_layer(const Small &S, int lane, const float (&feat)[MT], f4 (&h)[MT][kNT]) {
+  const int g4 = 4 * (lane >> 4);
+  const f4 a0 = ldf4(S.win + lane * 4), a1 = ldf4(S.win + 256 + lane * 4);
+#pragma unroll
+  for (int nt = 0; nt < kNT; ++nt) {
+    const f4 bias = ldf4(S.bin + 16 * nt + g4);
+    const float a = nt < 4 ? a0[nt & 3] : a1[nt & 3];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) h[mt][nt] = relu4(mfma4(a, feat[mt], bias));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -312,7 +219,7 @@ __device__ __forceinline__ Ring make_ring(const ChainW &W, float *ring_lds) {
 //  EXACT: nx == 16*MT, the wave owns the whole periodic IC, every face exact.
 //  else : MT == 4 window of 64 cells starting at w*55-4 (mod nx); faces
 //         [4,58] of the window (55 per window) are exact, the rest discarded.
-template <int MT, bool EXACT>
+template <class Core, int MT, bool EXACT>
 __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const float *__restrict__ nf,
                                                             const float *__restrict__ state,
                                                             int64_t ld_state,
@@ -320,10 +227,11 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
                                                             int nwin, int64_t items,
                                                             float *__restrict__ fe,
                                                             float *__restrict__ ff) {
-  __shared__ f4 lds4[kLdsFloats / 4];
+  constexpr int kRingFloats = kRingSlots * Core::kChunkFloats;
+  __shared__ f4 lds4[lds_floats<Core>() / 4];
   float *lds = reinterpret_cast<float *>(lds4);
   const Small S = stage_small(W, lds + kRingFloats);
-  Ring R = make_ring(W, lds);
+  auto R = make_ring<Core>(W, lds);
   const int lane = R.lane, j = lane & 15, g = lane >> 4;
   const int64_t item_raw = (int64_t)blockIdx.x * kWaves + R.wave;
   const bool live = item_raw < items;
@@ -344,7 +252,7 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
   __syncthreads();  // small weights staged (no DMA in flight yet)
   R.prime();
   float f_fwd[MT], f_bwd[MT];
-  gnn_chain<MT>(W, S, R, feat, f_fwd, f_bwd);
+  Core::template gnn<MT>(W, S, R, feat, f_fwd, f_bwd);
   R.drain();
   if (!live) return;
 #pragma unroll
@@ -368,19 +276,20 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
 // T steps of GNN -> symmetrise -> continuity -> Burgers -> spectral Poisson
 // with the IC's state in LDS (src/hybrid_solver.py:34-73).  The weight stream
 // runs continuously across steps.
-template <int MT>
+template <class Core, int MT>
 __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
     ChainW W, const float *__restrict__ state0, float *__restrict__ state_final,
     const float *__restrict__ x, const double *__restrict__ pc, int B, int T, float c, float dt,
     float *__restrict__ traj, float *__restrict__ flux_traj, float *__restrict__ metrics) {
   constexpr int NX = 16 * MT;
-  __shared__ f4 lds4[kLdsFloats / 4];
+  constexpr int kRingFloats = kRingSlots * Core::kChunkFloats;
+  __shared__ f4 lds4[lds_floats<Core>() / 4];
   float *lds = reinterpret_cast<float *>(lds4);
   const Small S = stage_small(W, lds + kRingFloats);
-  Ring R = make_ring(W, lds);
+  auto R = make_ring<Core>(W, lds);
   const int lane = R.lane, j = lane & 15, g = lane >> 4;
   float *scratch = lds + kRingFloats + kSmallFloats + R.wave * kWaveScratchFloats;
-  float *s_st = scratch;          // n | u | E | x   (4 x 64)
+  float *s_st = scratch;  // n | u | E | x   (4 x 64)
   float *s_F = scratch + 4 * 64;
   float *s_rho = scratch + 5 * 64;
   double *s_c = reinterpret_cast<double *>(scratch + 6 * 64);
@@ -415,7 +324,7 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) feat[mt] = s_st[g * 64 + 16 * mt + j];
     float f_fwd[MT], f_bwd[MT];
-    gnn_chain<MT>(W, S, R, feat, f_fwd, f_bwd);
+    Core::template gnn<MT>(W, S, R, feat, f_fwd, f_bwd);
     if (g == 0) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) s_F[16 * mt + j] = face_flux(f_fwd[mt], f_bwd[mt]);
@@ -446,57 +355,56 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
   for (int i = lane; i < 3 * NX; i += 64) out[i] = s_st[(i / NX) * 64 + i % NX];
 }
 
-template <int MT, bool EXACT>
+// ------------------------------------------------------------------ launchers
+template <class Core, int MT, bool EXACT>
 hipError_t flux_launch(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
                        int nx, int nwin, int64_t items, float *fe, float *ff, hipStream_t s) {
   const int64_t blocks = (items + kWaves - 1) / kWaves;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((chain_flux_kernel<MT, EXACT>), dim3((unsigned)blocks), dim3(64 * kWaves), 0, s, w, nf,
-                     state, ld_state, x, nx, nwin, items, fe, ff);
+  hipLaunchKernelGGL((chain_flux_kernel<Core, MT, EXACT>), dim3((unsigned)blocks), dim3(64 * kWaves), 0, s, w,
+                     nf, state, ld_state, x, nx, nwin, items, fe, ff);
   return hipGetLastError();
 }
 
-template <int MT>
-hipError_t rollout_mt(const ChainW &w, const float *state0, float *state_final, const float *x,
-                      const double *pc, int B, int T, float c, float dt, float *traj,
-                      float *flux_traj, float *metrics, hipStream_t s) {
-  const int blocks = (B + kWaves - 1) / kWaves;
-  hipLaunchKernelGGL(chain_rollout_kernel<MT>, dim3(blocks), dim3(64 * kWaves), 0, s, w, state0, state_final,
-                     x, pc, B, T, c, dt, traj, flux_traj, metrics);
-  return hipGetLastError();
-}
-
-}  // namespace
-
-hipError_t launch_chain_flux(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
-                             const float *x, int B, int nx, float *flux_edge, float *flux_face,
-                             hipStream_t s) {
+template <class Core>
+hipError_t launch_flux_core(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
+                            const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (nx) {
-    case 16: return flux_launch<1, true>(w, nf, state, ld_state, x, nx, 1, B, flux_edge, flux_face, s);
-    case 32: return flux_launch<2, true>(w, nf, state, ld_state, x, nx, 1, B, flux_edge, flux_face, s);
-    case 48: return flux_launch<3, true>(w, nf, state, ld_state, x, nx, 1, B, flux_edge, flux_face, s);
-    case 64: return flux_launch<4, true>(w, nf, state, ld_state, x, nx, 1, B, flux_edge, flux_face, s);
+    case 16: return flux_launch<Core, 1, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
+    case 32: return flux_launch<Core, 2, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
+    case 48: return flux_launch<Core, 3, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
+    case 64: return flux_launch<Core, 4, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
     default: {
       const int nwin = (nx + kWinFaces - 1) / kWinFaces;
-      return flux_launch<4, false>(w, nf, state, ld_state, x, nx, nwin, (int64_t)B * nwin, flux_edge,
-                                   flux_face, s);
+      return flux_launch<Core, 4, false>(w, nf, state, ld_state, x, nx, nwin, (int64_t)B * nwin, fe, ff, s);
     }
   }
 }
 
-hipError_t launch_chain_rollout(const ChainW &w, const float *state0, float *state_final,
-                                const float *x, const double *pc, int B, int nx, int T, float c,
-                                float dt, float *traj, float *flux_traj, float *metrics,
-                                hipStream_t s) {
+template <class Core, int MT>
+hipError_t rollout_launch(const ChainW &w, const float *state0, float *state_final, const float *x,
+                          const double *pc, int B, int T, float c, float dt, float *traj, float *flux_traj,
+                          float *metrics, hipStream_t s) {
+  const int blocks = (B + kWaves - 1) / kWaves;
+  hipLaunchKernelGGL((chain_rollout_kernel<Core, MT>), dim3(blocks), dim3(64 * kWaves), 0, s, w, state0,
+                     state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics);
+  return hipGetLastError();
+}
+
+template <class Core>
+hipError_t launch_rollout_core(const ChainW &w, const float *state0, float *state_final, const float *x,
+                               const double *pc, int B, int nx, int T, float c, float dt, float *traj,
+                               float *flux_traj, float *metrics, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (nx) {
-    case 16: return rollout_mt<1>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 32: return rollout_mt<2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 48: return rollout_mt<3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 64: return rollout_mt<4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 16: return rollout_launch<Core, 1>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 32: return rollout_launch<Core, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 48: return rollout_launch<Core, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 64: return rollout_launch<Core, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
     default: return hipErrorInvalidValue;
   }
 }
 
+}  // namespace chain
 }  // namespace hf

@@ -23,25 +23,32 @@ constexpr int kWinCells = 64;
 constexpr int kWinHalo = 4;
 constexpr int kWinFaces = kWinCells - 2 * kWinHalo - 1;  // 55
 
-// Packed float32 weights (device) for the chain kernels; see capi.cpp
-// pack_chain_f32 for the exact index maps.  The big matrices form ONE stream
-// of 8 KiB chunks, consumed in order through an LDS ring:
-//   chunk c <  16L : update layer l = c/16, k-steps 4*(c%16) .. +3, all 8 output tiles
-//   chunk c >= 16L : edge readout tile ot = (c-16L)/2, k-steps 16*((c-16L)%2) .. +15, P and Q
-// Each chunk is [j 8][lane 64][4] floats, so one wave instruction moves 1 KiB.
-constexpr int kChunkFloats = 8 * 64 * 4;
+// Packed weights (device) for the chain kernels; see capi.cpp pack_chain_*
+// for the exact index maps.  The big matrices form ONE stream of chunks,
+// consumed in order through an LDS ring (chain_common.h):
+//  f32   (v_mfma_f32_16x16x4_f32): 8 KiB chunks, 16 per update layer (4 k-steps
+//        each, [h ; agg] input order) + 2 per readout output tile.
+//  k32   (v_mfma_f32_16x16x32_{f16,bf16}): per update layer 8 chunks, (k-block
+//        kb = 0..3) x (W_a | W_b), then one chunk per readout output tile.
+//        f16x3: 16 KiB chunks of (hi, lo) fp16 fragment pairs; bf16: 8 KiB.
+// Each chunk is [fragment j][lane 64][16 B], so one wave instruction moves 1 KiB.
+enum ChainPrec { kPrecF32 = HF_WDTYPE_F32, kPrecBF16 = HF_WDTYPE_BF16, kPrecF16x3 = HF_WDTYPE_F16X3 };
 constexpr int kMaxChainLayers = 8;
-__host__ __device__ inline int chain_chunks(int layers) { return 16 * layers + 2 * kNT; }
+__host__ __device__ inline int chain_chunks(int layers, int prec) {
+  return prec == kPrecF32 ? 16 * layers + 2 * kNT : 8 * layers + kNT;
+}
+__host__ __device__ inline int chain_chunk_bytes(int prec) { return prec == kPrecF16x3 ? 16384 : 8192; }
 
 struct ChainW {
-  const float *stream;  // [chain_chunks(L)][8][64][4]
-  const float *win;     // [2][64][4]   input layer A fragments
+  const void *stream;   // [chain_chunks][chunk]
+  const float *win;     // [2][64][4]   input layer A fragments (f32; bf16-rounded in bf16 mode)
   const float *bin;     // [kH]
   const float *bl;      // [L][kH]
   const float *be;      // [kH]
   const float *w2;      // [kH]
   float b2;
   int layers;
+  int prec;             // ChainPrec
 };
 
 // Natural-layout float32 weights (device) for the generic-graph path.
@@ -53,17 +60,35 @@ struct GraphW {
   int in_dim, hidden, layers;
 };
 
+// Per-precision launchers (chain_f32.hip, chain_k32.hip); the generic entry
+// points below dispatch on ChainW::prec.
+hipError_t launch_chain_flux_f32(const ChainW &, const float *, const float *, int64_t, const float *, int, int,
+                                 float *, float *, hipStream_t);
+hipError_t launch_chain_flux_k32(const ChainW &, const float *, const float *, int64_t, const float *, int, int,
+                                 float *, float *, hipStream_t);
+hipError_t launch_chain_rollout_f32(const ChainW &, const float *, float *, const float *, const double *, int, int,
+                                    int, float, float, float *, float *, float *, hipStream_t);
+hipError_t launch_chain_rollout_k32(const ChainW &, const float *, float *, const float *, const double *, int, int,
+                                    int, float, float, float *, float *, float *, hipStream_t);
+
 // Chain flux.  Feature source: AoS node features [B*nx][4] (nf != nullptr)
 // or SoA state [B][3][nx] with IC stride ld_state floats + x[nx].
-hipError_t launch_chain_flux(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
-                             const float *x, int B, int nx, float *flux_edge, float *flux_face,
-                             hipStream_t s);
+inline hipError_t launch_chain_flux(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
+                                    const float *x, int B, int nx, float *flux_edge, float *flux_face,
+                                    hipStream_t s) {
+  return w.prec == kPrecF32 ? launch_chain_flux_f32(w, nf, state, ld_state, x, B, nx, flux_edge, flux_face, s)
+                            : launch_chain_flux_k32(w, nf, state, ld_state, x, B, nx, flux_edge, flux_face, s);
+}
 
 // Persistent fused rollout for nx in {16,32,48,64}.
-hipError_t launch_chain_rollout(const ChainW &w, const float *state0, float *state_final,
-                                const float *x, const double *pc, int B, int nx, int T, float c,
-                                float dt, float *traj, float *flux_traj, float *metrics,
-                                hipStream_t s);
+inline hipError_t launch_chain_rollout(const ChainW &w, const float *state0, float *state_final,
+                                       const float *x, const double *pc, int B, int nx, int T, float c,
+                                       float dt, float *traj, float *flux_traj, float *metrics,
+                                       hipStream_t s) {
+  return w.prec == kPrecF32
+             ? launch_chain_rollout_f32(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, s)
+             : launch_chain_rollout_k32(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, s);
+}
 
 // One FV + Poisson update (any nx).  face_flux != nullptr => hybrid update
 // with that F; nullptr => classical (F = n*u, viscosity).  IC strides in floats.

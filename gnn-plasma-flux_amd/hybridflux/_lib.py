@@ -17,6 +17,7 @@ HF_EHIP = -3
 HF_ENOMEM = -4
 HF_WDTYPE_F32 = 0
 HF_WDTYPE_BF16 = 1
+HF_WDTYPE_F16X3 = 2
 HF_NUM_METRICS = 4
 
 # name -> (restype, argtypes); mirrors include/hybridflux.h exactly.

@@ -55,10 +55,23 @@ def dims_of(sd):
     return in_dim, hidden, layers
 
 
-class DeviceModel:
-    """A packed, read-only copy of FluxGNN weights on one device (hf_model_t)."""
+PRECISIONS = {"f32": _lib.HF_WDTYPE_F32, "bf16": _lib.HF_WDTYPE_BF16, "f16x3": _lib.HF_WDTYPE_F16X3}
 
-    def __init__(self, state_dict, device):
+
+class DeviceModel:
+    """A packed, read-only copy of FluxGNN weights on one device (hf_model_t).
+
+    precision selects the chain kernels' matrix-core arithmetic:
+      "f32"   v_mfma_f32_16x16x4_f32, exact float32 (parity reference)
+      "f16x3" fp16 hi+lo split of weights and activations, 3 products on
+              v_mfma_f32_16x16x32_f16, f32 accumulate: float32-level accuracy
+      "bf16"  bf16 weights and activations, f32 accumulate (BASELINE config 4)
+    The generic-graph path always computes in float32."""
+
+    def __init__(self, state_dict, device, precision="f32"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
+        self.precision = precision
         self.in_dim, self.hidden, self.layers = dims_of(state_dict)
         self.device = torch.device(device)
         flat = flatten_params(state_dict, self.layers)
@@ -68,7 +81,7 @@ class DeviceModel:
         self.handle = c_void_p()
         with torch.cuda.device(self.device):
             check(lib().hf_model_create(flat.ctypes.data_as(c_void_p), self.in_dim, self.hidden,
-                                        self.layers, _lib.HF_WDTYPE_F32, self.handle))
+                                        self.layers, PRECISIONS[precision], self.handle))
 
     @property
     def chain_ok(self):

@@ -35,8 +35,9 @@ class _NoBackward(torch.autograd.Function):
 class FluxGNN(nn.Module):
     """Message-passing GNN predicting one flux per directed edge."""
 
-    def __init__(self, input_dim=2, hidden_dim=32, num_layers=2):
+    def __init__(self, input_dim=2, hidden_dim=32, num_layers=2, precision="f32"):
         super().__init__()
+        self.precision = precision  # chain-kernel arithmetic: "f32" | "f16x3" | "bf16" (engine.DeviceModel)
         self.input_dim = input_dim
         self.hidden_dim = hidden_dim
         self.num_layers = num_layers
@@ -49,7 +50,7 @@ class FluxGNN(nn.Module):
 
     # -- weights -------------------------------------------------------------
     def _signature(self):
-        return tuple((p.data_ptr(), p._version, str(p.device)) for p in self.parameters())
+        return (self.precision,) + tuple((p.data_ptr(), p._version, str(p.device)) for p in self.parameters())
 
     def device_model(self, device):
         """The packed libhybridflux weight handle for `device` (rebuilt when any
@@ -62,7 +63,7 @@ class FluxGNN(nn.Module):
             if hit is not None:
                 hit[1].close()
             sd = {k: v for k, v in self.state_dict().items()}
-            self._packed[key] = (sig, engine.DeviceModel(sd, device))
+            self._packed[key] = (sig, engine.DeviceModel(sd, device, self.precision))
         return self._packed[key][1]
 
     def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate packed copies

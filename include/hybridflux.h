@@ -43,6 +43,8 @@ extern "C" {
 
 #define HF_WDTYPE_F32 0     /* weights and arithmetic in float32 (parity mode) */
 #define HF_WDTYPE_BF16 1    /* bf16 MLP weights/activations, f32 accumulate    */
+#define HF_WDTYPE_F16X3 2   /* fp32-accurate: fp16 hi+lo split of weights and
+                               activations, 3 MFMA products, f32 accumulate   */
 
 /* Number of per-(IC, step) rollout metrics written by hf_run / hf_fv_step:
  * [0] energy 0.5*mean(u^2+E^2)  [1] charge mean(n)  [2] 1.0 if every state
@@ -72,7 +74,11 @@ int hf_device_count(void);
  *   edge_mlp.2.weight [1][H], edge_mlp.2.bias [1].
  * The handle packs them into the MFMA fragment order of the fused chain
  * kernels (when in_dim==4 && H==128) and keeps the natural layout for the
- * generic-graph path.  wdtype: HF_WDTYPE_F32 or HF_WDTYPE_BF16.
+ * generic-graph path (always float32).  wdtype selects the chain kernels'
+ * MFMA arithmetic: HF_WDTYPE_F32 (v_mfma_f32_16x16x4_f32, exact f32),
+ * HF_WDTYPE_F16X3 (v_mfma_f32_16x16x32_f16 on a two-term fp16 split of both
+ * operands, 3 products: fp32-level accuracy at ~5x the f32 MFMA rate) or
+ * HF_WDTYPE_BF16 (bf16 weights and activations, config 4).
  */
 int hf_model_create(const float *host_params, int in_dim, int hidden, int layers,
                     int wdtype, hf_model_t *out);
