@@ -30,6 +30,7 @@ import torch.distributed as dist  # noqa: E402
 GNN_FLOP_PER_CELL_STEP = 329_216   # input 1,024 + layers 262,144 + P/Q readout 66,048
 STATE_BYTES_PER_CELL_STEP = 24     # read (n,u,E) + write (n,u,E) float32
 PEAK_F32_MFMA_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+PEAK_F16_MFMA_TFLOPS = 2500.0      # MI355X_MICROARCH.md: dense FP16/BF16 matrix peak (no sparsity)
 PEAK_HBM_GBS = 8000.0
 METRIC = "hybrid rollout timesteps/sec (batched ICs) at 1/2/4/8 MI355X"
 
@@ -74,6 +75,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--ics-per-gpu", type=int, default=4096)
     ap.add_argument("--nx", type=int, default=64)
+    ap.add_argument("--dt", type=float, default=None,
+                    help="time step (default 5e-3 * 64/nx: the reference dt at nx=64, same dt/dx otherwise; "
+                         "the reference itself NaNs by step 17-33 at nx=1024 with dt=5e-3)")
     ap.add_argument("--weights", default=os.path.join(ROOT, "tests", "golden", "weights_W1_r3.npz"))
     ap.add_argument("--no-traj", action="store_true", help="do not record the state trajectory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -101,7 +105,8 @@ def main():
     weights = dict(np.load(args.weights, allow_pickle=False))
     B, nx, K, W = args.ics_per_gpu, args.nx, args.steps, args.warmup
     n_total = B * world
-    solver = HybridSolver(weights, radius=3, nx=nx, device=dev, precision=args.precision)
+    dt = args.dt if args.dt is not None else 5e-3 * 64.0 / nx
+    solver = HybridSolver(weights, radius=3, nx=nx, dt=dt, device=dev, precision=args.precision)
     ics = solver.baseline.initial_conditions(shard_seeds(1000, n_total, world, rank), as_tensor=True)
     stream = torch.cuda.current_stream(dev)
 
@@ -111,13 +116,15 @@ def main():
 
     # preallocate outputs so the timed region is launches only
     final = torch.empty_like(ics)
+    traj_buf = None if args.no_traj else torch.empty(B, K + 1, 3, nx, device=dev)
+    met_buf = torch.empty(B, K + 1, 4, device=dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
-    res = solver.run_batch(ics, K, traj=not args.no_traj, metrics=True, out=final)
+    res = solver.run_batch(ics, K, traj=traj_buf if traj_buf is not None else False, metrics=met_buf, out=final)
     ev1.record(stream)
     gathered = gather_ic_rows(res["metrics"][:, -1], n_total)   # RCCL all_gather of final metrics
     torch.cuda.synchronize(dev)
@@ -129,17 +136,18 @@ def main():
     # other precisions, same ICs / K / warmup, timed the same way (reported, not the headline)
     alt = {}
     for prec in [p for p in args.also.split(",") if p and p != args.precision]:
-        s2 = HybridSolver(weights, radius=3, nx=nx, device=dev, precision=prec)
+        s2 = HybridSolver(weights, radius=3, nx=nx, dt=dt, device=dev, precision=prec)
         s2.run_batch(ics, max(W, 1), traj=not args.no_traj)
+        final2 = torch.empty_like(ics)
         torch.cuda.synchronize(dev)
         a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ta = time.perf_counter()
         a0.record(stream)
-        r2 = s2.run_batch(ics, K, traj=not args.no_traj, metrics=True)
+        r2 = s2.run_batch(ics, K, traj=traj_buf if traj_buf is not None else False, metrics=met_buf, out=final2)
         a1.record(stream)
         torch.cuda.synchronize(dev)
         wall2 = time.perf_counter() - ta
-        dev_err = float((r2["final"] - final).abs().max().item())
+        dev_err = float((final2 - final).abs().max().item())
         alt[prec] = {"value": round(B * K / wall2, 1), "ms_per_step": round(wall2 / K * 1e3, 4),
                      "kernel_ms": round(a0.elapsed_time(a1), 3),
                      "max_abs_diff_vs_headline_final_state": dev_err}
@@ -156,6 +164,10 @@ def main():
         value = n_total * K / wall_max
         flop = GNN_FLOP_PER_CELL_STEP * B * nx * K
         achieved = flop / (kernel_ms * 1e-3) / 1e12
+        peak = PEAK_F32_MFMA_TFLOPS if args.precision == "f32" else PEAK_F16_MFMA_TFLOPS
+        fused = nx in (16, 32, 48, 64)
+        kernel = (f"chain_rollout_kernel<{args.precision},MT={nx // 16}> (one persistent launch)" if fused else
+                  f"chain_flux_kernel<{args.precision},window> + fv_step_kernel<hybrid> per step")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             threads = min(16, os.cpu_count() or 1)
@@ -178,14 +190,14 @@ def main():
             "dtype": {"f32": "f32", "f16x3": "f16x3 (fp32-accurate split: 3 fp16 MFMA products, f32 accumulate)",
                       "bf16": "bf16 (f32 accumulate)"}[args.precision],
             "data": "synthetic: reference IC generator seeds 1000.., fixture weights W1_r3 (1-epoch reference trainer)",
-            "config": {"workload": f"cfg3: {nx}-cell periodic chain, {B}-IC batch per GPU, FluxGNN(4,128,4) {args.precision}, "
+            "config": {"workload": f"{'cfg3' if (nx == 64 and B == 4096) else 'cfg2' if (nx == 64 and B == 256) else 'cfg4' if nx == 1024 else 'custom'}: {nx}-cell periodic chain, {B}-IC batch per GPU, FluxGNN(4,128,4) {args.precision}, "
                                    f"{K}-step persistent rollout{'' if args.no_traj else ' recording every state'}",
-                       "nx": nx, "ics_per_gpu": B, "global_ics": n_total, "parallelism": f"ic-shard x{world}"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F32_MFMA_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_MFMA_TFLOPS, 4),
+                       "nx": nx, "dt": dt, "ics_per_gpu": B, "global_ics": n_total, "parallelism": f"ic-shard x{world}"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "traffic": traffic["traffic_bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": "chain_rollout_kernel<4>", "kernel_ms": round(kernel_ms, 3),
+                         "kernel": kernel, "kernel_ms": round(kernel_ms, 3),
                          "flop_per_launch": flop,
                          "hbm_state_frac": round(STATE_BYTES_PER_CELL_STEP * B * nx * K / (kernel_ms * 1e-3)
                                                  / (PEAK_HBM_GBS * 1e9), 6)},

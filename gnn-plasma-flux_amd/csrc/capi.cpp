@@ -495,4 +495,47 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   return HF_OK;
 }
 
+int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B,
+                   int nx, int T, float c, float dt, float nu, float dx2, float *mse, float *metrics,
+                   float *metrics_cl, void *stream) {
+  if (!m) return fail(HF_EINVAL, "hf_run_compare: NULL model");
+  if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run_compare: need B >= 0, nx >= 1, T >= 0");
+  if (B == 0) return HF_OK;
+  if (!state0 || !state_final || !pc || !x || !mse) return fail(HF_EINVAL, "hf_run_compare: NULL pointer");
+  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run_compare: nx too large for the LDS solve");
+  if (int rc = chain_usable(m)) return rc;
+  hipStream_t s = as_stream(stream);
+  if (fused_nx(nx)) {
+    hf::RolloutExtras ex;
+    ex.nu = nu;
+    ex.dx2 = dx2;
+    ex.mse = mse;
+    ex.metrics_cl = metrics_cl;
+    HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, state0, state_final, x, pc, B, nx, T, c, dt, nullptr, nullptr,
+                                          metrics, s, ex),
+                 "hf_run_compare(fused)");
+    return HF_OK;
+  }
+  // generic nx: both trajectories through HBM, then the MSE reduction
+  const size_t traj_bytes = sizeof(float) * (size_t)B * (T + 1) * 3 * nx;
+  float *th = nullptr, *tc = nullptr, *fin_c = nullptr;
+  HF_CHECK_HIP(hipMallocAsync((void **)&th, traj_bytes, s), "hf_run_compare scratch");
+  if (hipMallocAsync((void **)&tc, traj_bytes, s) != hipSuccess ||
+      hipMallocAsync((void **)&fin_c, sizeof(float) * (size_t)B * 3 * nx, s) != hipSuccess) {
+    (void)hipFreeAsync(th, s);
+    if (tc) (void)hipFreeAsync(tc, s);
+    return fail(HF_ENOMEM, "hf_run_compare: trajectory scratch");
+  }
+  int rc = hf_run(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, th, nullptr, metrics, stream);
+  if (rc == HF_OK) rc = hf_run(nullptr, state0, fin_c, x, pc, B, nx, T, c, dt, nu, dx2, tc, nullptr, metrics_cl, stream);
+  hipError_t e = hipSuccess;
+  if (rc == HF_OK) e = hf::launch_traj_mse(th, tc, B, T + 1, nx, mse, s);
+  (void)hipFreeAsync(th, s);
+  (void)hipFreeAsync(tc, s);
+  (void)hipFreeAsync(fin_c, s);
+  if (rc != HF_OK) return rc;
+  HF_CHECK_HIP(e, "hf_run_compare mse");
+  return HF_OK;
+}
+
 }  // extern "C"

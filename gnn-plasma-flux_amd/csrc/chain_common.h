@@ -79,7 +79,8 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 constexpr int kWaves = 4;  // one IC (item) per wave
 constexpr int kRingSlots = 4;
 constexpr int kSmallFloats = 512 + kH * (3 + kMaxChainLayers);  // win, bin, be, w2, bl[L]
-constexpr int kWaveScratchFloats = 6 * 64 + 2 * 64;           // n,u,E,x,F,rho (+ 64 doubles)
+// per wave: n,u,E,x,F,rho | 64 doubles (Poisson column) | classical twin n,u,E,F,rho
+constexpr int kWaveScratchFloats = 6 * 64 + 2 * 64 + 5 * 64;
 
 struct Small {  // LDS copies of the small weight arrays
   const float *win, *bin, *bl, *be, *w2;
@@ -156,9 +157,16 @@ __device__ __forceinline__ Ring<Core::kChunkFloats> make_ring(const ChainW &W, f
   return R;
 }
 
+// LDS per workgroup: ring | small weights | per-wave scratch | per-wave park
+// (Core::kParkFloats: activations a core spills to LDS instead of VGPRs).
 template <class Core>
 constexpr int lds_floats() {
-  return kRingSlots * Core::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats;
+  return kRingSlots * Core::kChunkFloats + kSmallFloats + kWaves * (kWaveScratchFloats + Core::kParkFloats);
+}
+template <class Core>
+__device__ __forceinline__ float *park_of(float *lds, int wave) {
+  return lds + kRingSlots * Core::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats +
+         wave * Core::kParkFloats;
 }
 
 // Readout epilogue for one output tile ot: z_fwd(i) = P(i)+b + Q(i+1),
@@ -252,7 +260,7 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
   __syncthreads();  // small weights staged (no DMA in flight yet)
   R.prime();
   float f_fwd[MT], f_bwd[MT];
-  Core::template gnn<MT>(W, S, R, feat, f_fwd, f_bwd);
+  Core::template gnn<MT>(W, S, R, park_of<Core>(lds, R.wave), feat, f_fwd, f_bwd);
   R.drain();
   if (!live) return;
 #pragma unroll
@@ -280,7 +288,7 @@ template <class Core, int MT>
 __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
     ChainW W, const float *__restrict__ state0, float *__restrict__ state_final,
     const float *__restrict__ x, const double *__restrict__ pc, int B, int T, float c, float dt,
-    float *__restrict__ traj, float *__restrict__ flux_traj, float *__restrict__ metrics) {
+    float *__restrict__ traj, float *__restrict__ flux_traj, float *__restrict__ metrics, RolloutExtras ex) {
   constexpr int NX = 16 * MT;
   constexpr int kRingFloats = kRingSlots * Core::kChunkFloats;
   __shared__ f4 lds4[lds_floats<Core>() / 4];
@@ -293,11 +301,20 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
   float *s_F = scratch + 4 * 64;
   float *s_rho = scratch + 5 * 64;
   double *s_c = reinterpret_cast<double *>(scratch + 6 * 64);
+  float *s_cl = scratch + 8 * 64;  // classical twin n | u | E
+  float *s_Fc = scratch + 11 * 64;
+  float *s_rhoc = scratch + 12 * 64;
+  float *park = park_of<Core>(lds, R.wave);
+  const bool twin = ex.mse != nullptr;
   const int b_raw = blockIdx.x * kWaves + R.wave;
   const bool live = b_raw < B;
   const int64_t b = live ? b_raw : B - 1;
   const float *st0 = state0 + b * 3 * NX;
-  for (int i = lane; i < 3 * NX; i += 64) s_st[(i / NX) * 64 + i % NX] = st0[i];
+  for (int i = lane; i < 3 * NX; i += 64) {
+    const float v = st0[i];
+    s_st[(i / NX) * 64 + i % NX] = v;
+    if (twin) s_cl[(i / NX) * 64 + i % NX] = v;
+  }
   if (lane < NX) {
     s_st[3 * 64 + lane] = x[lane];
     s_c[lane] = pc[lane];
@@ -305,6 +322,8 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
   __syncthreads();  // small weights + per-wave state visible (no DMA in flight yet)
   float *tj = (traj && live) ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
   float *mt_out = (metrics && live) ? metrics + b * (int64_t)(T + 1) * HF_NUM_METRICS : nullptr;
+  float *mc_out = (ex.metrics_cl && live) ? ex.metrics_cl + b * (int64_t)(T + 1) * HF_NUM_METRICS : nullptr;
+  float *mse_out = (twin && live) ? ex.mse + b * (int64_t)(T + 1) * 3 : nullptr;
   float *ftj = (flux_traj && live) ? flux_traj + b * (int64_t)T * NX : nullptr;
   auto emit = [&](int t) {
     if (tj)
@@ -316,6 +335,26 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
       m.wave_reduce();
       if (lane == 0) m.store(mt_out + t * HF_NUM_METRICS, NX);
     }
+    if (mc_out) {
+      MetricAcc m;
+      m.init();
+      if (lane < NX) m.add(s_cl[lane], s_cl[64 + lane], s_cl[128 + lane]);
+      m.wave_reduce();
+      if (lane == 0) m.store(mc_out + t * HF_NUM_METRICS, NX);
+    }
+    if (mse_out) {  // scripts/evaluation/evaluate_multi_ic.py:88-90
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        double d2 = 0.0;
+        if (lane < NX) {
+          const double d = (double)s_st[ch * 64 + lane] - (double)s_cl[ch * 64 + lane];
+          d2 = d * d;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) d2 += __shfl_xor(d2, o, 64);
+        if (lane == 0) mse_out[t * 3 + ch] = (float)(d2 / NX);
+      }
+    }
   };
   emit(0);
   R.prime();
@@ -324,13 +363,14 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) feat[mt] = s_st[g * 64 + 16 * mt + j];
     float f_fwd[MT], f_bwd[MT];
-    Core::template gnn<MT>(W, S, R, feat, f_fwd, f_bwd);
+    Core::template gnn<MT>(W, S, R, park, feat, f_fwd, f_bwd);
     if (g == 0) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) s_F[16 * mt + j] = face_flux(f_fwd[mt], f_bwd[mt]);
     }
+    if (twin && lane < NX) s_Fc[lane] = __fmul_rn(s_cl[lane], s_cl[64 + lane]);  // F_n = n*u
     wave_lds_sync();
-    float n_new = 0.f, u_new = 0.f;
+    float n_new = 0.f, u_new = 0.f, nc = 0.f, uc = 0.f;
     if (lane < NX) {
       const int im = lane == 0 ? NX - 1 : lane - 1;
       const float F = s_F[lane];
@@ -338,6 +378,13 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
       u_new = velocity_hybrid(s_st[64 + lane], s_st[64 + im], s_st[128 + lane], c, dt);
       s_rho[lane] = __fsub_rn(n_new, 1.0f);
       if (ftj) ftj[(int64_t)t * NX + lane] = F;
+      if (twin) {  // BaselineSolver.step (src/baseline_solver.py:80-101)
+        const int ip = lane == NX - 1 ? 0 : lane + 1;
+        nc = continuity(s_cl[lane], s_Fc[lane], s_Fc[im], c);
+        uc = velocity_classical(s_cl[64 + lane], s_cl[64 + im], s_cl[64 + ip], s_cl[128 + lane], c, dt, ex.nu,
+                                ex.dx2);
+        s_rhoc[lane] = __fsub_rn(nc, 1.0f);
+      }
     }
     wave_lds_sync();
     if (lane < NX) {
@@ -345,6 +392,12 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
       s_st[lane] = n_new;
       s_st[64 + lane] = u_new;
       s_st[128 + lane] = E_new;
+      if (twin) {
+        const float Ec = poisson_cell(s_rhoc, s_c, lane, NX);
+        s_cl[lane] = nc;
+        s_cl[64 + lane] = uc;
+        s_cl[128 + lane] = Ec;
+      }
     }
     wave_lds_sync();
     emit(t + 1);
@@ -385,23 +438,23 @@ hipError_t launch_flux_core(const ChainW &w, const float *nf, const float *state
 template <class Core, int MT>
 hipError_t rollout_launch(const ChainW &w, const float *state0, float *state_final, const float *x,
                           const double *pc, int B, int T, float c, float dt, float *traj, float *flux_traj,
-                          float *metrics, hipStream_t s) {
+                          float *metrics, const RolloutExtras &ex, hipStream_t s) {
   const int blocks = (B + kWaves - 1) / kWaves;
   hipLaunchKernelGGL((chain_rollout_kernel<Core, MT>), dim3(blocks), dim3(64 * kWaves), 0, s, w, state0,
-                     state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics);
+                     state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex);
   return hipGetLastError();
 }
 
 template <class Core>
 hipError_t launch_rollout_core(const ChainW &w, const float *state0, float *state_final, const float *x,
                                const double *pc, int B, int nx, int T, float c, float dt, float *traj,
-                               float *flux_traj, float *metrics, hipStream_t s) {
+                               float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (nx) {
-    case 16: return rollout_launch<Core, 1>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 32: return rollout_launch<Core, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 48: return rollout_launch<Core, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 64: return rollout_launch<Core, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 16: return rollout_launch<Core, 1>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex, s);
+    case 32: return rollout_launch<Core, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex, s);
+    case 48: return rollout_launch<Core, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex, s);
+    case 64: return rollout_launch<Core, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -23,6 +23,7 @@ using namespace chain;
 
 struct CoreF32 {
   static constexpr int kChunkFloats = 2048;  // 8 KiB: 4 k-steps x 8 tiles, or 16 k-steps x (P, Q)
+  static constexpr int kParkFloats = 0;
   using R_t = Ring<kChunkFloats>;
 
   static __device__ __forceinline__ void read_chunk(const float *slot, int lane, f4 (&v)[8]) {
@@ -80,7 +81,8 @@ struct CoreF32 {
   // the edge fluxes of (i -> i+1) in ffwd and of (i+1 -> i) in fbwd for cell
   // i, on every lane of the cell's column.  Consumes one pass of the stream.
   template <int MT>
-  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, const float (&feat)[MT],
+  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, float * /*park*/,
+                                             const float (&feat)[MT],
                                              float (&ffwd)[MT], float (&fbwd)[MT]) {
     const int lane = R.lane;
     const int g4 = 4 * (lane >> 4);
@@ -143,9 +145,9 @@ hipError_t launch_chain_flux_f32(const ChainW &w, const float *nf, const float *
 
 hipError_t launch_chain_rollout_f32(const ChainW &w, const float *state0, float *state_final, const float *x,
                                     const double *pc, int B, int nx, int T, float c, float dt, float *traj,
-                                    float *flux_traj, float *metrics, hipStream_t s) {
+                                    float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
   return chain::launch_rollout_core<CoreF32>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj,
-                                             metrics, s);
+                                             metrics, ex, s);
 }
 
 }  // namespace hf

@@ -62,6 +62,9 @@ struct ModeBF16 {
 template <class M>
 struct CoreK32 {
   static constexpr int kChunkFloats = M::kChunkFloats;
+  // first output half of a layer parked in LDS while the second half runs:
+  // [mt 4][tile 4][lane 64][4] floats per wave
+  static constexpr int kParkFloats = 4 * 4 * 64 * 4;
   static constexpr int kNS = M::kNS;
   static constexpr int kKB = kH / 32;  // k-blocks per 128-wide operand
   using T = typename M::T;
@@ -165,8 +168,8 @@ struct CoreK32 {
   }
 
   template <int MT>
-  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, const float (&feat)[MT],
-                                             float (&ffwd)[MT], float (&fbwd)[MT]) {
+  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, float *park,
+                                             const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
     const int lane = R.lane;
     const int g4 = 4 * (lane >> 4);
     Frag B[MT][kKB];
@@ -178,17 +181,28 @@ struct CoreK32 {
     // message passing (src/flux_gnn.py:53-60)
     for (int l = 0; l < W.layers; ++l) {
       const float *bias = S.bl + l * kH;
+      {
+        f4 lo[MT][4];
+        layer_half<MT, 0>(R, B, bias, g4, lo);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) *reinterpret_cast<f4 *>(park + ((mt * 4 + n) * 64 + lane) * 4) = lo[mt][n];
+      }
       f4 h[MT][kNT];
-      f4 lo[MT][4], hi[MT][4];
-      layer_half<MT, 0>(R, B, bias, g4, lo);
-      layer_half<MT, 1>(R, B, bias, g4, hi);
+      {
+        f4 hi[MT][4];
+        layer_half<MT, 1>(R, B, bias, g4, hi);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) h[mt][n + 4] = hi[mt][n];
+      }
+      wave_lds_sync();
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          h[mt][n] = lo[mt][n];
-          h[mt][n + 4] = hi[mt][n];
-        }
+        for (int n = 0; n < 4; ++n) h[mt][n] = ldf4(park + ((mt * 4 + n) * 64 + lane) * 4);
       to_frags<MT>(h, B);
     }
     // edge readout, P/Q split (src/flux_gnn.py:62-66)
@@ -217,12 +231,12 @@ hipError_t launch_chain_flux_k32(const ChainW &w, const float *nf, const float *
 
 hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float *state_final, const float *x,
                                     const double *pc, int B, int nx, int T, float c, float dt, float *traj,
-                                    float *flux_traj, float *metrics, hipStream_t s) {
+                                    float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
   if (w.prec == kPrecF16x3)
     return chain::launch_rollout_core<CoreK32<ModeF16x3>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
-                                                          flux_traj, metrics, s);
+                                                          flux_traj, metrics, ex, s);
   return chain::launch_rollout_core<CoreK32<ModeBF16>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
-                                                       flux_traj, metrics, s);
+                                                       flux_traj, metrics, ex, s);
 }
 
 }  // namespace hf

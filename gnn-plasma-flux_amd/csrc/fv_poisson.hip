@@ -112,7 +112,39 @@ __global__ __launch_bounds__(kFvThreads) void poisson_kernel(const float *__rest
   for (int i = threadIdx.x; i < nx; i += kFvThreads) E[b * ld_E + i] = poisson_cell(s_rho, s_c, i, nx);
 }
 
+// Per-step channel MSE of two trajectories (scripts/evaluation/evaluate_multi_ic.py:88-90).
+__global__ __launch_bounds__(kFvThreads) void traj_mse_kernel(const float *__restrict__ a,
+                                                              const float *__restrict__ b, int nx,
+                                                              float *__restrict__ mse) {
+  __shared__ double s_part[kFvThreads / 64];
+  const int64_t row = blockIdx.x;  // (ic, t)
+  const float *pa = a + row * 3 * nx, *pb = b + row * 3 * nx;
+  for (int ch = 0; ch < 3; ++ch) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < nx; i += kFvThreads) {
+      const double d = (double)pa[ch * nx + i] - (double)pb[ch * nx + i];
+      acc += d * d;
+    }
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int w = 0; w < kFvThreads / 64; ++w) t += s_part[w];
+      mse[row * 3 + ch] = (float)(t / nx);
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
+
+hipError_t launch_traj_mse(const float *a, const float *b, int B, int T1, int nx, float *mse, hipStream_t s) {
+  const int64_t rows = (int64_t)B * T1;
+  if (rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(traj_mse_kernel, dim3((unsigned)rows), dim3(kFvThreads), 0, s, a, b, nx, mse);
+  return hipGetLastError();
+}
 
 hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld_out,
                           const float *face_flux, const double *pc, int B, int nx, float c,

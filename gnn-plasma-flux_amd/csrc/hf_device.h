@@ -17,9 +17,10 @@
 
 namespace hf {
 
-// torch.relu semantics: NaN propagates (a v_max_f32 would turn NaN into 0 and
-// hide a blow-up from the finiteness metric).
-__device__ __forceinline__ float relu(float x) { return x < 0.f ? 0.f : x; }
+// torch.relu semantics: NaN propagates (v_max_f32 would turn NaN into 0 and
+// hide a blow-up from the finiteness metric).  IEEE-754-2019 maximum lowers to
+// one gfx950 v_maximum3_f32, which propagates NaN.
+__device__ __forceinline__ float relu(float x) { return __builtin_elementwise_maximum(x, 0.0f); }
 
 // F = f32(0.5 * f32(F_fwd + F_bwd))                 src/hybrid_solver.py:45-48
 __device__ __forceinline__ float face_flux(float ffwd, float fbwd) {

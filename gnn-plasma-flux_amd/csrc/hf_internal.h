@@ -66,10 +66,19 @@ hipError_t launch_chain_flux_f32(const ChainW &, const float *, const float *, i
                                  float *, float *, hipStream_t);
 hipError_t launch_chain_flux_k32(const ChainW &, const float *, const float *, int64_t, const float *, int, int,
                                  float *, float *, hipStream_t);
+// Extra outputs of the persistent rollout: a classical twin of every IC
+// stepped in the same wave (hf_run_compare), all optional.
+struct RolloutExtras {
+  float nu = 0.f, dx2 = 1.f;        // classical viscosity and f32(dx*dx)
+  float *mse = nullptr;             // [B][T+1][3]; non-null enables the twin
+  float *metrics_cl = nullptr;      // [B][T+1][HF_NUM_METRICS]
+};
 hipError_t launch_chain_rollout_f32(const ChainW &, const float *, float *, const float *, const double *, int, int,
-                                    int, float, float, float *, float *, float *, hipStream_t);
+                                    int, float, float, float *, float *, float *, const RolloutExtras &,
+                                    hipStream_t);
 hipError_t launch_chain_rollout_k32(const ChainW &, const float *, float *, const float *, const double *, int, int,
-                                    int, float, float, float *, float *, float *, hipStream_t);
+                                    int, float, float, float *, float *, float *, const RolloutExtras &,
+                                    hipStream_t);
 
 // Chain flux.  Feature source: AoS node features [B*nx][4] (nf != nullptr)
 // or SoA state [B][3][nx] with IC stride ld_state floats + x[nx].
@@ -84,11 +93,16 @@ inline hipError_t launch_chain_flux(const ChainW &w, const float *nf, const floa
 inline hipError_t launch_chain_rollout(const ChainW &w, const float *state0, float *state_final,
                                        const float *x, const double *pc, int B, int nx, int T, float c,
                                        float dt, float *traj, float *flux_traj, float *metrics,
-                                       hipStream_t s) {
+                                       hipStream_t s, const RolloutExtras &ex = RolloutExtras()) {
   return w.prec == kPrecF32
-             ? launch_chain_rollout_f32(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, s)
-             : launch_chain_rollout_k32(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, s);
+             ? launch_chain_rollout_f32(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics,
+                                        ex, s)
+             : launch_chain_rollout_k32(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics,
+                                        ex, s);
 }
+
+// Per-step channel MSE between two trajectories [B][T+1][3][nx] -> [B][T+1][3].
+hipError_t launch_traj_mse(const float *a, const float *b, int B, int T1, int nx, float *mse, hipStream_t s);
 
 // One FV + Poisson update (any nx).  face_flux != nullptr => hybrid update
 // with that F; nullptr => classical (F = n*u, viscosity).  IC strides in floats.

@@ -38,6 +38,8 @@ SIGNATURES = {
                         c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "hf_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                        c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hf_run_compare": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                               c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -147,21 +147,51 @@ def step(model, grid, state, flux_face=False, metrics=False):
     return out, F, M
 
 
+def _buf(want, given, shape, dev):
+    """An output buffer: the caller's preallocated tensor (checked), a new one, or None."""
+    if isinstance(given, torch.Tensor):
+        if tuple(given.shape) != tuple(shape) or given.dtype != torch.float32 or given.device != dev \
+                or not given.is_contiguous():
+            raise ValueError(f"preallocated output must be contiguous float32 {tuple(shape)} on {dev}")
+        return given
+    return torch.empty(shape, device=dev) if want else None
+
+
 def run(model, grid, state0, T, traj=True, flux=False, metrics=False, out=None):
-    """T-step rollout; returns dict(final, traj [B,T+1,3,nx], flux [B,T,nx], metrics [B,T+1,4])."""
+    """T-step rollout; returns dict(final, traj [B,T+1,3,nx], flux [B,T,nx], metrics [B,T+1,4]).
+    traj/flux/metrics may be bools or preallocated tensors (kept out of timed regions)."""
     state0 = _state(state0, grid.nx)
     B, dev = state0.shape[0], state0.device
     T = int(T)
     final = torch.empty_like(state0) if out is None else out
-    tr = torch.empty(B, T + 1, 3, grid.nx, device=dev) if traj else None
-    fl = torch.empty(B, T, grid.nx, device=dev) if flux else None
-    me = torch.empty(B, T + 1, HF_NUM_METRICS, device=dev) if metrics else None
+    tr = _buf(traj, traj, (B, T + 1, 3, grid.nx), dev)
+    fl = _buf(flux, flux, (B, T, grid.nx), dev)
+    me = _buf(metrics, metrics, (B, T + 1, HF_NUM_METRICS), dev)
     x, pc = grid.on(dev)
     with torch.cuda.device(dev):
         check(lib().hf_run(model.handle if model else None, ptr(state0), ptr(final), ptr(x), ptr(pc), B,
                            grid.nx, T, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(tr), ptr(fl),
                            ptr(me), stream_of(dev)))
     return {"final": final, "traj": tr, "flux": fl, "metrics": me}
+
+
+def run_compare(model, grid, state0, T, metrics=True):
+    """Hybrid rollout and its classical twin from the same ICs, scored per step
+    (scripts/evaluation/evaluate_multi_ic.py:21-94).  Returns dict(final,
+    mse [B,T+1,3] (n,u,E), metrics [B,T+1,4], metrics_classical [B,T+1,4])."""
+    state0 = _state(state0, grid.nx)
+    B, dev = state0.shape[0], state0.device
+    T = int(T)
+    final = torch.empty_like(state0)
+    mse = torch.empty(B, T + 1, 3, device=dev)
+    me = torch.empty(B, T + 1, HF_NUM_METRICS, device=dev) if metrics else None
+    mc = torch.empty(B, T + 1, HF_NUM_METRICS, device=dev) if metrics else None
+    x, pc = grid.on(dev)
+    with torch.cuda.device(dev):
+        check(lib().hf_run_compare(model.handle, ptr(state0), ptr(final), ptr(x), ptr(pc), B, grid.nx, T,
+                                   grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(mse), ptr(me), ptr(mc),
+                                   stream_of(dev)))
+    return {"final": final, "mse": mse, "metrics": me, "metrics_classical": mc}
 
 
 def chain_flux(model, node_features, B, nx):

@@ -153,6 +153,24 @@ int hf_run(hf_model_t model, const float *dev_state0, float *dev_state_final,
            float c, float dt, float nu, float dx2,
            float *dev_traj, float *dev_flux_traj, float *dev_metrics, void *stream);
 
+/*
+ * Hybrid rollout scored against the classical solver from the same ICs, in
+ * one pass (replaces the serial per-IC loop of
+ * scripts/evaluation/evaluate_multi_ic.py:21-94: BaselineSolver.step from
+ * state0, HybridSolver.run from state0, per-step channel MSE; and the
+ * energy/charge series of scripts/evaluation/evaluate_all.py:118-159).
+ * The classical twin uses the same dt/dx and viscosity `nu`.
+ * dev_mse [B][T+1][3] (required): mean over cells of (hybrid - classical)^2
+ *   for n, u, E at every step (step 0 is 0).
+ * dev_metrics / dev_metrics_classical [B][T+1][HF_NUM_METRICS] (may be NULL).
+ * dev_state_final receives the hybrid final state.  For nx in {16,32,48,64}
+ * both solvers advance inside the one persistent kernel.
+ */
+int hf_run_compare(hf_model_t model, const float *dev_state0, float *dev_state_final,
+                   const float *dev_x, const double *dev_c, int B, int nx, int T,
+                   float c, float dt, float nu, float dx2, float *dev_mse,
+                   float *dev_metrics, float *dev_metrics_classical, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -270,3 +270,26 @@ def test_full_batch_properties(hf):
     pick = np.random.RandomState(0).choice(4096, 24, replace=False)
     want, _ = O.hybrid_run(O.params_from(w), O.Grid(64), ics[pick].cpu().numpy(), 30)
     close(a["final"][pick].cpu().numpy(), want[:, -1], ROLL_ATOL, ROLL_RTOL)
+
+
+# ------------------------------------------------- fused classical comparison
+@pytest.mark.parametrize("nx,precision", [(64, "f32"), (64, "f16x3"), (32, "f32"), (100, "f32")])
+def test_compare_vs_oracle(hf, nx, precision):
+    """hf_run_compare == evaluate_multi_ic.py's hybrid-vs-classical MSE, per step."""
+    w = weights("W1_r1")
+    G = O.Grid(nx, dt=5e-3 * min(1.0, nx / 64.0))
+    ics = np.stack([O.initial_condition(G, s) for s in (1000, 1001, 1002)])
+    Sh, _ = O.hybrid_run(O.params_from(w), G, ics, 20)
+    Sc, _ = O.classical_run(G, ics, 20)
+    want = np.mean((Sh - Sc).astype(np.float64) ** 2, axis=-1)          # [B, T+1, 3]
+    solver = hf.HybridSolver(w, radius=1, nx=nx, dt=G.dt, device=DEV, precision=precision)
+    out = solver.compare_batch(ics, 20)
+    got = out["mse"].cpu().numpy()
+    assert got.shape == (3, 21, 3) and (got[:, 0] == 0).all()
+    close(got, want, 1e-9, 2e-3)
+    e, q, f = O.rollout_metrics(Sc)
+    mc = out["metrics_classical"].cpu().numpy()
+    close(mc[..., 0], e, 1e-6, 1e-6)
+    close(mc[..., 1], q, 1e-6, 1e-6)
+    per_ic = got.sum(-1).mean(-1)                                        # evaluate_multi_ic.py:91-94
+    close(per_ic, want.sum(-1).mean(-1), 1e-9, 2e-3)
