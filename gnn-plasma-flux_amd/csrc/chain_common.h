@@ -33,7 +33,9 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 
 // GFX9 DPP controls.
 constexpr int kRowShl1 = 0x101;
+constexpr int kRowShl15 = 0x10F;
 constexpr int kRowShr1 = 0x111;
+constexpr int kRowShr15 = 0x11F;
 constexpr int kRowRor1 = 0x121;
 constexpr int kRowRor15 = 0x12F;
 
@@ -65,6 +67,27 @@ __device__ __forceinline__ void left_nb(const float (&v)[MT], float (&l)[MT]) {
   for (int mt = 0; mt < MT; ++mt) rot[mt] = dpp_mov<kRowRor1>(v[mt]);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) l[mt] = dpp_over<kRowShr1>(rot[(mt + MT - 1) % MT], v[mt]);
+}
+
+// Lanes whose DPP source falls outside their row read 0 (bound_ctrl), so the
+// mov folds into the consuming v_add_f32 as a DPP operand.
+template <int CTRL>
+__device__ __forceinline__ float dpp_zero(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// v[i+1] + v[i-1] for every cell (periodic over the MT m-tiles), 4 VALU per
+// value: the in-row pair, then the wrap lane from each neighbouring tile.  The
+// extra terms are exact +0s, so the result is bit-identical to the two-term
+// sum the reference's index_add_ forms (src/flux_gnn.py:57).
+template <int MT>
+__device__ __forceinline__ void nb_sum(const float (&v)[MT], float (&s)[MT]) {
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    float t = __fadd_rn(dpp_zero<kRowShl1>(v[mt]), dpp_zero<kRowShr1>(v[mt]));  // lane 15 / lane 0 get 0
+    t = __fadd_rn(t, dpp_zero<kRowShl15>(v[(mt + MT - 1) % MT]));              // lane 0 += tile mt-1, lane 15
+    s[mt] = __fadd_rn(t, dpp_zero<kRowShr15>(v[(mt + 1) % MT]));               // lane 15 += tile mt+1, lane 0
+  }
 }
 
 __device__ __forceinline__ f4 relu4(f4 v) { return f4{relu(v.x), relu(v.y), relu(v.z), relu(v.w)}; }

@@ -45,11 +45,10 @@ struct CoreF32 {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) b[mt] = h[mt][s >> 2][s & 3];
       if (GI >= kHalf) {
-        float bl[MT], br[MT];
-        left_nb<MT>(b, bl);
-        right_nb<MT>(b, br);
+        float sum[MT];
+        nb_sum<MT>(b, sum);  // index_add_ of h[i+1], h[i-1]
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) b[mt] = __fmul_rn(__fadd_rn(br[mt], bl[mt]), 0.5f);  // index_add_ h[i+1], h[i-1]; / deg 2
+        for (int mt = 0; mt < MT; ++mt) b[mt] = __fmul_rn(sum[mt], 0.5f);  // / deg 2 (exact)
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)

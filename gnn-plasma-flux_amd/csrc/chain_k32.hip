@@ -122,15 +122,15 @@ struct CoreK32 {
       const f4 b = ldf4(bias + 16 * ntl + g4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float gv[MT], gl[MT], gr[MT];
+        float gv[MT], gs[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) gv[mt] = gac[mt][ntl][r];
-        left_nb<MT>(gv, gl);
-        right_nb<MT>(gv, gr);
+        nb_sum<MT>(gv, gs);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const float agg = __fmul_rn(__fadd_rn(gr[mt], gl[mt]), 0.5f);
-          out[mt][ntl][r] = relu(__fadd_rn(__fadd_rn(acc[mt][ntl][r], agg), b[r]));
+          // acc + 0.5*(G[i+1] + G[i-1]): one rounding either way, 0.5*x is exact
+          const float a = fmaf(gs[mt], 0.5f, acc[mt][ntl][r]);
+          out[mt][ntl][r] = relu(__fadd_rn(a, b[r]));
         }
       }
     }
