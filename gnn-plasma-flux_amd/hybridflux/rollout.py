@@ -36,11 +36,15 @@ def gather_ic_rows(local, n_total, group=None):
     counts = [shard_bounds(n_total, world, r)[1] - shard_bounds(n_total, world, r)[0] for r in range(world)]
     assert local.shape[0] == counts[rank], (local.shape, counts)
     cap = max(counts)
-    pad = local.new_zeros((cap,) + tuple(local.shape[1:]))
-    pad[: local.shape[0]] = local
+    # gloo moves host memory: stage device tensors through the host for it
+    stage = local.is_cuda and dist.get_backend(group) == "gloo"
+    src = local.cpu() if stage else local
+    pad = src.new_zeros((cap,) + tuple(src.shape[1:]))
+    pad[: src.shape[0]] = src
     bufs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(bufs, pad.contiguous(), group=group)
-    return torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+    out = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+    return out.to(local.device) if stage else out
 
 
 def sharded_rollout(run_local, make_ics, seed0, n_total, T, group=None):

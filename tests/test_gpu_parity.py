@@ -293,3 +293,22 @@ def test_compare_vs_oracle(hf, nx, precision):
     close(mc[..., 1], q, 1e-6, 1e-6)
     per_ic = got.sum(-1).mean(-1)                                        # evaluate_multi_ic.py:91-94
     close(per_ic, want.sum(-1).mean(-1), 1e-9, 2e-3)
+
+
+# ------------------------------------------------------------- dataset writer
+def test_generate_dataset_vs_oracle(hf, tmp_path):
+    """hybridflux.datagen == scripts/training/generate_data.py (keys, order, values)."""
+    from hybridflux.datagen import generate_dataset
+    out = tmp_path / "dataset.npz"
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=3, steps_per_ic=7, out_path=str(out),
+                                                 device=DEV)
+    d = np.load(out)
+    assert sorted(d.files) == sorted(["state_t", "flux_t", "state_next", "x", "dt", "dx", "nu"])
+    G = O.Grid(64)
+    S, F = O.classical_run(G, np.stack([O.initial_condition(G, s) for s in range(3)]), 7)
+    close(d["state_t"], S[:, :-1].reshape(21, 3, 64), 1e-5, 1e-5)
+    close(d["state_next"], S[:, 1:].reshape(21, 3, 64), 1e-5, 1e-5)
+    close(d["flux_t"], F.reshape(21, 64), 1e-5, 1e-5)
+    assert np.array_equal(d["x"], G.x.astype(np.float32)) and float(d["dx"]) == G.dx
+    # first step of every IC is bit-exact (n, u of step 1; F of step 0)
+    assert np.array_equal(d["flux_t"][::7], F[:, 0]) and np.array_equal(d["state_next"][::7, :2], S[:, 1, :2])
