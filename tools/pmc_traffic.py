@@ -13,14 +13,14 @@ import sqlite3
 import sys
 from glob import glob
 
-KERNEL = "chain_rollout_kernel"
+KERNEL = "chain_rollout_kernel<hf::CoreF32"   # the headline (f32) kernel; bench times alt precisions after it
 
 
 def last_value(db, counter):
     c = sqlite3.connect(db)
-    rows = c.execute("select dispatch_id, sum(counter_value), max(duration) from pmc_events where name like ? "
+    rows = c.execute("select dispatch_id, sum(counter_value), max(duration) from pmc_events where instr(name, ?) > 0 "
                      "and counter_name = ? group by dispatch_id order by dispatch_id",
-                     (f"%{KERNEL}%", counter)).fetchall()
+                     (KERNEL, counter)).fetchall()
     return rows[-1]
 
 
