@@ -13,7 +13,7 @@ import sqlite3
 import sys
 from glob import glob
 
-KERNEL = "chain_rollout_kernel<hf::CoreF32"   # the headline (f32) kernel; bench times alt precisions after it
+KERNEL = "CoreF32, 4>"   # the headline (f32) kernel; bench times alt precisions after it
 
 
 def last_value(db, counter):
