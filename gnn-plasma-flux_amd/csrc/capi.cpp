@@ -361,6 +361,8 @@ int hf_graph_flux(hf_model_t m, const float *nf, int64_t N, const int64_t *ei, i
   return HF_OK;
 }
 
+int hf_poisson_plan_len(int nx) { return nx < 1 ? -1 : hf::poisson_plan_len(nx); }
+
 int hf_poisson_coeffs(int nx, double length, double *c) {
   if (nx < 1 || !(length > 0) || !c) return fail(HF_EINVAL, "hf_poisson_coeffs: bad argument");
   // E = Re(ifft(i fft(rho)/k)), k_q = 2 pi q'/L over the signed fftfreq q'
@@ -377,6 +379,20 @@ int hf_poisson_coeffs(int nx, double length, double *c) {
     }
     c[d] = (double)(-(long double)length / ((long double)pi * nx) * acc);
   }
+  if (hf::poisson_uses_fft(nx)) {  // FFT plan: twiddles exp(-2 pi i m/nx), then 1/k_q
+    double *tw = c + nx, *inv_k = c + 2 * nx;
+    for (int m = 0; m < nx / 2; ++m) {
+      const long double a = -2.0L * (long double)pi * (long double)m / (long double)nx;
+      tw[2 * m] = (double)cosl(a);
+      tw[2 * m + 1] = (double)sinl(a);
+    }
+    const double dx = length / nx;  // k = 2 pi fftfreq(nx, d=dx)   (src/baseline_solver.py:26)
+    for (int q = 0; q < nx; ++q) {
+      const int f = q < (nx + 1) / 2 ? q : q - nx;
+      const double k = 2.0 * pi * ((double)f / (nx * dx));
+      inv_k[q] = f == 0 ? 0.0 : 1.0 / k;
+    }
+  }
   return HF_OK;
 }
 
@@ -385,7 +401,7 @@ int hf_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, i
   if (B < 0 || nx < 1 || ld_n < nx || ld_E < nx) return fail(HF_EINVAL, "hf_poisson: bad shape");
   if (B == 0) return HF_OK;
   if (!n || !E || !pc) return fail(HF_EINVAL, "hf_poisson: NULL pointer");
-  if (nx > 2 * kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_poisson: nx too large for the LDS solve");
+  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_poisson: nx too large for the LDS solve");
   HF_CHECK_HIP(hf::launch_poisson(n, ld_n, E, ld_E, pc, B, nx, as_stream(stream)), "hf_poisson");
   return HF_OK;
 }

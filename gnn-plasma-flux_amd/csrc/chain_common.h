@@ -264,42 +264,48 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
   const Small S = stage_small(W, lds + kRingFloats);
   auto R = make_ring<Core>(W, lds);
   const int lane = R.lane, j = lane & 15, g = lane >> 4;
-  const int64_t item_raw = (int64_t)blockIdx.x * kWaves + R.wave;
-  const bool live = item_raw < items;
-  const int64_t item = live ? item_raw : items - 1;  // idle waves mirror a real item, write nothing
-  const int64_t b = item / nwin;
-  const int w = (int)(item - b * nwin);
-  const int start = EXACT ? 0 : w * kWinFaces - kWinHalo;
-  float feat[MT];
-  int cell[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    int cidx = (start + 16 * mt + j) % nx;
-    if (cidx < 0) cidx += nx;
-    cell[mt] = cidx;
-    feat[mt] = nf ? nf[(b * nx + cidx) * kIn + g]
-                  : (g < 3 ? state[b * ld_state + (int64_t)g * nx + cidx] : x[cidx]);
-  }
   __syncthreads();  // small weights staged (no DMA in flight yet)
   R.prime();
-  float f_fwd[MT], f_bwd[MT];
-  Core::template gnn<MT>(W, S, R, park_of<Core>(lds, R.wave), feat, f_fwd, f_bwd);
-  R.drain();
-  if (!live) return;
+  // Persistent over groups of 4 items: the weight stream keeps flowing from one
+  // group's forward pass into the next, so the ring fill is paid once per workgroup.
+  const int64_t groups = (items + kWaves - 1) / kWaves;
+  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    const int64_t item_raw = grp * kWaves + R.wave;
+    const bool live = item_raw < items;
+    const int64_t item = live ? item_raw : items - 1;  // idle waves mirror a real item, write nothing
+    const int64_t b = item / nwin;
+    const int w = (int)(item - b * nwin);
+    const int start = EXACT ? 0 : w * kWinFaces - kWinHalo;
+    float feat[MT];
+    int cell[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int wc = 16 * mt + j;
-    int face = cell[mt];
-    bool ok = true;
-    if (!EXACT) {
-      face = w * kWinFaces + (wc - kWinHalo);
-      ok = wc >= kWinHalo && wc < kWinHalo + kWinFaces && face < nx;
+    for (int mt = 0; mt < MT; ++mt) {
+      int cidx = (start + 16 * mt + j) % nx;
+      if (cidx < 0) cidx += nx;
+      cell[mt] = cidx;
+      feat[mt] = nf ? nf[(b * nx + cidx) * kIn + g]
+                    : (g < 3 ? state[b * ld_state + (int64_t)g * nx + cidx] : x[cidx]);
     }
-    if (!ok) continue;
-    if (fe && g == 0) fe[b * 2 * nx + face] = f_fwd[mt];
-    if (fe && g == 1) fe[b * 2 * nx + nx + face] = f_bwd[mt];
-    if (ff && g == 2) ff[b * nx + face] = face_flux(f_fwd[mt], f_bwd[mt]);
+    float f_fwd[MT], f_bwd[MT];
+    Core::template gnn<MT>(W, S, R, park_of<Core>(lds, R.wave), feat, f_fwd, f_bwd);
+    if (live) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int wc = 16 * mt + j;
+        int face = cell[mt];
+        bool ok = true;
+        if (!EXACT) {
+          face = w * kWinFaces + (wc - kWinHalo);
+          ok = wc >= kWinHalo && wc < kWinHalo + kWinFaces && face < nx;
+        }
+        if (!ok) continue;
+        if (fe && g == 0) fe[b * 2 * nx + face] = f_fwd[mt];
+        if (fe && g == 1) fe[b * 2 * nx + nx + face] = f_bwd[mt];
+        if (ff && g == 2) ff[b * nx + face] = face_flux(f_fwd[mt], f_bwd[mt]);
+      }
+    }
   }
+  R.drain();
 }
 
 // ---------------------------------------------------------------------------
@@ -432,11 +438,24 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
 }
 
 // ------------------------------------------------------------------ launchers
+// Workgroups resident at once: one per CU (the chain kernels hold ~500
+// registers per lane, so 4 waves = one per SIMD fill a CU).
+inline int resident_groups() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
 template <class Core, int MT, bool EXACT>
 hipError_t flux_launch(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
                        int nx, int nwin, int64_t items, float *fe, float *ff, hipStream_t s) {
-  const int64_t blocks = (items + kWaves - 1) / kWaves;
-  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  const int64_t groups = (items + kWaves - 1) / kWaves;
+  const int64_t blocks = groups < resident_groups() ? groups : resident_groups();  // persistent: 1 per CU
   hipLaunchKernelGGL((chain_flux_kernel<Core, MT, EXACT>), dim3((unsigned)blocks), dim3(64 * kWaves), 0, s, w,
                      nf, state, ld_state, x, nx, nwin, items, fe, ff);
   return hipGetLastError();

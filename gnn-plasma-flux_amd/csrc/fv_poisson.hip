@@ -38,7 +38,13 @@ __device__ __forceinline__ void block_metrics(MetricAcc &m, float *dst, int nx) 
   }
 }
 
-// LDS: u[nx] F[nx] rho[nx] (float) + c[nx] (double)
+// LDS: c[nx] (double) | u, F, rho, E (float) | FFT buffers 2 x nx double2 (FFT nx only)
+inline size_t fv_lds_bytes(int nx) {
+  size_t b = (size_t)nx * (sizeof(double) + 4 * sizeof(float));
+  if (poisson_uses_fft(nx)) b = ((b + 15) & ~size_t(15)) + 2 * sizeof(double2) * nx;
+  return b;
+}
+
 template <bool HYBRID>
 __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     const float *__restrict__ in, int64_t ld_in, float *__restrict__ out, int64_t ld_out,
@@ -50,6 +56,10 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
   float *s_u = reinterpret_cast<float *>(s_c + nx);
   float *s_F = s_u + nx;
   float *s_rho = s_F + nx;
+  float *s_E = s_rho + nx;
+  const bool fft = poisson_uses_fft(nx);
+  double2 *fa = reinterpret_cast<double2 *>(reinterpret_cast<char *>(s_dyn) +
+                                            (((size_t)nx * (sizeof(double) + 4 * sizeof(float)) + 15) & ~size_t(15)));
   const int64_t b = blockIdx.x;
   const float *st = in + b * ld_in;
   float *so = out + b * ld_out;
@@ -57,7 +67,7 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     const float u = st[nx + i];
     s_u[i] = u;
     s_F[i] = HYBRID ? face_flux[b * nx + i] : __fmul_rn(st[i], u);  // F_n = n*u (:70-71)
-    s_c[i] = pc[i];
+    if (!fft) s_c[i] = pc[i];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
@@ -74,10 +84,11 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     if (flux_out) flux_out[b * ld_flux + i] = F;
   }
   __syncthreads();
+  if (fft) poisson_fft(s_rho, fa, fa + nx, pc, nx, s_E);
   MetricAcc m;
   m.init();
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-    const float E_new = poisson_cell(s_rho, s_c, i, nx);
+    const float E_new = fft ? s_E[i] : poisson_cell(s_rho, s_c, i, nx);
     so[2 * nx + i] = E_new;
     if (metrics) m.add(so[i], so[nx + i], E_new);
   }
@@ -102,14 +113,21 @@ __global__ __launch_bounds__(kFvThreads) void poisson_kernel(const float *__rest
                                                              int nx) {
   extern __shared__ double s_dyn[];
   double *s_c = s_dyn;
-  float *s_rho = reinterpret_cast<float *>(s_c + nx);
+  float *s_u = reinterpret_cast<float *>(s_c + nx);  // unused: keeps the fv LDS layout
+  float *s_rho = s_u + 2 * nx;
+  float *s_E = s_rho + nx;
+  const bool fft = poisson_uses_fft(nx);
+  double2 *fa = reinterpret_cast<double2 *>(reinterpret_cast<char *>(s_dyn) +
+                                            (((size_t)nx * (sizeof(double) + 4 * sizeof(float)) + 15) & ~size_t(15)));
   const int64_t b = blockIdx.x;
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-    s_c[i] = pc[i];
+    if (!fft) s_c[i] = pc[i];
     s_rho[i] = __fsub_rn(n[b * ld_n + i], 1.0f);  // rho = n - n0 (:60)
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nx; i += kFvThreads) E[b * ld_E + i] = poisson_cell(s_rho, s_c, i, nx);
+  if (fft) poisson_fft(s_rho, fa, fa + nx, pc, nx, s_E);
+  for (int i = threadIdx.x; i < nx; i += kFvThreads)
+    E[b * ld_E + i] = fft ? s_E[i] : poisson_cell(s_rho, s_c, i, nx);
 }
 
 // Per-step channel MSE of two trajectories (scripts/evaluation/evaluate_multi_ic.py:88-90).
@@ -151,7 +169,7 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
                           float dt, float nu, float dx2, float *flux_out, int64_t ld_flux,
                           float *metrics, int64_t ld_metrics, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  const size_t lds = (size_t)nx * (sizeof(double) + 3 * sizeof(float));
+  const size_t lds = fv_lds_bytes(nx);
   if (face_flux)
     hipLaunchKernelGGL(fv_step_kernel<true>, dim3(B), dim3(kFvThreads), lds, s, in, ld_in, out,
                        ld_out, face_flux, pc, nx, c, dt, nu, dx2, flux_out, ld_flux, metrics,
@@ -174,7 +192,7 @@ hipError_t launch_state_metrics(const float *st, int64_t ld, int B, int nx, floa
 hipError_t launch_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B,
                           int nx, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  const size_t lds = (size_t)nx * (sizeof(double) + sizeof(float));
+  const size_t lds = fv_lds_bytes(nx);
   hipLaunchKernelGGL(poisson_kernel, dim3(B), dim3(kFvThreads), lds, s, n, ld_n, E, ld_E, pc, nx);
   return hipGetLastError();
 }

@@ -65,6 +65,52 @@ __device__ __forceinline__ float poisson_cell(const float *s_rho, const double *
   return (float)(a0 + a1);
 }
 
+// ---------------------------------------------------------------- FFT Poisson
+// For power-of-two nx >= kFftMinNx the spectral operator is applied as the
+// reference writes it (src/baseline_solver.py:59-68), E = Re(ifft(1j*fft(rho)/k)),
+// with a float64 Stockham radix-2 FFT in LDS instead of the O(nx^2) circulant.
+// The plan buffer (hf_poisson_coeffs) then holds, after the circulant column
+// c[nx]: twiddles exp(-2 pi i m / nx) for m < nx/2 as (re, im), and 1/k_q (0 at q = 0).
+// In-place-style block FFT: returns the buffer holding the result (a or b).
+__device__ __forceinline__ double2 *fft_block(double2 *a, double2 *b, const double2 *__restrict__ tw, int n,
+                                              bool inverse) {
+  for (int ns = 1; ns < n; ns <<= 1) {
+    __syncthreads();
+    for (int jj = threadIdx.x; jj < n / 2; jj += blockDim.x) {
+      const double2 a0 = a[jj], a1 = a[jj + n / 2];
+      const int k = jj & (ns - 1);
+      double2 w = tw[k * (n / (2 * ns))];
+      if (inverse) w.y = -w.y;
+      const double2 t = make_double2(a1.x * w.x - a1.y * w.y, a1.x * w.y + a1.y * w.x);
+      const int d = ((jj - k) << 1) + k;
+      b[d] = make_double2(a0.x + t.x, a0.y + t.y);
+      b[d + ns] = make_double2(a0.x - t.x, a0.y - t.y);
+    }
+    double2 *s = a;
+    a = b;
+    b = s;
+  }
+  __syncthreads();
+  return a;
+}
+
+// E[q] for the whole IC (block-wide): rho (LDS floats) -> out (LDS floats).
+__device__ __forceinline__ void poisson_fft(const float *s_rho, double2 *a, double2 *b, const double *plan, int nx,
+                                           float *out) {
+  const double2 *tw = reinterpret_cast<const double2 *>(plan + nx);
+  const double *inv_k = plan + 2 * nx;
+  for (int q = threadIdx.x; q < nx; q += blockDim.x) a[q] = make_double2((double)s_rho[q], 0.0);
+  double2 *X = fft_block(a, b, tw, nx, false);
+  double2 *Y = X == a ? b : a;
+  for (int q = threadIdx.x; q < nx; q += blockDim.x) {
+    const double ik = inv_k[q];                       // 1j * X / k, k = 0 mode zeroed
+    X[q] = make_double2(-X[q].y * ik, X[q].x * ik);
+  }
+  X = fft_block(X, Y, tw, nx, true);
+  for (int q = threadIdx.x; q < nx; q += blockDim.x) out[q] = (float)(X[q].x / nx);
+  __syncthreads();
+}
+
 // Per-state rollout metrics, partial sums for one cell.
 struct MetricAcc {
   double energy;  // sum u^2 + E^2

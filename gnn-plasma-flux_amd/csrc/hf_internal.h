@@ -34,6 +34,15 @@ constexpr int kWinFaces = kWinCells - 2 * kWinHalo - 1;  // 55
 // Each chunk is [fragment j][lane 64][16 B], so one wave instruction moves 1 KiB.
 enum ChainPrec { kPrecF32 = HF_WDTYPE_F32, kPrecBF16 = HF_WDTYPE_BF16, kPrecF16x3 = HF_WDTYPE_F16X3 };
 constexpr int kMaxChainLayers = 8;
+
+// Poisson by float64 FFT for power-of-two nx in [kFftMinNx, kFftMaxNx] (fv_poisson.hip).
+constexpr int kFftMinNx = 256;
+constexpr int kFftMaxNx = 2048;
+__host__ __device__ inline bool poisson_uses_fft(int nx) {
+  return nx >= kFftMinNx && nx <= kFftMaxNx && (nx & (nx - 1)) == 0;
+}
+__host__ __device__ inline int poisson_plan_len(int nx) { return poisson_uses_fft(nx) ? 3 * nx : nx; }
+
 __host__ __device__ inline int chain_chunks(int layers, int prec) {
   return prec == kPrecF32 ? 16 * layers + 2 * kNT : 8 * layers + kNT;
 }

@@ -111,7 +111,7 @@ class Grid:
         self.dt32 = float(np.float32(self.dt))
         self.nu32 = float(np.float32(self.nu))
         self.dx2_32 = float(np.float32(self.dx ** 2))
-        pc = np.empty(self.nx, dtype=np.float64)
+        pc = np.empty(lib().hf_poisson_plan_len(self.nx), dtype=np.float64)
         check(lib().hf_poisson_coeffs(self.nx, self.length, pc.ctypes.data_as(c_void_p)))
         self.poisson_c = pc
         self._dev = {}

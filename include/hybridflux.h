@@ -107,11 +107,17 @@ int hf_graph_flux(hf_model_t model, const float *dev_node_features, int64_t N,
                   void *dev_workspace, void *stream);
 
 /*
- * Host helper (no device work): first column c[0..nx) of the real circulant
- * matrix equal to the reference's spectral Poisson operator
+ * Host helper (no device work): the Poisson "plan" for nx cells, length
+ * hf_poisson_plan_len(nx) doubles.  plan[0..nx) is the first column c of the
+ * real circulant matrix equal to the reference's spectral Poisson operator
  * E = Re(ifft(1j*fft(n-1)/k)), k=0 mode zeroed (src/baseline_solver.py:26,59-68):
- * E[i] = sum_j c[(i-j) mod nx] * (n[j]-1).  Computed in float64.
+ * E[i] = sum_j c[(i-j) mod nx] * (n[j]-1), computed in float64.  For power-of-two
+ * nx in [256, 2048] the kernels apply the operator by float64 FFT instead and
+ * the plan continues with the twiddles exp(-2 pi i m/nx), m < nx/2, as (re, im)
+ * pairs, then 1/k_q (0 for q = 0).  Every dev_c argument below is a device copy
+ * of this plan.
  */
+int hf_poisson_plan_len(int nx);
 int hf_poisson_coeffs(int nx, double length, double *host_c);
 
 /* Replaces: BaselineSolver.solve_poisson (src/baseline_solver.py:59-68), batched.

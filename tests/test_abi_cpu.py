@@ -51,13 +51,54 @@ def test_poisson_coefficients_reproduce_spectral_solve(nx):
     """The circulant column from hf_poisson_coeffs applied in float64 equals the
     reference FFT solve (src/baseline_solver.py:59-68) to < 1e-7."""
     lib = _lib.lib()
-    c = np.empty(nx)
+    c = np.empty(lib.hf_poisson_plan_len(nx))
     _lib.check(lib.hf_poisson_coeffs(nx, 2 * np.pi, c.ctypes.data_as(ctypes.c_void_p)))
     g = golden("poisson.npz")
     rho = g[f"n_nx{nx}"].astype(np.float64) - 1.0
     idx = (np.arange(nx)[:, None] - np.arange(nx)[None, :]) % nx
     E = (rho @ c[idx].T).astype(np.float32)
     assert np.abs(E - g[f"E_nx{nx}"]).max() < 1e-7
+
+
+def _stockham(x, tw, inverse):
+    """The radix-2 Stockham passes of fv_poisson.hip fft_block, in numpy."""
+    n = x.size
+    w_all = np.conj(tw) if inverse else tw
+    ns = 1
+    j = np.arange(n // 2)
+    while ns < n:
+        a0, a1 = x[: n // 2], x[n // 2:]
+        k = j & (ns - 1)
+        t = a1 * w_all[k * (n // (2 * ns))]
+        d = ((j - k) << 1) + k
+        y = np.empty_like(x)
+        y[d], y[d + ns] = a0 + t, a0 - t
+        x, ns = y, ns * 2
+    return x
+
+
+@pytest.mark.parametrize("nx", [256, 512, 1024, 2048])
+def test_poisson_fft_plan(nx):
+    """For power-of-two nx >= 256 the plan carries twiddles and 1/k; the kernel's
+    FFT sequence applied with them equals the reference spectral solve
+    (src/baseline_solver.py:59-68) in float64 to 1e-12."""
+    lib = _lib.lib()
+    L = lib.hf_poisson_plan_len(nx)
+    assert L == 3 * nx
+    plan = np.empty(L)
+    _lib.check(lib.hf_poisson_coeffs(nx, 2 * np.pi, plan.ctypes.data_as(ctypes.c_void_p)))
+    tw = plan[nx:2 * nx].reshape(-1, 2) @ np.array([1, 1j])
+    inv_k = plan[2 * nx:]
+    rho = np.random.default_rng(nx).standard_normal(nx) * 0.1
+    X = _stockham(rho.astype(np.complex128), tw, False)
+    assert np.abs(X - np.fft.fft(rho)).max() < 1e-12
+    E = (_stockham(1j * X * inv_k, tw, True) / nx).real
+    k = 2 * np.pi * np.fft.fftfreq(nx, d=2 * np.pi / nx)
+    kk = np.where(k == 0, 1.0, k)
+    ref = np.real(np.fft.ifft(np.where(k == 0, 0, 1j * np.fft.fft(rho) / kk)))
+    assert np.abs(E - ref).max() < 1e-12
+    assert lib.hf_poisson_plan_len(64) == 64 and lib.hf_poisson_plan_len(384) == 384
+    assert lib.hf_poisson_plan_len(4096) == 4096 and lib.hf_poisson_plan_len(0) == -1
 
 
 def test_poisson_coefficients_errors():
