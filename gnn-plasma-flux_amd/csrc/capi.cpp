@@ -304,6 +304,8 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
     g.b_in = d + o; o += hidden;
     g.w_l = d + o; o += (int64_t)layers * hidden * 2 * hidden;
     g.b_l = d + o; o += (int64_t)layers * hidden;
+    g.lsw = (int64_t)hidden * 2 * hidden;
+    g.lsb = hidden;
     g.w_e = d + o; o += (int64_t)hidden * 2 * hidden;
     g.b_e = d + o; o += hidden;
     g.w_2 = d + o; o += hidden;
@@ -358,6 +360,54 @@ int hf_graph_flux(hf_model_t m, const float *nf, int64_t N, const int64_t *ei, i
   if (!nf || !ei || !flux || !ws) return fail(HF_EINVAL, "hf_graph_flux: NULL pointer");
   if (N > 0x7fffffffLL || E > 0x7fffffffLL) return fail(HF_EUNSUPPORTED, "hf_graph_flux: > 2^31 nodes/edges");
   HF_CHECK_HIP(hf::launch_graph_flux(m->graph, nf, N, ei, E, flux, ws, as_stream(stream)), "hf_graph_flux");
+  return HF_OK;
+}
+
+// ------------------------------------------------------------------ training
+static int train_dims_ok(int in_dim, int hidden, int layers) {
+  return in_dim >= 1 && hidden >= 1 && layers >= 0 && layers <= hf::kMaxChainLayers;
+}
+
+int64_t hf_graph_tape_bytes(int in_dim, int hidden, int layers, int64_t N, int64_t E) {
+  if (!train_dims_ok(in_dim, hidden, layers) || N < 0 || E < 0) return -1;
+  return hf::graph_tape_bytes(hf::graph_view_state_dict(nullptr, in_dim, hidden, layers), N, E);
+}
+
+int64_t hf_graph_backward_workspace_bytes(int in_dim, int hidden, int layers, int64_t N, int64_t E) {
+  if (!train_dims_ok(in_dim, hidden, layers) || N < 0 || E < 0) return -1;
+  return hf::graph_backward_ws_bytes(hf::graph_view_state_dict(nullptr, in_dim, hidden, layers), N, E);
+}
+
+static int train_args(const char *fn, int in_dim, int hidden, int layers, int64_t N, int64_t E) {
+  if (!train_dims_ok(in_dim, hidden, layers))
+    return fail(HF_EINVAL, std::string(fn) + ": bad model dimensions (layers <= 8)");
+  if (N < 0 || E < 0) return fail(HF_EINVAL, std::string(fn) + ": negative size");
+  if (E > 0 && N == 0) return fail(HF_EINVAL, std::string(fn) + ": edges without nodes");
+  if (N > 0x7fffffffLL || E > 0x7fffffffLL) return fail(HF_EUNSUPPORTED, std::string(fn) + ": > 2^31 nodes/edges");
+  return HF_OK;
+}
+
+int hf_graph_forward_train(const float *params, int in_dim, int hidden, int layers, const float *nf, int64_t N,
+                           const int64_t *ei, int64_t E, float *flux, void *tape, void *stream) {
+  if (int rc = train_args("hf_graph_forward_train", in_dim, hidden, layers, N, E)) return rc;
+  if (E == 0) return HF_OK;
+  if (!params || !nf || !ei || !flux || !tape) return fail(HF_EINVAL, "hf_graph_forward_train: NULL pointer");
+  const hf::GraphW w = hf::graph_view_state_dict(params, in_dim, hidden, layers);
+  HF_CHECK_HIP(hf::launch_graph_forward_train(w, nf, N, ei, E, flux, tape, as_stream(stream)),
+               "hf_graph_forward_train");
+  return HF_OK;
+}
+
+int hf_graph_backward(const float *params, int in_dim, int hidden, int layers, const float *nf, int64_t N,
+                      const int64_t *ei, int64_t E, const void *tape, const float *grad_flux, float *grad_params,
+                      float *grad_nf, void *ws, void *stream) {
+  if (int rc = train_args("hf_graph_backward", in_dim, hidden, layers, N, E)) return rc;
+  if (!params || !grad_params) return fail(HF_EINVAL, "hf_graph_backward: NULL pointer");
+  if (E > 0 && (!nf || !ei || !tape || !grad_flux || !ws)) return fail(HF_EINVAL, "hf_graph_backward: NULL pointer");
+  const hf::GraphW w = hf::graph_view_state_dict(params, in_dim, hidden, layers);
+  HF_CHECK_HIP(hf::launch_graph_backward(w, nf, N, ei, E, tape, grad_flux, grad_params, grad_nf, ws,
+                                         as_stream(stream)),
+               "hf_graph_backward");
   return HF_OK;
 }
 

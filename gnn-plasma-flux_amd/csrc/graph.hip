@@ -1,8 +1,11 @@
-// FluxGNN.forward on an arbitrary graph (src/flux_gnn.py:40-67), float32.
+// FluxGNN on an arbitrary graph (src/flux_gnn.py:40-67), float32: inference,
+// and the training forward + backward that make FluxGNN differentiable.
 //
-// This is the compatibility path for edge_index tensors that are not the
-// periodic chain (examples/smoke_test.py:53 feeds a random one).  The chain
-// — the hot path — never comes here; it runs in chain_gnn.hip.
+// This is the path for edge_index tensors that are not the periodic chain
+// (examples/smoke_test.py:53 feeds a random one) and for training on any
+// graph (scripts/training/train_ablation.py:120-206 calls loss.backward()
+// through FluxGNN).  Chain inference — the hot path — never comes here; it
+// runs in chain_f32.hip / chain_k32.hip.
 //
 //  * Mean aggregation is deterministic and in reference order: edges are
 //    bucketed by destination row into a CSR whose segments are sorted by edge
@@ -10,7 +13,14 @@
 //    index_add_ (src/flux_gnn.py:57), then divides by max(deg,1) (:58-59).
 //  * Linear layers are one LDS-tiled kernel computing
 //    act(b + W [A1[r1(m)] ; A2[r2(m)]]) with optional row gathers, so the
-//    concatenations of :60 and :62-64 are never materialised.
+//    concatenations of :60 and :62-64 are never materialised.  The weight is
+//    read through a strided view, so the same kernel multiplies by W^T in
+//    the backward pass without a transposed copy.
+//  * Weight gradients dW = sum_m delta[m] (x) X[m] are a split-K reduction
+//    over rows: each split writes its partial tile, a second kernel sums the
+//    splits in a fixed order (deterministic, no atomics).
+#include <algorithm>
+
 #include "hf_device.h"
 #include "hf_internal.h"
 
@@ -19,15 +29,23 @@ namespace {
 
 constexpr int kBM = 64, kBO = 64, kBK = 16;
 
-// out[m][o] = act(bias[o] + sum_k W[o][k] * in(m,k)),
+// weight(o, k) = k < K1 ? w1[o*so + k*si] : w2[o*so + (k-K1)*si]
+struct WView {
+  const float *w1, *w2;
+  int64_t so, si;
+};
+inline WView wv_rows(const float *W, int K1, int K) { return {W, W + K1, K, 1}; }  // nn.Linear [O][K]
+inline WView wv_t(const float *W, int Kf) { return {W, W, 1, Kf}; }              // W^T of [Kf'][Kf]
+
+// out[m][o] = act(bias[o] + sum_k weight(o,k) * in(m,k)) [* (mask[m][o] > 0)],
 // in(m,k) = k < K1 ? A1[r1(m)][k] : A2[r2(m)][k-K1],  r(m) = idx ? idx[m] : m.
 __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ A1, int K1,
                                                      const int64_t *__restrict__ idx1,
                                                      const float *__restrict__ A2, int K2,
-                                                     const int64_t *__restrict__ idx2,
-                                                     const float *__restrict__ W,
+                                                     const int64_t *__restrict__ idx2, WView W,
                                                      const float *__restrict__ bias, float *out,
-                                                     int64_t M, int O, int relu_out) {
+                                                     int64_t M, int O, int relu_out,
+                                                     const float *__restrict__ mask) {
   __shared__ float sA[kBK][kBM + 1];
   __shared__ float sW[kBK][kBO + 1];
   const int K = K1 + K2;
@@ -48,9 +66,11 @@ __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ A
       sA[kk][mm] = v;
     }
     for (int e = threadIdx.x; e < kBK * kBO; e += 256) {
-      const int kk = e % kBK, oo = e / kBK;
+      const int kk = W.si == 1 ? e % kBK : e / kBO, oo = W.si == 1 ? e / kBK : e % kBO;
       const int o = o0 + oo, k = k0 + kk;
-      sW[kk][oo] = (o < O && k < K) ? W[(int64_t)o * K + k] : 0.f;
+      float v = 0.f;
+      if (o < O && k < K) v = k < K1 ? W.w1[o * W.so + k * W.si] : W.w2[o * W.so + (k - K1) * W.si];
+      sW[kk][oo] = v;
     }
     __syncthreads();
 #pragma unroll
@@ -75,15 +95,91 @@ __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ A
     for (int q = 0; q < 4; ++q) {
       const int o = o0 + tx + 16 * q;
       if (o >= O) continue;
-      float v = __fadd_rn(acc[i][q], bias[o]);
-      out[m * O + o] = relu_out ? relu(v) : v;
+      float v = bias ? __fadd_rn(acc[i][q], bias[o]) : acc[i][q];
+      if (relu_out) v = relu(v);
+      if (mask && !(mask[m * O + o] > 0.f)) v = 0.f;
+      out[m * O + o] = v;
     }
   }
 }
 
-__global__ void count_deg_kernel(const int64_t *__restrict__ row, int64_t E, int *deg) {
+// part[s][o][k] = sum_{m in split s} D[m][o] * X(m,k) for k < K1+K2, and
+// sum D[m][o] at k = K1+K2 (bias column); X(m,k) = in(m,k) of linear_kernel.
+__global__ __launch_bounds__(256) void wgrad_kernel(const float *__restrict__ D, int O,
+                                                    const float *__restrict__ A1, int K1,
+                                                    const int64_t *__restrict__ idx1,
+                                                    const float *__restrict__ A2, int K2,
+                                                    const int64_t *__restrict__ idx2, int64_t M,
+                                                    int64_t R, float *__restrict__ part) {
+  __shared__ float sD[kBK][kBO + 1];
+  __shared__ float sX[kBK][kBM + 1];
+  const int K = K1 + K2, KB = K + 1;
+  const int o0 = blockIdx.x * kBO, k0 = blockIdx.y * kBM;
+  const int64_t mb = (int64_t)blockIdx.z * R;
+  const int64_t me = mb + R < M ? mb + R : M;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[4][4] = {};  // [o = o0 + ty + 16i][k = k0 + tx + 16q]
+  for (int64_t mm0 = mb; mm0 < me; mm0 += kBK) {
+    for (int e = threadIdx.x; e < kBK * kBO; e += 256) {
+      const int mm = e / kBO, oo = e % kBO;
+      const int64_t m = mm0 + mm;
+      const int o = o0 + oo;
+      sD[mm][oo] = (m < me && o < O) ? D[m * O + o] : 0.f;
+    }
+    for (int e = threadIdx.x; e < kBK * kBM; e += 256) {
+      const int mm = e / kBM, kk = e % kBM;
+      const int64_t m = mm0 + mm;
+      const int k = k0 + kk;
+      float v = 0.f;
+      if (m < me) {
+        if (k < K1) v = A1[(idx1 ? idx1[m] : m) * K1 + k];
+        else if (k < K) v = A2[(idx2 ? idx2[m] : m) * K2 + (k - K1)];
+        else if (k == K) v = 1.f;
+      }
+      sX[mm][kk] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int mm = 0; mm < kBK; ++mm) {
+      float d[4], x[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[i] = sD[mm][ty + 16 * i];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = sX[mm][tx + 16 * q];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][q] = fmaf(d[i], x[q], acc[i][q]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int o = o0 + ty + 16 * i;
+    if (o >= O) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k0 + tx + 16 * q;
+      if (k < KB) part[((int64_t)blockIdx.z * O + o) * KB + k] = acc[i][q];
+    }
+  }
+}
+
+// gw[o][k] = sum_s part[s][o][k] (k < K), gb[o] = sum_s part[s][o][K], s ascending.
+__global__ void wgrad_reduce_kernel(const float *__restrict__ part, int S, int O, int K, float *gw, float *gb) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int KB = K + 1;
+  if (t >= (int64_t)O * KB) return;
+  const int o = (int)(t / KB), k = (int)(t - (int64_t)o * KB);
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v = __fadd_rn(v, part[(int64_t)s * O * KB + t]);
+  if (k < K) gw[(int64_t)o * K + k] = v;
+  else if (gb) gb[o] = v;
+}
+
+__global__ void count_deg_kernel(const int64_t *__restrict__ key, int64_t E, int *deg) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < E) atomicAdd(&deg[row[e]], 1);
+  if (e < E) atomicAdd(&deg[key[e]], 1);
 }
 
 // Exclusive scan of deg[N] into off[N+1] by one 1024-thread block.
@@ -115,13 +211,12 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int *__restrict__ deg,
   if (threadIdx.x == 0) off[N] = carry;
 }
 
-__global__ void fill_kernel(const int64_t *__restrict__ row, int64_t E, int *cur,
-                            int *__restrict__ perm) {
+__global__ void fill_kernel(const int64_t *__restrict__ key, int64_t E, int *cur, int *__restrict__ perm) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < E) perm[atomicAdd(&cur[row[e]], 1)] = (int)e;
+  if (e < E) perm[atomicAdd(&cur[key[e]], 1)] = (int)e;
 }
 
-// Restore edge order inside each destination segment (insertion sort by id).
+// Restore edge order inside each segment (insertion sort by id).
 __global__ void sort_segments_kernel(const int *__restrict__ off, int64_t N, int *perm) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= N) return;
@@ -151,77 +246,317 @@ __global__ void aggregate_kernel(const float *__restrict__ h, const int64_t *__r
   agg[t] = __fdiv_rn(s, (float)(deg > 0 ? deg : 1));
 }
 
+// ------------------------------------------------------------- backward pieces
+// dz[e][f] = g[e] * w2[f] where relu(z)[e][f] > 0   (d of w2 . relu(z) + b2)
+__global__ void readout_delta_kernel(const float *__restrict__ g, const float *__restrict__ r,
+                                     const float *__restrict__ w2, int64_t E, int H, float *__restrict__ dz) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= E * H) return;
+  const int64_t e = t / H;
+  const int f = (int)(t - e * H);
+  dz[t] = r[t] > 0.f ? __fmul_rn(g[e], w2[f]) : 0.f;
+}
+
+// S_row[j] = sum over edges e with row[e] = j of dz[e]; S_col likewise by col.
+__global__ void edge_scatter_kernel(const float *__restrict__ dz, const int *__restrict__ off_r,
+                                    const int *__restrict__ perm_r, const int *__restrict__ off_c,
+                                    const int *__restrict__ perm_c, int64_t N, int H, float *__restrict__ s_row,
+                                    float *__restrict__ s_col) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * H) return;
+  const int64_t j = t / H;
+  const int f = (int)(t - j * H);
+  float a = 0.f, b = 0.f;
+  for (int p = off_r[j]; p < off_r[j + 1]; ++p) a = __fadd_rn(a, dz[(int64_t)perm_r[p] * H + f]);
+  for (int p = off_c[j]; p < off_c[j + 1]; ++p) b = __fadd_rn(b, dz[(int64_t)perm_c[p] * H + f]);
+  s_row[t] = a;
+  s_col[t] = b;
+}
+
+// Backward of h' = mlp([h ; agg(h)]) into h, then through the ReLU that made h:
+// dh[j] = dX[j][:H] + sum_{e: col[e]=j} dX[row[e]][H:] / max(deg(row[e]),1);
+// delta[j] = dh[j] where h[j] > 0.
+__global__ void agg_backward_kernel(const float *__restrict__ dX, const int64_t *__restrict__ row,
+                                    const int *__restrict__ off_r, const int *__restrict__ off_c,
+                                    const int *__restrict__ perm_c, const float *__restrict__ h, int64_t N, int H,
+                                    float *__restrict__ delta) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * H) return;
+  const int64_t j = t / H;
+  const int f = (int)(t - j * H);
+  float v = dX[j * 2 * H + f];
+  for (int p = off_c[j]; p < off_c[j + 1]; ++p) {
+    const int64_t i = row[perm_c[p]];
+    const int deg = off_r[i + 1] - off_r[i];
+    v = __fadd_rn(v, __fdiv_rn(dX[i * 2 * H + H + f], (float)(deg > 0 ? deg : 1)));
+  }
+  delta[t] = h[t] > 0.f ? v : 0.f;
+}
+
 inline size_t align256(size_t v) { return (v + 255) & ~size_t(255); }
 
-hipError_t linear(const float *A1, int K1, const int64_t *i1, const float *A2, int K2,
-                  const int64_t *i2, const float *W, const float *b, float *out, int64_t M, int O,
-                  bool act, hipStream_t s) {
+struct Carve {
+  char *p;
+  template <class T>
+  T *take(size_t n) {
+    T *r = reinterpret_cast<T *>(p);
+    p += align256(sizeof(T) * n);
+    return r;
+  }
+};
+
+hipError_t linear(const float *A1, int K1, const int64_t *i1, const float *A2, int K2, const int64_t *i2,
+                  WView W, const float *b, float *out, int64_t M, int O, bool act, hipStream_t s,
+                  const float *mask = nullptr) {
   if (M <= 0) return hipSuccess;
   dim3 grid((unsigned)((M + kBM - 1) / kBM), (unsigned)((O + kBO - 1) / kBO));
-  hipLaunchKernelGGL(linear_kernel, grid, dim3(256), 0, s, A1, K1, i1, A2, K2, i2, W, b, out, M, O,
-                     act ? 1 : 0);
+  hipLaunchKernelGGL(linear_kernel, grid, dim3(256), 0, s, A1, K1, i1, A2, K2, i2, W, b, out, M, O, act ? 1 : 0,
+                     mask);
   return hipGetLastError();
+}
+
+constexpr int64_t kMaxSplits = 128;
+inline int64_t split_rows(int64_t M) {
+  int64_t R = (M + kMaxSplits - 1) / kMaxSplits;
+  R = R < 512 ? 512 : R;
+  return (R + kBK - 1) / kBK * kBK;
+}
+
+// gw[O][K1+K2] = D^T X, gb[O] = column sums of D (gb may be NULL).
+hipError_t wgrad(const float *D, int O, const float *A1, int K1, const int64_t *i1, const float *A2, int K2,
+                 const int64_t *i2, int64_t M, float *gw, float *gb, float *part, hipStream_t s) {
+  const int K = K1 + K2;
+  if (M <= 0) {
+    hipError_t e = hipMemsetAsync(gw, 0, sizeof(float) * O * K, s);
+    if (e == hipSuccess && gb) e = hipMemsetAsync(gb, 0, sizeof(float) * O, s);
+    return e;
+  }
+  const int64_t R = split_rows(M);
+  const int S = (int)((M + R - 1) / R);
+  dim3 grid((unsigned)((O + kBO - 1) / kBO), (unsigned)((K + 1 + kBM - 1) / kBM), (unsigned)S);
+  hipLaunchKernelGGL(wgrad_kernel, grid, dim3(256), 0, s, D, O, A1, K1, i1, A2, K2, i2, M, R, part);
+  const int64_t n = (int64_t)O * (K + 1);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, S, O, K, gw,
+                     gb);
+  return hipGetLastError();
+}
+
+inline int64_t wgrad_part_floats(const GraphW &w, int64_t N, int64_t E) {
+  const int64_t H = w.hidden;
+  auto need = [](int64_t M, int64_t O, int64_t K) {
+    const int64_t R = split_rows(M > 0 ? M : 1);
+    return ((M + R - 1) / R) * O * (K + 1);
+  };
+  int64_t m = need(N, H, 2 * H);
+  m = std::max(m, need(E, H, 2 * H));
+  m = std::max(m, need(E, 1, H));
+  m = std::max(m, need(N, H, w.in_dim));
+  return m;
+}
+
+// CSR of edges bucketed by key[e] (row or col), segments sorted by edge id.
+hipError_t build_csr(const int64_t *key, int64_t E, int64_t N, int *deg, int *off, int *cur, int *perm,
+                     hipStream_t s) {
+  hipError_t err;
+  if ((err = hipMemsetAsync(deg, 0, sizeof(int) * N, s)) != hipSuccess) return err;
+  const unsigned eb = (unsigned)((E + 255) / 256), nb = (unsigned)((N + 255) / 256);
+  if (E > 0) hipLaunchKernelGGL(count_deg_kernel, dim3(eb), dim3(256), 0, s, key, E, deg);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, s, deg, N, off, cur);
+  if (E > 0) hipLaunchKernelGGL(fill_kernel, dim3(eb), dim3(256), 0, s, key, E, cur, perm);
+  hipLaunchKernelGGL(sort_segments_kernel, dim3(nb), dim3(256), 0, s, off, N, perm);
+  return hipGetLastError();
+}
+
+// Forward over a CSR already built; h[l] for l = 0..L are separate buffers
+// when `keep` (training tape), or ping-pong h[0]/h[1] otherwise.
+hipError_t forward_core(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
+                        const int *off, const int *perm, float *const *h, float *const *agg, bool keep, float *z,
+                        float *flux, hipStream_t s) {
+  const int H = w.hidden;
+  const int64_t *row = ei, *col = ei + E;
+  hipError_t err;
+  // input MLP (src/flux_gnn.py:49)
+  if ((err = linear(nf, w.in_dim, nullptr, nullptr, 0, nullptr, wv_rows(w.w_in, w.in_dim, w.in_dim), w.b_in, h[0],
+                    N, H, true, s)))
+    return err;
+  int cur = 0;
+  for (int l = 0; l < w.layers; ++l) {  // :53-60
+    const int nxt = keep ? l + 1 : 1 - cur;
+    float *a = keep ? agg[l] : agg[0];
+    const unsigned ab = (unsigned)((N * H + 255) / 256);
+    hipLaunchKernelGGL(aggregate_kernel, dim3(ab), dim3(256), 0, s, h[cur], col, off, perm, N, H, a);
+    if ((err = linear(h[cur], H, nullptr, a, H, nullptr, wv_rows(w.w_l + l * w.lsw, H, 2 * H), w.b_l + l * w.lsb,
+                      h[nxt], N, H, true, s)))
+      return err;
+    cur = nxt;
+  }
+  // edge readout (:62-66): z = ReLU(W_e [h[row] ; h[col]] + b_e); flux = w2 z + b2
+  if ((err = linear(h[cur], H, row, h[cur], H, col, wv_rows(w.w_e, H, 2 * H), w.b_e, z, E, H, true, s))) return err;
+  return linear(z, H, nullptr, nullptr, 0, nullptr, wv_rows(w.w_2, H, H), w.b_2, flux, E, 1, false, s);
+}
+
+inline int64_t param_count(const GraphW &w) {
+  const int64_t H = w.hidden;
+  return H * w.in_dim + H + w.layers * (2 * H * H + H) + 2 * H * H + H + H + 1;
+}
+
+struct Tape {
+  int *deg, *off, *cur, *perm;  // CSR by row (forward aggregation)
+  float *h[kMaxChainLayers + 1];
+  float *agg[kMaxChainLayers];
+  float *z;                     // relu(z) of the edge readout [E][H]
+};
+
+Tape carve_tape(const GraphW &w, int64_t N, int64_t E, void *base) {
+  Carve c{static_cast<char *>(base)};
+  Tape t{};
+  t.deg = c.take<int>(N);
+  t.off = c.take<int>(N + 1);
+  t.cur = c.take<int>(N);
+  t.perm = c.take<int>(E);
+  for (int l = 0; l <= w.layers; ++l) t.h[l] = c.take<float>(N * w.hidden);
+  for (int l = 0; l < w.layers; ++l) t.agg[l] = c.take<float>(N * w.hidden);
+  t.z = c.take<float>(E * w.hidden);
+  return t;
 }
 
 }  // namespace
 
+GraphW graph_view_state_dict(const float *p, int in_dim, int hidden, int layers) {
+  GraphW g{};
+  const int64_t H = hidden;
+  int64_t o = 0;
+  g.in_dim = in_dim;
+  g.hidden = hidden;
+  g.layers = layers;
+  g.w_in = p + o; o += H * in_dim;
+  g.b_in = p + o; o += H;
+  g.w_l = p + o;
+  g.b_l = p + o + H * 2 * H;
+  g.lsw = g.lsb = H * 2 * H + H;
+  o += layers * (H * 2 * H + H);
+  g.w_e = p + o; o += H * 2 * H;
+  g.b_e = p + o; o += H;
+  g.w_2 = p + o; o += H;
+  g.b_2 = p + o;
+  return g;
+}
+
 int64_t graph_workspace_bytes(const GraphW &w, int64_t N, int64_t E) {
   const int64_t H = w.hidden;
   size_t b = 0;
-  b += align256(sizeof(int) * (size_t)N);            // deg
-  b += align256(sizeof(int) * (size_t)(N + 1));      // off
-  b += align256(sizeof(int) * (size_t)N);            // cursor
-  b += align256(sizeof(int) * (size_t)E);            // perm
+  b += align256(sizeof(int) * (size_t)N);              // deg
+  b += align256(sizeof(int) * (size_t)(N + 1));        // off
+  b += align256(sizeof(int) * (size_t)N);              // cursor
+  b += align256(sizeof(int) * (size_t)E);              // perm
   b += 3 * align256(sizeof(float) * (size_t)(N * H));  // h, h', agg
-  b += align256(sizeof(float) * (size_t)(E * H));    // z
+  b += align256(sizeof(float) * (size_t)(E * H));      // z
   return (int64_t)b;
 }
 
-hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei,
-                             int64_t E, float *flux, void *ws, hipStream_t s) {
+hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
+                             float *flux, void *ws, hipStream_t s) {
   if (E <= 0) return hipSuccess;
   const int H = w.hidden;
-  char *p = static_cast<char *>(ws);
-  auto take = [&](size_t bytes) {
-    char *r = p;
-    p += align256(bytes);
-    return r;
-  };
-  int *deg = reinterpret_cast<int *>(take(sizeof(int) * N));
-  int *off = reinterpret_cast<int *>(take(sizeof(int) * (N + 1)));
-  int *cur = reinterpret_cast<int *>(take(sizeof(int) * N));
-  int *perm = reinterpret_cast<int *>(take(sizeof(int) * E));
-  float *h0 = reinterpret_cast<float *>(take(sizeof(float) * N * H));
-  float *h1 = reinterpret_cast<float *>(take(sizeof(float) * N * H));
-  float *agg = reinterpret_cast<float *>(take(sizeof(float) * N * H));
-  float *z = reinterpret_cast<float *>(take(sizeof(float) * E * H));
+  Carve c{static_cast<char *>(ws)};
+  int *deg = c.take<int>(N), *off = c.take<int>(N + 1), *cur = c.take<int>(N), *perm = c.take<int>(E);
+  float *h[2] = {c.take<float>(N * H), c.take<float>(N * H)};
+  float *agg[1] = {c.take<float>(N * H)};
+  float *z = c.take<float>(E * H);
+  hipError_t err;
+  if ((err = build_csr(ei, E, N, deg, off, cur, perm, s))) return err;
+  return forward_core(w, nf, N, ei, E, off, perm, h, agg, false, z, flux, s);
+}
+
+// ------------------------------------------------------------------ training
+int64_t graph_tape_bytes(const GraphW &w, int64_t N, int64_t E) {
+  const int64_t H = w.hidden;
+  size_t b = align256(sizeof(int) * N) * 2 + align256(sizeof(int) * (N + 1)) + align256(sizeof(int) * E);
+  b += (size_t)(2 * w.layers + 1) * align256(sizeof(float) * N * H);
+  b += align256(sizeof(float) * E * H);
+  return (int64_t)b;
+}
+
+int64_t graph_backward_ws_bytes(const GraphW &w, int64_t N, int64_t E) {
+  const int64_t H = w.hidden;
+  size_t b = align256(sizeof(float) * E * H);                    // dz
+  b += 3 * align256(sizeof(float) * N * H);                      // S_row, S_col, deltas
+  b += align256(sizeof(float) * N * 2 * H);                      // dX
+  b += align256(sizeof(float) * wgrad_part_floats(w, N, E));     // split-K partials
+  b += align256(sizeof(int) * N) * 2 + align256(sizeof(int) * (N + 1)) + align256(sizeof(int) * E);  // CSR by col
+  return (int64_t)b;
+}
+
+hipError_t launch_graph_forward_train(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
+                                      float *flux, void *tape, hipStream_t s) {
+  Tape t = carve_tape(w, N, E, tape);
+  hipError_t err;
+  if (E <= 0) return hipSuccess;  // no flux to compute; the backward returns zeros
+  if ((err = build_csr(ei, E, N, t.deg, t.off, t.cur, t.perm, s))) return err;
+  return forward_core(w, nf, N, ei, E, t.off, t.perm, t.h, t.agg, true, t.z, flux, s);
+}
+
+// Reverse of forward_core (autograd of src/flux_gnn.py:40-67).  grad_params
+// is written in state-dict order (the layout of graph_view_state_dict).
+hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
+                                 const void *tape, const float *grad_flux, float *grad_params, float *grad_nf,
+                                 void *ws, hipStream_t s) {
+  const int H = w.hidden, L = w.layers;
+  const Tape t = carve_tape(w, N, E, const_cast<void *>(tape));
+  const GraphW g = graph_view_state_dict(grad_params, w.in_dim, H, L);
+  float *gw_in = const_cast<float *>(g.w_in), *gb_in = const_cast<float *>(g.b_in);
+  float *gw_e = const_cast<float *>(g.w_e), *gb_e = const_cast<float *>(g.b_e);
+  float *gw_2 = const_cast<float *>(g.w_2), *gb_2 = const_cast<float *>(g.b_2);
   const int64_t *row = ei, *col = ei + E;
 
   hipError_t err;
-  if ((err = hipMemsetAsync(deg, 0, sizeof(int) * N, s)) != hipSuccess) return err;
-  const unsigned eb = (unsigned)((E + 255) / 256), nb = (unsigned)((N + 255) / 256);
-  hipLaunchKernelGGL(count_deg_kernel, dim3(eb), dim3(256), 0, s, row, E, deg);
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, s, deg, N, off, cur);
-  hipLaunchKernelGGL(fill_kernel, dim3(eb), dim3(256), 0, s, row, E, cur, perm);
-  hipLaunchKernelGGL(sort_segments_kernel, dim3(nb), dim3(256), 0, s, off, N, perm);
-  if ((err = hipGetLastError()) != hipSuccess) return err;
-
-  // input MLP (src/flux_gnn.py:49)
-  if ((err = linear(nf, w.in_dim, nullptr, nullptr, 0, nullptr, w.w_in, w.b_in, h0, N, H, true, s)))
-    return err;
-  for (int l = 0; l < w.layers; ++l) {  // :53-60
-    const unsigned ab = (unsigned)((N * H + 255) / 256);
-    hipLaunchKernelGGL(aggregate_kernel, dim3(ab), dim3(256), 0, s, h0, col, off, perm, N, H, agg);
-    if ((err = linear(h0, H, nullptr, agg, H, nullptr, w.w_l + (size_t)l * H * 2 * H,
-                      w.b_l + (size_t)l * H, h1, N, H, true, s)))
-      return err;
-    float *t = h0;
-    h0 = h1;
-    h1 = t;
+  if (E <= 0) {  // no edges, no flux: every gradient is zero
+    if ((err = hipMemsetAsync(grad_params, 0, sizeof(float) * param_count(w), s))) return err;
+    if (grad_nf && (err = hipMemsetAsync(grad_nf, 0, sizeof(float) * N * w.in_dim, s))) return err;
+    return hipSuccess;
   }
-  // edge readout (:62-66): z = ReLU(W_e [h[row] ; h[col]] + b_e); flux = w2 z + b2
-  if ((err = linear(h0, H, row, h0, H, col, w.w_e, w.b_e, z, E, H, true, s))) return err;
-  return linear(z, H, nullptr, nullptr, 0, nullptr, w.w_2, w.b_2, flux, E, 1, false, s);
+  Carve c{static_cast<char *>(ws)};
+  float *dz = c.take<float>(E * H);
+  float *buf[3] = {c.take<float>(N * H), c.take<float>(N * H), c.take<float>(N * H)};
+  float *dX = c.take<float>(N * 2 * H);
+  float *part = c.take<float>(wgrad_part_floats(w, N, E));
+  int *deg_c = c.take<int>(N), *off_c = c.take<int>(N + 1), *cur_c = c.take<int>(N), *perm_c = c.take<int>(E);
+  const unsigned nb = (unsigned)((N * H + 255) / 256);
+
+  if ((err = build_csr(col, E, N, deg_c, off_c, cur_c, perm_c, s))) return err;
+  // readout: flux = w2 . relu(z) + b2, z = W_e [h[row] ; h[col]] + b_e        (:62-66)
+  if ((err = wgrad(grad_flux, 1, t.z, H, nullptr, nullptr, 0, nullptr, E, gw_2, gb_2, part, s))) return err;
+  hipLaunchKernelGGL(readout_delta_kernel, dim3((unsigned)((E * H + 255) / 256)), dim3(256), 0, s, grad_flux, t.z,
+                     w.w_2, E, H, dz);
+  if ((err = wgrad(dz, H, t.h[L], H, row, t.h[L], H, col, E, gw_e, gb_e, part, s))) return err;
+  hipLaunchKernelGGL(edge_scatter_kernel, dim3(nb), dim3(256), 0, s, dz, t.off, t.perm, off_c, perm_c, N, H, buf[0],
+                     buf[1]);
+  // dh_L = W_a^T S_row + W_b^T S_col, masked by relu'(h_L): the delta of layer L-1 (or of the input MLP)
+  const WView wet{w.w_e, w.w_e + H, 1, 2 * H};
+  if ((err = linear(buf[0], H, nullptr, buf[1], H, nullptr, wet, nullptr, buf[2], N, H, false, s, t.h[L])))
+    return err;
+  int cur = 2;
+  // update layers, last to first                                                 (:53-60)
+  for (int l = L - 1; l >= 0; --l) {
+    float *gw_l = const_cast<float *>(g.w_l + l * g.lsw), *gb_l = const_cast<float *>(g.b_l + l * g.lsb);
+    if ((err = wgrad(buf[cur], H, t.h[l], H, nullptr, t.agg[l], H, nullptr, N, gw_l, gb_l, part, s))) return err;
+    // [d h_l ; d agg_l] = W_l^T delta                                             ([N][2H])
+    if ((err = linear(buf[cur], H, nullptr, nullptr, 0, nullptr, wv_t(w.w_l + l * w.lsw, 2 * H), nullptr, dX, N,
+                      2 * H, false, s)))
+      return err;
+    const int nxt = cur == 0 ? 1 : 0;
+    hipLaunchKernelGGL(agg_backward_kernel, dim3(nb), dim3(256), 0, s, dX, row, t.off, off_c, perm_c, t.h[l], N, H,
+                       buf[nxt]);
+    cur = nxt;
+  }
+  const float *delta = buf[cur];
+  // input MLP                                                                   (:49)
+  if ((err = wgrad(delta, H, nf, w.in_dim, nullptr, nullptr, 0, nullptr, N, gw_in, gb_in, part, s))) return err;
+  if (grad_nf &&
+      (err = linear(delta, H, nullptr, nullptr, 0, nullptr, wv_t(w.w_in, w.in_dim), nullptr, grad_nf, N, w.in_dim,
+                    false, s)))
+    return err;
+  return hipGetLastError();
 }
 
 }  // namespace hf

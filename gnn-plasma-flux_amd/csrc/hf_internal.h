@@ -63,11 +63,15 @@ struct ChainW {
 // Natural-layout float32 weights (device) for the generic-graph path.
 struct GraphW {
   const float *w_in, *b_in;        // [H][in], [H]
-  const float *w_l, *b_l;          // [L][H][2H], [L][H]
+  const float *w_l, *b_l;          // layer l: w_l + l*lsw [H][2H], b_l + l*lsb [H]
   const float *w_e, *b_e;          // [H][2H], [H]
   const float *w_2, *b_2;          // [H], [1]
   int in_dim, hidden, layers;
+  int64_t lsw, lsb;                // per-layer strides (grouped or state-dict order)
 };
+// View of a flat float32 parameter buffer in state-dict order (the host_params
+// order of hf_model_create): update layers interleave weight and bias.
+GraphW graph_view_state_dict(const float *p, int in_dim, int hidden, int layers);
 
 // Per-precision launchers (chain_f32.hip, chain_k32.hip); the generic entry
 // points below dispatch on ChainW::prec.
@@ -128,6 +132,14 @@ hipError_t launch_poisson(const float *n, int ld_n, float *E, int ld_E, const do
                           int nx, hipStream_t s);
 
 int64_t graph_workspace_bytes(const GraphW &w, int64_t N, int64_t E);
+// Training forward (activation tape) and backward, graph_train section of graph.hip.
+int64_t graph_tape_bytes(const GraphW &w, int64_t N, int64_t E);
+int64_t graph_backward_ws_bytes(const GraphW &w, int64_t N, int64_t E);
+hipError_t launch_graph_forward_train(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
+                                      float *flux, void *tape, hipStream_t s);
+hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
+                                 const void *tape, const float *grad_flux, float *grad_params, float *grad_nf,
+                                 void *ws, hipStream_t s);
 hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei,
                              int64_t E, float *flux, void *ws, hipStream_t s);
 

@@ -228,6 +228,54 @@ def graph_flux(model, node_features, edge_index):
     return flux
 
 
+def _graph_inputs(node_features, edge_index, in_dim):
+    require_device(node_features, "node_features")
+    nf = node_features.detach().to(torch.float32).contiguous()
+    ei = edge_index.to(device=nf.device, dtype=torch.int64).contiguous()
+    if nf.dim() != 2 or nf.shape[1] != in_dim:
+        raise ValueError(f"node_features must be [N,{in_dim}], got {tuple(nf.shape)}")
+    if ei.dim() != 2 or ei.shape[0] != 2:
+        raise ValueError(f"edge_index must be [2,E], got {tuple(ei.shape)}")
+    N, E = nf.shape[0], ei.shape[1]
+    if E:
+        lo, hi = int(ei.min()), int(ei.max())  # the reference raises IndexError on these too
+        if lo < 0 or hi >= N:
+            raise IndexError(f"edge_index entries must lie in [0, {N}), got [{lo}, {hi}]")
+    return nf, ei, N, E
+
+
+def graph_forward_train(params, dims, node_features, edge_index):
+    """Training forward (hf_graph_forward_train): params is the flat float32
+    device buffer in state-dict order.  Returns (flux [E], tape, nf, ei)."""
+    in_dim, hidden, layers = dims
+    nf, ei, N, E = _graph_inputs(node_features, edge_index, in_dim)
+    if params.device != nf.device:
+        raise RuntimeError(f"FluxGNN parameters on {params.device} but node_features on {nf.device}")
+    flux = torch.empty(E, device=nf.device)
+    tape = torch.empty(int(lib().hf_graph_tape_bytes(in_dim, hidden, layers, N, E)), dtype=torch.uint8,
+                       device=nf.device)
+    with torch.cuda.device(nf.device):
+        check(lib().hf_graph_forward_train(ptr(params), in_dim, hidden, layers, ptr(nf), N, ptr(ei), E,
+                                           ptr(flux), ptr(tape), stream_of(nf.device)))
+    return flux, tape, nf, ei
+
+
+def graph_backward(params, dims, nf, ei, tape, grad_flux, want_nf_grad):
+    """hf_graph_backward: (d params flat [P], d node_features [N,in] or None)."""
+    in_dim, hidden, layers = dims
+    N, E = nf.shape[0], ei.shape[1]
+    g = grad_flux.detach().to(device=nf.device, dtype=torch.float32).contiguous()
+    gp = torch.empty_like(params)
+    gnf = torch.empty_like(nf) if want_nf_grad else None
+    ws = torch.empty(int(lib().hf_graph_backward_workspace_bytes(in_dim, hidden, layers, N, E)),
+                     dtype=torch.uint8, device=nf.device)
+    with torch.cuda.device(nf.device):
+        check(lib().hf_graph_backward(ptr(params), in_dim, hidden, layers, ptr(nf), N, ptr(ei), E, ptr(tape),
+                                      ptr(g), ptr(gp), ptr(gnf) if gnf is not None else None, ptr(ws),
+                                      stream_of(nf.device)))
+    return gp, gnf
+
+
 def poisson(grid, n):
     """Spectral Poisson E for densities n [B,nx] (src/baseline_solver.py:59-68)."""
     require_device(n, "n")

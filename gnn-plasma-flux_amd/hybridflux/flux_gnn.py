@@ -10,8 +10,13 @@ change) into a device weight handle and the edge fluxes come from
     has MODEL_CONFIG's width (in 4, hidden 128);
   * the generic-graph kernels (graph.hip) for any other edge_index
     (examples/smoke_test.py:53 passes a random one) or width.
-There is no CPU path: CPU inputs raise.  Backward kernels are not part of this
-engine yet, so autograd through forward() raises at backward time.
+There is no CPU path: CPU inputs raise.
+
+Under autograd (grad enabled and a parameter or the node features requiring
+grad) forward() runs the generic-graph training kernels instead: the forward
+keeps an activation tape on the device and backward() runs the HIP backward
+kernels (hf_graph_backward), so `loss.backward()` in the reference trainer
+(scripts/training/train_ablation.py:203-205) works unchanged.
 """
 import torch
 import torch.nn as nn
@@ -20,16 +25,32 @@ from . import engine
 from .graph_constructor import chain_edge_index, chain_tag
 
 
-class _NoBackward(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, flux, *params):
-        return flux.view_as(flux)
+class _TrainForward(torch.autograd.Function):
+    """FluxGNN.forward with HIP backward kernels (parameter order = state dict)."""
 
     @staticmethod
-    def backward(ctx, *grads):
-        raise NotImplementedError(
-            "hybridflux FluxGNN has no backward kernels yet (differentiable hybrid step is the next "
-            "component, SURVEY.md 8f rank 2); train with the reference trainer and load the state dict")
+    def forward(ctx, node_features, edge_index, dims, *params):
+        flat = torch.cat([q.detach().reshape(-1).to(torch.float32) for q in params])
+        flux, tape, nf, ei = engine.graph_forward_train(flat, dims, node_features, edge_index)
+        ctx.save_for_backward(flat, tape, nf, ei)
+        ctx.dims = dims
+        ctx.shapes = [q.shape for q in params]
+        ctx.nf_dtype = node_features.dtype
+        return flux
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad_flux):
+        flat, tape, nf, ei = ctx.saved_tensors
+        gp, gnf = engine.graph_backward(flat, ctx.dims, nf, ei, tape, grad_flux, ctx.needs_input_grad[0])
+        grads, o = [], 0
+        for shp in ctx.shapes:
+            n = 1
+            for d in shp:
+                n *= d
+            grads.append(gp[o:o + n].view(shp))
+            o += n
+        return (gnf.to(ctx.nf_dtype) if gnf is not None else None, None, None, *grads)
 
 
 class FluxGNN(nn.Module):
@@ -90,13 +111,14 @@ class FluxGNN(nn.Module):
     def forward(self, node_features, edge_index):
         """node_features [N, input_dim] float32, edge_index [2, E] int64 -> flux [E]."""
         engine.require_device(node_features, "node_features")
+        params = list(self.parameters())
+        if torch.is_grad_enabled() and (node_features.requires_grad or any(q.requires_grad for q in params)):
+            dims = (self.input_dim, self.hidden_dim, self.num_layers)
+            return _TrainForward.apply(node_features, edge_index, dims, *params)
         dm = self.device_model(node_features.device)
         geom = self._chain_geometry(node_features, edge_index)
         if geom is not None and dm.chain_ok:
             flux = engine.chain_flux(dm, node_features.to(torch.float32), geom[0], geom[1])
         else:
             flux = engine.graph_flux(dm, node_features, edge_index)
-        if torch.is_grad_enabled() and (node_features.requires_grad or
-                                        any(p.requires_grad for p in self.parameters())):
-            return _NoBackward.apply(flux, *[p for p in self.parameters() if p.requires_grad])
         return flux

@@ -1,0 +1,157 @@
+"""FluxGNN training on the MI355X (differentiable hybrid step).
+
+Mirrors scripts/training/train_ablation.py (FluxDataset, train_model and the
+per-sample ablation loss of :107-200).  FluxGNN's forward and backward run in
+the HIP training kernels (graph.hip through FluxGNN's autograd Function); the
+loss assembly, the finite-volume update it differentiates through and Adam are
+the reference trainer's own torch expressions, executed on the device.
+
+Batching: the reference trains with batch size 1 (DataLoader(batch_size=1),
+:85).  `batch_size=1` reproduces that loop step for step; `batch_size=B`
+evaluates B samples as one batched graph (B disjoint chains) and averages the
+per-sample losses, which for every term equals the mean of the B
+single-sample losses — the batched training the survey asks for.
+
+As in the reference, the Poisson / energy terms go through a detached
+Poisson solve (there numpy, :138-145; here hf_poisson), so they contribute to
+the loss value but not to the gradient; the multi-step rollout energies depend
+only on u, which the model does not touch (:174-196).
+"""
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import engine
+from .baseline_solver import BaselineSolver
+from .config import ABLATION_CONFIGS, MODEL_CONFIG
+from .flux_gnn import FluxGNN
+from .graph_constructor import build_chain_graph_batch
+
+
+def _mse(a, b):
+    return torch.mean((a - b) ** 2)
+
+
+def _poisson_detached(grid, n):
+    """E of densities n [B,nx] without gradient (train_ablation.py:47-57 solve_poisson_np)."""
+    return engine.poisson(grid, n.detach())
+
+
+def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0):
+    """Loss of train_ablation.py:107-200 for a batch: st, st_next [B,3,nx], ft [B,nx]
+    on the device.  Returns (loss, flux_loss); B=1 is the reference formula."""
+    B, _, nx = st.shape
+    n_t, u_t = st[:, 0], st[:, 1]
+    n_next_true, u_next_true, E_next_true = st_next[:, 0], st_next[:, 1], st_next[:, 2]
+    nf, ei = build_chain_graph_batch(st, x)
+    flux_edge = model(nf, ei).reshape(B, 2 * nx)
+    F_pred = 0.5 * (flux_edge[:, :nx] + flux_edge[:, nx:])                        # :124-126
+    flux_loss = _mse(F_pred, ft)                                                   # :129
+    loss = flux_loss
+    n_next_pred = n_t - (dt / dx) * (F_pred - torch.roll(F_pred, 1, dims=-1))     # :134-135
+    if cfg["lambda_state"] > 0:
+        loss = loss + cfg["lambda_state"] * _mse(n_next_pred, n_next_true)
+    E_next_pred = None
+    if cfg["lambda_poisson"] > 0 or cfg["lambda_energy_one"] > 0:
+        E_next_pred = _poisson_detached(grid, n_next_pred)
+    if cfg["lambda_poisson"] > 0:                                                  # :140-147
+        loss = loss + cfg["lambda_poisson"] * _mse(E_next_pred, E_next_true)
+    if cfg["lambda_charge"] > 0:                                                   # :150-156
+        charge_t = torch.sum(n_t - n0, dim=-1) * dx
+        charge_next = torch.sum(n_next_pred - n0, dim=-1) * dx
+        loss = loss + cfg["lambda_charge"] * _mse(charge_next, charge_t)
+    if cfg["lambda_energy_one"] > 0:                                               # :159-170
+        e_p = 0.5 * torch.mean(u_next_true ** 2 + E_next_pred ** 2, dim=-1)
+        e_t = 0.5 * torch.mean(u_next_true ** 2 + E_next_true ** 2, dim=-1)
+        loss = loss + cfg["lambda_energy_one"] * _mse(e_p, e_t)
+    if cfg["rollout_steps"] > 0 and cfg["lambda_energy_multi"] > 0:               # :173-200
+        state = st.clone()
+        energies = []
+        for _ in range(cfg["rollout_steps"]):
+            n_r, u_r, E_r = state[:, 0], state[:, 1], state[:, 2]
+            energies.append(0.5 * torch.mean(u_r ** 2, dim=-1))
+            nf_r, ei_r = build_chain_graph_batch(state, x)
+            fe_r = model(nf_r, ei_r).reshape(B, 2 * nx)
+            F_r = 0.5 * (fe_r[:, :nx] + fe_r[:, nx:])
+            n_next_r = n_r - (dt / dx) * (F_r - torch.roll(F_r, 1, dims=-1))
+            F_u = 0.5 * u_r * u_r
+            u_next_r = u_r - (dt / dx) * (F_u - torch.roll(F_u, 1, dims=-1)) + dt * E_r
+            state = torch.stack([n_next_r, u_next_r, _poisson_detached(grid, n_next_r)], dim=1)
+        energies = torch.stack(energies)                                           # [K, B]
+        loss = loss + cfg["lambda_energy_multi"] * torch.mean((energies - energies[0]) ** 2)
+    return loss, flux_loss
+
+
+class FluxDataset:
+    """Device-resident (state_t, flux_t, state_next) triples (train_ablation.py:27-44)."""
+
+    def __init__(self, state_t, flux_t, state_next, device="cuda"):
+        assert state_t.shape == state_next.shape and state_t.shape[0] == flux_t.shape[0]
+        as_t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float32), device=device)  # noqa: E731
+        self.state_t, self.flux_t, self.state_next = as_t(state_t), as_t(flux_t), as_t(state_next)
+        self.N, self.C, self.nx = self.state_t.shape
+
+    def __len__(self):
+        return self.N
+
+    def batch(self, idx):
+        return self.state_t[idx], self.flux_t[idx], self.state_next[idx]
+
+
+def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid):
+    """One pass over `order` (sample indices) in batches; returns (sum of
+    losses, sum of flux losses) weighted by batch size, and the step count."""
+    tot, tot_flux, steps = 0.0, 0.0, 0
+    losses = []
+    for b0 in range(0, len(order), batch_size):
+        idx = order[b0:b0 + batch_size]
+        st, ft, sn = data.batch(idx)
+        loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append((loss.detach(), flux_loss.detach(), len(idx)))
+        steps += 1
+    for l, f, n in losses:  # one host sync per pass, not per step
+        tot += float(l) * n
+        tot_flux += float(f) * n
+    return tot, tot_flux, steps
+
+
+def train_model(state_t, flux_t, state_next, x, dt, dx, nu, config_name, stencil_radius, epochs=20, lr=1e-3,
+                device="cuda", batch_size=1, seed=None, save_dir="checkpoints", log=print):
+    """scripts/training/train_ablation.py:64-237 on the MI355X.  Returns
+    (model, history) and writes checkpoints/hybrid_<config>_r<radius>.pt and
+    history_<config>_r<radius>.json like the reference (save_dir=None skips)."""
+    cfg = ABLATION_CONFIGS[config_name]
+    engine.require_device(torch.empty(0, device=device), "device")
+    if seed is not None:
+        torch.manual_seed(seed)
+    data = FluxDataset(state_t, flux_t, state_next, device)
+    grid = BaselineSolver(nx=data.nx, dt=dt, nu=nu, device=device).grid
+    x_dev = torch.as_tensor(np.asarray(x, dtype=np.float32), device=device)
+    model = FluxGNN(MODEL_CONFIG["input_dim"], MODEL_CONFIG["hidden_dim"], MODEL_CONFIG["num_layers"]).to(device)
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    gen = torch.Generator().manual_seed(0 if seed is None else seed)
+    history = {"epoch": [], "loss": [], "flux_loss": [], "seconds": []}
+    model.train()
+    for epoch in range(1, epochs + 1):
+        order = torch.randperm(len(data), generator=gen).to(device)
+        t0 = time.perf_counter()
+        tot, tot_flux, _ = train_steps(model, opt, data, order, batch_size, x_dev, dt, dx, cfg, grid)
+        torch.cuda.synchronize(device)
+        history["epoch"].append(epoch)
+        history["loss"].append(tot / len(data))
+        history["flux_loss"].append(tot_flux / len(data))
+        history["seconds"].append(time.perf_counter() - t0)
+        if log:
+            log(f"[Epoch {epoch}/{epochs}] Loss: {history['loss'][-1]:.6e}, Flux: {history['flux_loss'][-1]:.6e}")
+    if save_dir is not None:
+        os.makedirs(save_dir, exist_ok=True)
+        torch.save(model.state_dict(), os.path.join(save_dir, f"hybrid_{config_name}_r{stencil_radius}.pt"))
+        with open(os.path.join(save_dir, f"history_{config_name}_r{stencil_radius}.json"), "w") as f:
+            json.dump(history, f, indent=2)
+    return model, history

@@ -107,6 +107,31 @@ int hf_graph_flux(hf_model_t model, const float *dev_node_features, int64_t N,
                   void *dev_workspace, void *stream);
 
 /*
+ * Training: FluxGNN.forward + autograd backward on any
+ * graph (src/flux_gnn.py:40-67 under loss.backward() in
+ * scripts/training/train_ablation.py:120-206).  Weights are read from a DEVICE
+ * float32 buffer dev_params in the host_params order of hf_model_create
+ * (state-dict order), so an optimizer can update them in place between steps.
+ *
+ * hf_graph_forward_train writes dev_flux[E] (as hf_graph_flux) and an
+ * activation tape (hf_graph_tape_bytes) that hf_graph_backward consumes.
+ * hf_graph_backward writes dL/dparams (overwriting, same layout as
+ * dev_params, hf_model_param_count floats) and, when dev_grad_node_features
+ * is not NULL, dL/dnode_features [N][in_dim].  dev_grad_flux is dL/dflux [E].
+ * Weight gradients are split-K sums reduced in a fixed order: bitwise
+ * deterministic for a given N, E.
+ */
+int64_t hf_graph_tape_bytes(int in_dim, int hidden, int layers, int64_t N, int64_t E);
+int64_t hf_graph_backward_workspace_bytes(int in_dim, int hidden, int layers, int64_t N, int64_t E);
+int hf_graph_forward_train(const float *dev_params, int in_dim, int hidden, int layers,
+                           const float *dev_node_features, int64_t N, const int64_t *dev_edge_index,
+                           int64_t E, float *dev_flux, void *dev_tape, void *stream);
+int hf_graph_backward(const float *dev_params, int in_dim, int hidden, int layers,
+                      const float *dev_node_features, int64_t N, const int64_t *dev_edge_index, int64_t E,
+                      const void *dev_tape, const float *dev_grad_flux, float *dev_grad_params,
+                      float *dev_grad_node_features, void *dev_workspace, void *stream);
+
+/*
  * Host helper (no device work): the Poisson "plan" for nx cells, length
  * hf_poisson_plan_len(nx) doubles.  plan[0..nx) is the first column c of the
  * real circulant matrix equal to the reference's spectral Poisson operator

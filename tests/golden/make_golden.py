@@ -28,6 +28,16 @@ hybrid_W1_r2_nx1024   same at nx=1024, dt=3.125e-4, seeds 1000..1003.
 fluxgnn_random.npz    FluxGNN(4,64,3) (seed 7) on random node features and a
                       random edge_index, as examples/smoke_test.py:45-56 does,
                       plus FluxGNN(4,128,4)=W0 on a random graph.
+grads.npz             autograd of the reference FluxGNN (src/flux_gnn.py:40-67):
+                      d(sum g*flux)/d(params, node_features) for seeded g on the
+                      two random graphs above; and the ablation training loss
+                      (scripts/training/train_ablation.py:107-206, 'full' config)
+                      with its parameter gradients on three chain samples of the
+                      classical fixture, W1_r1 weights; and a 6-step batch-size-1
+                      Adam run ('physics' config, fixed sample order): per-step
+                      losses and final weights.
+
+    python tests/golden/make_golden.py grads     # regenerate grads.npz only
 """
 import json
 import os
@@ -189,7 +199,117 @@ def make_random_graph():
     save("fluxgnn_random.npz", **arrs)
 
 
+def ref_training_loss(model, st, ft, st_next, x, dt, dx, cfg):
+    """The per-sample loss of scripts/training/train_ablation.py:107-200, with the
+    reference's own FluxGNN / build_chain_graph / solve_poisson_np."""
+    from train_ablation import solve_poisson_np
+    mse = torch.nn.MSELoss()
+    n0 = 1.0
+    n_t, u_t = st[0], st[1]
+    n_next_true, u_next_true, E_next_true = st_next[0], st_next[1], st_next[2]
+    node_features, edge_index = build_chain_graph(st, x, device="cpu")
+    flux_edge = model(node_features, edge_index)
+    nx_loc = n_t.shape[0]
+    F_pred = 0.5 * (flux_edge[:nx_loc] + flux_edge[nx_loc:])
+    flux_loss = mse(F_pred, ft)
+    loss = flux_loss
+    n_next_pred = n_t - (dt / dx) * (F_pred - torch.roll(F_pred, 1))
+    if cfg["lambda_state"] > 0:
+        loss = loss + cfg["lambda_state"] * mse(n_next_pred, n_next_true)
+    if cfg["lambda_poisson"] > 0:
+        E_pred = torch.from_numpy(solve_poisson_np(n_next_pred.detach().numpy(), n0, dx))
+        loss = loss + cfg["lambda_poisson"] * mse(E_pred, E_next_true)
+    if cfg["lambda_charge"] > 0:
+        charge_t = torch.sum(n_t - n0) * dx
+        charge_next_pred = torch.sum(n_next_pred - n0) * dx
+        loss = loss + cfg["lambda_charge"] * mse(charge_next_pred, charge_t)
+    if cfg["lambda_energy_one"] > 0:
+        E_pred = torch.from_numpy(solve_poisson_np(n_next_pred.detach().numpy(), n0, dx))
+        e_p = 0.5 * torch.mean(u_next_true ** 2 + E_pred ** 2)
+        e_t = 0.5 * torch.mean(u_next_true ** 2 + E_next_true ** 2)
+        loss = loss + cfg["lambda_energy_one"] * mse(e_p, e_t)
+    if cfg["rollout_steps"] > 0 and cfg["lambda_energy_multi"] > 0:
+        state_roll = st.clone()
+        energies = []
+        for _ in range(cfg["rollout_steps"]):
+            n_r, u_r, E_r = state_roll[0], state_roll[1], state_roll[2]
+            energies.append(0.5 * torch.mean(u_r ** 2))
+            nf_r, ei_r = build_chain_graph(state_roll, x, device="cpu")
+            fe_r = model(nf_r, ei_r)
+            F_r = 0.5 * (fe_r[:nx_loc] + fe_r[nx_loc:])
+            n_next_r = n_r - (dt / dx) * (F_r - torch.roll(F_r, 1))
+            F_u = 0.5 * u_r * u_r
+            u_next_r = u_r - (dt / dx) * (F_u - torch.roll(F_u, 1)) + dt * E_r
+            E_next_r = torch.from_numpy(solve_poisson_np(n_next_r.detach().numpy(), n0, dx))
+            state_roll = torch.stack([n_next_r, u_next_r, E_next_r], dim=0)
+        energies = torch.stack(energies)
+        loss = loss + cfg["lambda_energy_multi"] * torch.mean((energies - energies[0]) ** 2)
+    return loss, flux_loss
+
+
+def make_grads():
+    from src.config import ABLATION_CONFIGS
+    arrs = {}
+    rnd = np.load(OUT / "fluxgnn_random.npz")
+    g = torch.Generator().manual_seed(9)
+    # (1) random graphs: d(sum g*flux)
+    small = FluxGNN(input_dim=4, hidden_dim=64, num_layers=3)
+    small.load_state_dict({k[len("small."):]: torch.from_numpy(rnd[k]) for k in rnd.files if k.startswith("small.")})
+    w0 = np.load(OUT / "weights_W0.npz")
+    big = FluxGNN(input_dim=4, hidden_dim=128, num_layers=4)
+    big.load_state_dict({k: torch.from_numpy(w0[k]) for k in w0.files})
+    for tag, m in (("small", small), ("big", big)):
+        nf = torch.from_numpy(rnd[f"{tag}_nf"]).clone().requires_grad_(True)
+        ei = torch.from_numpy(rnd[f"{tag}_ei"])
+        flux = m(nf, ei)
+        gg = torch.randn(flux.shape[0], generator=g)
+        m.zero_grad()
+        (flux * gg).sum().backward()
+        arrs[f"{tag}_g"] = gg.numpy()
+        arrs[f"{tag}_grad_nf"] = nf.grad.numpy()
+        for k, p in m.named_parameters():
+            arrs[f"{tag}_grad.{k}"] = p.grad.numpy()
+    # (2) ablation loss on chain samples (classical fixture seeds 1000.., steps t -> t+1)
+    cl = np.load(OUT / "classical.npz")
+    S, F = cl["b16_states"], cl["b16_fluxes"]
+    solver = BaselineSolver(nx=64)
+    x = solver.x
+    w1 = np.load(OUT / "weights_W1_r1.npz")
+    model = FluxGNN(input_dim=4, hidden_dim=128, num_layers=4)
+    model.load_state_dict({k: torch.from_numpy(w1[k]) for k in w1.files})
+    picks = [(0, 0), (3, 11), (9, 29)]
+    for j, (ic, t) in enumerate(picks):
+        st, ft, sn = (torch.from_numpy(S[ic, t]), torch.from_numpy(F[ic, t]), torch.from_numpy(S[ic, t + 1]))
+        model.zero_grad()
+        loss, fl = ref_training_loss(model, st, ft, sn, x, solver.dt, solver.dx, ABLATION_CONFIGS["full"])
+        loss.backward()
+        arrs[f"loss{j}_value"] = np.float32(loss.item())
+        arrs[f"loss{j}_flux"] = np.float32(fl.item())
+        for k, p in model.named_parameters():
+            arrs[f"loss{j}_grad.{k}"] = p.grad.numpy()
+    arrs["loss_picks"] = np.array(picks)
+    # (3) 6 Adam steps, batch size 1, 'physics' config, fixed order          (train_ablation.py:87-210)
+    model.load_state_dict({k: torch.from_numpy(w1[k]) for k in w1.files})
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    order = [(1, 4), (7, 20), (2, 2), (12, 8), (5, 27), (14, 15)]
+    losses = []
+    for ic, t in order:
+        st, ft, sn = (torch.from_numpy(S[ic, t]), torch.from_numpy(F[ic, t]), torch.from_numpy(S[ic, t + 1]))
+        loss, _ = ref_training_loss(model, st, ft, sn, x, solver.dt, solver.dx, ABLATION_CONFIGS["physics"])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    arrs["adam_order"] = np.array(order)
+    arrs["adam_losses"] = np.array(losses, dtype=np.float64)
+    arrs.update({f"adam_final.{k}": v for k, v in sd_to_np(model.state_dict()).items()})
+    save("grads.npz", **arrs)
+
+
 def main():
+    if sys.argv[1:] == ["grads"]:
+        make_grads()
+        return
     with tempfile.TemporaryDirectory() as wd:
         make_weights(wd)
         pts = {}
@@ -202,6 +322,7 @@ def main():
         make_classical()
         make_hybrid(pts)
         make_random_graph()
+        make_grads()
     meta = {"torch": torch.__version__, "numpy": np.__version__,
             "reference": "shanedirksen/gnn-plasma-flux @ /root/reference (2026-01-02 snapshot)",
             "generator": "tests/golden/make_golden.py"}

@@ -106,13 +106,16 @@ def test_generic_graph_isolated_nodes_and_bad_index(hf):
         m(nf.to(DEV), torch.tensor([[0, 11], [1, 2]], device=DEV))
 
 
-def test_forward_autograd_is_loud(hf):
-    m = model(hf, "W0")
-    nf, ei = hf.build_chain_graph(golden("ics.npz")["ics_nx64"][0], np.linspace(0, 1, 64), DEV)
-    out = m(nf, ei)                                  # grad enabled: forward works
+def test_forward_under_autograd_matches_inference(hf):
+    """With grad enabled FluxGNN runs the training kernels (tests/test_gpu_training.py
+    covers the backward); their forward equals the fused chain kernel's."""
+    m = model(hf, "W1_r1")
+    nf, ei = hf.build_chain_graph(golden("ics.npz")["ics_nx64"][0], hf.BaselineSolver(64).x, DEV)
+    out = m(nf, ei)
     assert out.requires_grad and out.shape == (128,)
-    with pytest.raises(NotImplementedError):
-        out.sum().backward()
+    with torch.no_grad():
+        ref = m(nf, ei)
+    close(out.detach().cpu().numpy(), ref.cpu().numpy(), FLUX_ATOL)
 
 
 # ------------------------------------------------------------------- Poisson

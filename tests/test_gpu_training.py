@@ -1,0 +1,200 @@
+"""GPU parity of the differentiable path: FluxGNN forward +
+HIP backward kernels (hf_graph_forward_train / hf_graph_backward) against the
+reference's own autograd (tests/golden/grads.npz, made by make_golden.py from
+src/flux_gnn.py and scripts/training/train_ablation.py) and the CPU oracle.
+
+Tolerances: gradients are float32 sums over ~10^4 terms in a different order
+than the CPU BLAS, so each tensor is compared at
+  |got - ref| <= 2e-5 * max|ref| + 1e-9
+(the reference's own fp32 gradient differs from an fp64 evaluation at the
+1e-6 relative level).  Loss values: rtol 1e-5.  Six Adam steps: per-step loss
+rtol 1e-4; weights atol 2e-5 (Adam's first steps move each weight by ~lr
+whatever the gradient's size, so ulp-level gradient noise on tiny components
+can show up at lr scale on a handful of them: at most 0.1 % may exceed it, by
+no more than 2*lr).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import hybrid_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+REL = 2e-5
+
+
+def grads_close(got, want, rel=REL):
+    got = got.detach().cpu().numpy() if isinstance(got, torch.Tensor) else np.asarray(got)
+    scale = float(np.abs(want).max())
+    err = float(np.abs(got.astype(np.float64) - want).max())
+    assert err <= rel * scale + 1e-9, (err, scale)
+
+
+@pytest.fixture(scope="module")
+def hf():
+    import hybridflux
+    return hybridflux
+
+
+def load(hf, sd, dims):
+    m = hf.FluxGNN(*dims)
+    m.load_state_dict({k: torch.as_tensor(v) for k, v in sd.items()})
+    return m.to(DEV)
+
+
+def random_graph_model(hf, tag):
+    rnd = golden("fluxgnn_random.npz")
+    if tag == "small":
+        return load(hf, {k[6:]: rnd[k] for k in rnd.files if k.startswith("small.")}, (4, 64, 3)), rnd
+    w0 = golden("weights_W0.npz")
+    return load(hf, {k: w0[k] for k in w0.files}, (4, 128, 4)), rnd
+
+
+@pytest.mark.parametrize("tag", ["small", "big"])
+def test_backward_random_graph_vs_reference(hf, tag):
+    """d(sum g*flux)/d(params, node_features) == the reference's autograd."""
+    g = golden("grads.npz")
+    m, rnd = random_graph_model(hf, tag)
+    nf = torch.as_tensor(rnd[f"{tag}_nf"], device=DEV).requires_grad_(True)
+    ei = torch.as_tensor(rnd[f"{tag}_ei"], device=DEV)
+    flux = m(nf, ei)
+    assert flux.requires_grad
+    grads_close(flux, rnd[f"{tag}_flux"], 1e-5)
+    (flux * torch.as_tensor(g[f"{tag}_g"], device=DEV)).sum().backward()
+    grads_close(nf.grad, g[f"{tag}_grad_nf"])
+    for k, p in m.named_parameters():
+        grads_close(p.grad, g[f"{tag}_grad.{k}"])
+
+
+def test_backward_deterministic_and_chain_batch_vs_oracle(hf):
+    """Batched chains (8 ICs x 64 cells, W1_r2): gradients equal torch-CPU autograd
+    of the oracle, and two backward passes are bitwise identical."""
+    w = golden("weights_W1_r2.npz")
+    sd = {k: w[k] for k in w.files}
+    m = load(hf, sd, (4, 128, 4))
+    h = golden("hybrid_W1_r2_nx64.npz")
+    states = h["states"][:8, 5]
+    x = hf.BaselineSolver(64, device=DEV).x
+    gup = torch.randn(8 * 128, generator=torch.Generator().manual_seed(4))
+    runs = []
+    for _ in range(2):
+        m.zero_grad()
+        nf, ei = hf.build_chain_graph_batch(states, x, DEV)
+        (m(nf, ei) * gup.to(DEV)).sum().backward()
+        runs.append({k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()})
+    for k in runs[0]:
+        assert np.array_equal(runs[0][k], runs[1][k]), k
+    p = {k: v.clone().requires_grad_(True) for k, v in O.params_from(sd).items()}
+    fe = O.flux_gnn_forward(p, O.node_features(O.Grid(64), states), O.chain_edges(64, 8))
+    (fe * gup).sum().backward()
+    for k, v in p.items():
+        grads_close(runs[0][k], v.grad.numpy())
+
+
+def test_backward_edge_cases(hf):
+    """No edges -> zero gradients; isolated nodes -> gradients only where reached."""
+    m = hf.FluxGNN(4, 32, 2).to(DEV)
+    nf = torch.randn(10, 4, device=DEV, requires_grad=True)
+    out = m(nf, torch.zeros(2, 0, dtype=torch.long, device=DEV))
+    assert out.shape == (0,)
+    out.sum().backward()
+    assert all(float(p.grad.abs().max()) == 0.0 for p in m.parameters()) and float(nf.grad.abs().max()) == 0.0
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ei = torch.tensor([[0, 0, 0, 5, 5], [1, 2, 9, 0, 0]])
+    nf_c = torch.randn(10, 4, generator=torch.Generator().manual_seed(3))
+    m.zero_grad()
+    nf_d = nf_c.to(DEV).requires_grad_(True)
+    (m(nf_d, ei.to(DEV)) ** 2).sum().backward()
+    p = {k: v.clone().requires_grad_(True) for k, v in O.params_from(sd).items()}
+    nf_o = nf_c.clone().requires_grad_(True)
+    (O.flux_gnn_forward(p, nf_o, ei) ** 2).sum().backward()
+    grads_close(nf_d.grad, nf_o.grad.numpy())
+    for k, q in m.named_parameters():
+        grads_close(q.grad, p[k].grad.numpy())
+
+
+def _sample(ic, t):
+    cl = golden("classical.npz")
+    S, F = cl["b16_states"], cl["b16_fluxes"]
+    return S[ic, t], F[ic, t], S[ic, t + 1]
+
+
+def _w1_model(hf):
+    w1 = golden("weights_W1_r1.npz")
+    return load(hf, {k: w1[k] for k in w1.files}, (4, 128, 4))
+
+
+def test_ablation_loss_grads_vs_reference(hf):
+    """hybridflux.training.ablation_loss ('full' config) == train_ablation.py's
+    loss and parameter gradients on the three golden samples (B=1 each), and the
+    batched loss over all three is the mean of the three (loss and gradients)."""
+    from hybridflux.training import ablation_loss
+    g = golden("grads.npz")
+    m = _w1_model(hf)
+    solver = hf.BaselineSolver(64, device=DEV)
+    cfg = hf.ABLATION_CONFIGS["full"]
+    x = torch.as_tensor(solver.x, dtype=torch.float32, device=DEV)
+    picks = [tuple(int(v) for v in pk) for pk in g["loss_picks"]]
+    for j, (ic, t) in enumerate(picks):
+        st, ft, sn = (torch.as_tensor(a[None], device=DEV) for a in _sample(ic, t))
+        m.zero_grad()
+        loss, fl = ablation_loss(m, st, ft, sn, x, solver.dt, solver.dx, cfg, solver.grid)
+        loss.backward()
+        assert abs(loss.item() - float(g[f"loss{j}_value"])) <= 1e-5 * abs(float(g[f"loss{j}_value"]))
+        assert abs(fl.item() - float(g[f"loss{j}_flux"])) <= 1e-5 * abs(float(g[f"loss{j}_flux"]))
+        for k, p in m.named_parameters():
+            grads_close(p.grad, g[f"loss{j}_grad.{k}"])
+    batch = [np.stack(a) for a in zip(*[_sample(ic, t) for ic, t in picks])]
+    st, ft, sn = (torch.as_tensor(a, device=DEV) for a in batch)
+    m.zero_grad()
+    loss, _ = ablation_loss(m, st, ft, sn, x, solver.dt, solver.dx, cfg, solver.grid)
+    loss.backward()
+    want = np.mean([float(g[f"loss{j}_value"]) for j in range(3)])
+    assert abs(loss.item() - want) <= 1e-5 * abs(want)
+    for k, p in m.named_parameters():
+        grads_close(p.grad, np.mean([g[f"loss{j}_grad.{k}"] for j in range(3)], axis=0))
+
+
+def test_adam_steps_vs_reference(hf):
+    """Six batch-size-1 Adam steps of the reference trainer ('physics' config,
+    fixed sample order) reproduced with hybridflux.training.train_steps."""
+    from hybridflux.training import FluxDataset, train_steps
+    g = golden("grads.npz")
+    m = _w1_model(hf)
+    solver = hf.BaselineSolver(64, device=DEV)
+    order = [tuple(int(v) for v in o) for o in g["adam_order"]]
+    samples = [_sample(ic, t) for ic, t in order]
+    data = FluxDataset(np.stack([s[0] for s in samples]), np.stack([s[1] for s in samples]),
+                       np.stack([s[2] for s in samples]), DEV)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    x = torch.as_tensor(solver.x, dtype=torch.float32, device=DEV)
+    losses = []
+    for i in range(len(order)):
+        tot, _, _ = train_steps(m, opt, data, torch.tensor([i], device=DEV), 1, x, solver.dt, solver.dx,
+                                hf.ABLATION_CONFIGS["physics"], solver.grid)
+        losses.append(tot)
+    np.testing.assert_allclose(losses, g["adam_losses"], rtol=1e-4)
+    total, bad = 0, 0
+    for k, p in m.state_dict().items():
+        d = np.abs(p.cpu().numpy().astype(np.float64) - g[f"adam_final.{k}"])
+        total += d.size
+        bad += int((d > 2e-5).sum())
+        assert d.max() <= 2.1e-3, (k, d.max())
+    assert bad <= 1e-3 * total, (bad, total)
+
+
+def test_train_model_smoke(hf, tmp_path):
+    """train_model end to end on a GPU-generated dataset: loss decreases, the
+    checkpoint loads into HybridSolver (reference file layout)."""
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import train_model
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=4, steps_per_ic=16, out_path=None,
+                                                 device=DEV)
+    m, hist = train_model(st, ft, sn, x, dt, dx, nu, "physics", 2, epochs=3, lr=1e-3, device=DEV, batch_size=8,
+                          seed=1, save_dir=str(tmp_path), log=None)
+    assert len(hist["loss"]) == 3 and hist["loss"][-1] < hist["loss"][0]
+    solver = hf.HybridSolver(str(tmp_path / "hybrid_physics_r2.pt"), radius=2, device=DEV)
+    out = solver.run(st[0], 5)
+    assert out.shape == (6, 3, 64) and np.isfinite(out).all()

@@ -3,6 +3,7 @@ tests/golden/make_golden.py produced by running the reference itself.
 Every comparison here is bit-exact."""
 import numpy as np
 import pytest
+import torch
 
 from conftest import golden
 from oracle import hybrid_oracle as O
@@ -70,3 +71,47 @@ def test_random_graph_forward():
     big = O.params_from(dict(golden("weights_W0.npz")))
     got = O.flux_gnn_forward(big, torch.from_numpy(g["big_nf"]), torch.from_numpy(g["big_ei"]))
     assert np.array_equal(got.detach().numpy(), g["big_flux"])
+
+
+# ------------------------------------------------------------------ gradients
+def _grads_close(got, want, rel=1e-5):
+    scale = float(np.abs(want).max()) or 1.0
+    assert np.abs(got - want).max() <= rel * scale + 1e-12, (np.abs(got - want).max(), scale)
+
+
+@pytest.mark.parametrize("tag", ["small", "big"])
+def test_oracle_backward_random_graph_vs_reference(tag):
+    """Autograd through the oracle forward == the reference FluxGNN's autograd."""
+    g = golden("grads.npz")
+    rnd = golden("fluxgnn_random.npz")
+    if tag == "small":
+        sd = {k[6:]: rnd[k] for k in rnd.files if k.startswith("small.")}
+    else:
+        w0 = golden("weights_W0.npz")
+        sd = {k: w0[k] for k in w0.files}
+    p = {k: v.clone().requires_grad_(True) for k, v in O.params_from(sd).items()}
+    nf = torch.from_numpy(rnd[f"{tag}_nf"]).clone().requires_grad_(True)
+    flux = O.flux_gnn_forward(p, nf, torch.from_numpy(rnd[f"{tag}_ei"]))
+    (flux * torch.from_numpy(g[f"{tag}_g"])).sum().backward()
+    _grads_close(nf.grad.numpy(), g[f"{tag}_grad_nf"])
+    for k, v in p.items():
+        _grads_close(v.grad.numpy(), g[f"{tag}_grad.{k}"])
+
+
+def test_oracle_ablation_loss_vs_reference():
+    """oracle.ablation_loss == scripts/training/train_ablation.py's loss ('full'
+    config) and its parameter gradients, on the three golden samples."""
+    from hybridflux.config import ABLATION_CONFIGS
+    g = golden("grads.npz")
+    cl = golden("classical.npz")
+    w1 = golden("weights_W1_r1.npz")
+    grid = O.Grid(64)
+    for j, (ic, t) in enumerate(g["loss_picks"]):
+        p = {k: v.clone().requires_grad_(True) for k, v in O.params_from({k: w1[k] for k in w1.files}).items()}
+        S, F = cl["b16_states"], cl["b16_fluxes"]
+        loss, fl = O.ablation_loss(p, grid, S[ic, t], F[ic, t], S[ic, t + 1], ABLATION_CONFIGS["full"])
+        loss.backward()
+        assert abs(loss.item() - float(g[f"loss{j}_value"])) <= 1e-6 * abs(float(g[f"loss{j}_value"]))
+        assert abs(fl.item() - float(g[f"loss{j}_flux"])) <= 1e-6 * abs(float(g[f"loss{j}_flux"]))
+        for k, v in p.items():
+            _grads_close(v.grad.numpy(), g[f"loss{j}_grad.{k}"])
