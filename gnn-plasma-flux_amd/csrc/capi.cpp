@@ -387,25 +387,33 @@ static int train_args(const char *fn, int in_dim, int hidden, int layers, int64_
   return HF_OK;
 }
 
+static int chain_args(const char *fn, int chain_nx, int64_t N, int64_t E) {
+  if (chain_nx < 0 || (chain_nx > 0 && (N % chain_nx != 0 || E != 2 * N)))
+    return fail(HF_EINVAL, std::string(fn) + ": chain_nx must divide N with E == 2N (or be 0)");
+  return HF_OK;
+}
+
 int hf_graph_forward_train(const float *params, int in_dim, int hidden, int layers, const float *nf, int64_t N,
-                           const int64_t *ei, int64_t E, float *flux, void *tape, void *stream) {
+                           const int64_t *ei, int64_t E, int chain_nx, float *flux, void *tape, void *stream) {
   if (int rc = train_args("hf_graph_forward_train", in_dim, hidden, layers, N, E)) return rc;
+  if (int rc = chain_args("hf_graph_forward_train", chain_nx, N, E)) return rc;
   if (E == 0) return HF_OK;
   if (!params || !nf || !ei || !flux || !tape) return fail(HF_EINVAL, "hf_graph_forward_train: NULL pointer");
   const hf::GraphW w = hf::graph_view_state_dict(params, in_dim, hidden, layers);
-  HF_CHECK_HIP(hf::launch_graph_forward_train(w, nf, N, ei, E, flux, tape, as_stream(stream)),
+  HF_CHECK_HIP(hf::launch_graph_forward_train(w, nf, N, ei, E, chain_nx, flux, tape, as_stream(stream)),
                "hf_graph_forward_train");
   return HF_OK;
 }
 
 int hf_graph_backward(const float *params, int in_dim, int hidden, int layers, const float *nf, int64_t N,
-                      const int64_t *ei, int64_t E, const void *tape, const float *grad_flux, float *grad_params,
-                      float *grad_nf, void *ws, void *stream) {
+                      const int64_t *ei, int64_t E, int chain_nx, const void *tape, const float *grad_flux,
+                      float *grad_params, float *grad_nf, void *ws, void *stream) {
   if (int rc = train_args("hf_graph_backward", in_dim, hidden, layers, N, E)) return rc;
+  if (int rc = chain_args("hf_graph_backward", chain_nx, N, E)) return rc;
   if (!params || !grad_params) return fail(HF_EINVAL, "hf_graph_backward: NULL pointer");
   if (E > 0 && (!nf || !ei || !tape || !grad_flux || !ws)) return fail(HF_EINVAL, "hf_graph_backward: NULL pointer");
   const hf::GraphW w = hf::graph_view_state_dict(params, in_dim, hidden, layers);
-  HF_CHECK_HIP(hf::launch_graph_backward(w, nf, N, ei, E, tape, grad_flux, grad_params, grad_nf, ws,
+  HF_CHECK_HIP(hf::launch_graph_backward(w, nf, N, ei, E, chain_nx, tape, grad_flux, grad_params, grad_nf, ws,
                                          as_stream(stream)),
                "hf_graph_backward");
   return HF_OK;

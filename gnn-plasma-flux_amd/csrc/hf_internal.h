@@ -136,9 +136,9 @@ int64_t graph_workspace_bytes(const GraphW &w, int64_t N, int64_t E);
 int64_t graph_tape_bytes(const GraphW &w, int64_t N, int64_t E);
 int64_t graph_backward_ws_bytes(const GraphW &w, int64_t N, int64_t E);
 hipError_t launch_graph_forward_train(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
-                                      float *flux, void *tape, hipStream_t s);
+                                      int chain_nx, float *flux, void *tape, hipStream_t s);
 hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
-                                 const void *tape, const float *grad_flux, float *grad_params, float *grad_nf,
+                                 int chain_nx, const void *tape, const float *grad_flux, float *grad_params, float *grad_nf,
                                  void *ws, hipStream_t s);
 hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei,
                              int64_t E, float *flux, void *ws, hipStream_t s);

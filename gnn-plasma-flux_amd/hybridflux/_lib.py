@@ -34,10 +34,10 @@ SIGNATURES = {
                               c_void_p]),
     "hf_graph_tape_bytes": (c_int64, [c_int, c_int, c_int, c_int64, c_int64]),
     "hf_graph_backward_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int64, c_int64]),
-    "hf_graph_forward_train": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64,
+    "hf_graph_forward_train": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
                                        c_void_p, c_void_p, c_void_p]),
-    "hf_graph_backward": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
-                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hf_graph_backward": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hf_poisson_plan_len": (c_int, [c_int]),
     "hf_poisson_coeffs": (c_int, [c_int, c_double, c_void_p]),
     "hf_poisson": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p]),

@@ -237,30 +237,33 @@ def _graph_inputs(node_features, edge_index, in_dim):
     if ei.dim() != 2 or ei.shape[0] != 2:
         raise ValueError(f"edge_index must be [2,E], got {tuple(ei.shape)}")
     N, E = nf.shape[0], ei.shape[1]
-    if E:
+    from .graph_constructor import chain_tag
+    tag = chain_tag(edge_index)
+    chain_nx = tag[1] if tag is not None and tag[0] * tag[1] == N and E == 2 * N else 0
+    if E and not chain_nx:  # an unmodified tagged chain is in range by construction
         lo, hi = int(ei.min()), int(ei.max())  # the reference raises IndexError on these too
         if lo < 0 or hi >= N:
             raise IndexError(f"edge_index entries must lie in [0, {N}), got [{lo}, {hi}]")
-    return nf, ei, N, E
+    return nf, ei, N, E, chain_nx
 
 
 def graph_forward_train(params, dims, node_features, edge_index):
     """Training forward (hf_graph_forward_train): params is the flat float32
     device buffer in state-dict order.  Returns (flux [E], tape, nf, ei)."""
     in_dim, hidden, layers = dims
-    nf, ei, N, E = _graph_inputs(node_features, edge_index, in_dim)
+    nf, ei, N, E, chain_nx = _graph_inputs(node_features, edge_index, in_dim)
     if params.device != nf.device:
         raise RuntimeError(f"FluxGNN parameters on {params.device} but node_features on {nf.device}")
     flux = torch.empty(E, device=nf.device)
     tape = torch.empty(int(lib().hf_graph_tape_bytes(in_dim, hidden, layers, N, E)), dtype=torch.uint8,
                        device=nf.device)
     with torch.cuda.device(nf.device):
-        check(lib().hf_graph_forward_train(ptr(params), in_dim, hidden, layers, ptr(nf), N, ptr(ei), E,
+        check(lib().hf_graph_forward_train(ptr(params), in_dim, hidden, layers, ptr(nf), N, ptr(ei), E, chain_nx,
                                            ptr(flux), ptr(tape), stream_of(nf.device)))
-    return flux, tape, nf, ei
+    return flux, tape, nf, ei, chain_nx
 
 
-def graph_backward(params, dims, nf, ei, tape, grad_flux, want_nf_grad):
+def graph_backward(params, dims, nf, ei, chain_nx, tape, grad_flux, want_nf_grad):
     """hf_graph_backward: (d params flat [P], d node_features [N,in] or None)."""
     in_dim, hidden, layers = dims
     N, E = nf.shape[0], ei.shape[1]
@@ -270,7 +273,7 @@ def graph_backward(params, dims, nf, ei, tape, grad_flux, want_nf_grad):
     ws = torch.empty(int(lib().hf_graph_backward_workspace_bytes(in_dim, hidden, layers, N, E)),
                      dtype=torch.uint8, device=nf.device)
     with torch.cuda.device(nf.device):
-        check(lib().hf_graph_backward(ptr(params), in_dim, hidden, layers, ptr(nf), N, ptr(ei), E, ptr(tape),
+        check(lib().hf_graph_backward(ptr(params), in_dim, hidden, layers, ptr(nf), N, ptr(ei), E, chain_nx, ptr(tape),
                                       ptr(g), ptr(gp), ptr(gnf) if gnf is not None else None, ptr(ws),
                                       stream_of(nf.device)))
     return gp, gnf

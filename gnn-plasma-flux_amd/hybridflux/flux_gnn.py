@@ -31,9 +31,10 @@ class _TrainForward(torch.autograd.Function):
     @staticmethod
     def forward(ctx, node_features, edge_index, dims, *params):
         flat = torch.cat([q.detach().reshape(-1).to(torch.float32) for q in params])
-        flux, tape, nf, ei = engine.graph_forward_train(flat, dims, node_features, edge_index)
+        flux, tape, nf, ei, chain_nx = engine.graph_forward_train(flat, dims, node_features, edge_index)
         ctx.save_for_backward(flat, tape, nf, ei)
         ctx.dims = dims
+        ctx.chain_nx = chain_nx
         ctx.shapes = [q.shape for q in params]
         ctx.nf_dtype = node_features.dtype
         return flux
@@ -42,7 +43,8 @@ class _TrainForward(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, grad_flux):
         flat, tape, nf, ei = ctx.saved_tensors
-        gp, gnf = engine.graph_backward(flat, ctx.dims, nf, ei, tape, grad_flux, ctx.needs_input_grad[0])
+        gp, gnf = engine.graph_backward(flat, ctx.dims, nf, ei, ctx.chain_nx, tape, grad_flux,
+                                        ctx.needs_input_grad[0])
         grads, o = [], 0
         for shp in ctx.shapes:
             n = 1

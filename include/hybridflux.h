@@ -119,16 +119,20 @@ int hf_graph_flux(hf_model_t model, const float *dev_node_features, int64_t N,
  * dev_params, hf_model_param_count floats) and, when dev_grad_node_features
  * is not NULL, dL/dnode_features [N][in_dim].  dev_grad_flux is dL/dflux [E].
  * Weight gradients are split-K sums reduced in a fixed order: bitwise
- * deterministic for a given N, E.
+ * deterministic for a given N, E.  chain_nx > 0 declares that edge_index is
+ * N/chain_nx disjoint periodic chains of chain_nx cells in build_chain_graph
+ * order (src/graph_constructor.py:34-38, E == 2N): the edge buckets are then
+ * formed arithmetically instead of by the count/scan/fill CSR build.  0 for
+ * any other graph.
  */
 int64_t hf_graph_tape_bytes(int in_dim, int hidden, int layers, int64_t N, int64_t E);
 int64_t hf_graph_backward_workspace_bytes(int in_dim, int hidden, int layers, int64_t N, int64_t E);
 int hf_graph_forward_train(const float *dev_params, int in_dim, int hidden, int layers,
                            const float *dev_node_features, int64_t N, const int64_t *dev_edge_index,
-                           int64_t E, float *dev_flux, void *dev_tape, void *stream);
+                           int64_t E, int chain_nx, float *dev_flux, void *dev_tape, void *stream);
 int hf_graph_backward(const float *dev_params, int in_dim, int hidden, int layers,
                       const float *dev_node_features, int64_t N, const int64_t *dev_edge_index, int64_t E,
-                      const void *dev_tape, const float *dev_grad_flux, float *dev_grad_params,
+                      int chain_nx, const void *dev_tape, const float *dev_grad_flux, float *dev_grad_params,
                       float *dev_grad_node_features, void *dev_workspace, void *stream);
 
 /*

@@ -116,3 +116,18 @@ def test_no_device_fails_loudly():
     h = ctypes.c_void_p()
     rc = lib.hf_model_create(w.ctypes.data_as(ctypes.c_void_p), 4, 128, 4, 0, ctypes.byref(h))
     assert rc == _lib.HF_EHIP and b"no CPU path" in lib.hf_last_error()
+
+
+def test_training_entry_points_validate_before_device():
+    lib = _lib.lib()
+    P = lib.hf_model_param_count(4, 16, 2)
+    assert lib.hf_graph_tape_bytes(4, 16, 2, 10, 20) > 0 and lib.hf_graph_backward_workspace_bytes(4, 16, 2, 10, 20) > 0
+    assert lib.hf_graph_tape_bytes(4, 16, 9, 10, 20) == -1          # > 8 layers
+    dummy = ctypes.c_void_p(1)
+    # chain_nx must divide N and E == 2N
+    assert lib.hf_graph_forward_train(dummy, 4, 16, 2, dummy, 10, dummy, 20, 3, dummy, dummy, None) == _lib.HF_EINVAL
+    assert b"chain_nx" in lib.hf_last_error()
+    assert lib.hf_graph_backward(dummy, 4, 16, 2, dummy, 10, dummy, 19, 5, dummy, dummy, dummy, None, dummy,
+                                 None) == _lib.HF_EINVAL
+    assert lib.hf_graph_forward_train(dummy, 4, 16, 2, dummy, 0, dummy, 4, 0, dummy, dummy, None) == _lib.HF_EINVAL
+    assert P > 0

@@ -70,7 +70,8 @@ def test_backward_random_graph_vs_reference(hf, tag):
 
 def test_backward_deterministic_and_chain_batch_vs_oracle(hf):
     """Batched chains (8 ICs x 64 cells, W1_r2): gradients equal torch-CPU autograd
-    of the oracle, and two backward passes are bitwise identical."""
+    of the oracle; two backward passes are bitwise identical, and so is the
+    generic CSR path (untagged edge_index) to the arithmetic chain buckets."""
     w = golden("weights_W1_r2.npz")
     sd = {k: w[k] for k in w.files}
     m = load(hf, sd, (4, 128, 4))
@@ -84,8 +85,13 @@ def test_backward_deterministic_and_chain_batch_vs_oracle(hf):
         nf, ei = hf.build_chain_graph_batch(states, x, DEV)
         (m(nf, ei) * gup.to(DEV)).sum().backward()
         runs.append({k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()})
+    m.zero_grad()
+    nf, ei = hf.build_chain_graph_batch(states, x, DEV)
+    (m(nf, ei.clone()) * gup.to(DEV)).sum().backward()   # untagged copy: generic CSR build
+    runs.append({k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()})
     for k in runs[0]:
         assert np.array_equal(runs[0][k], runs[1][k]), k
+        assert np.array_equal(runs[0][k], runs[2][k]), k
     p = {k: v.clone().requires_grad_(True) for k, v in O.params_from(sd).items()}
     fe = O.flux_gnn_forward(p, O.node_features(O.Grid(64), states), O.chain_edges(64, 8))
     (fe * gup).sum().backward()

@@ -1,0 +1,103 @@
+"""Training-step throughput of the differentiable path.
+
+One "step" = one optimizer step of scripts/training/train_ablation.py's loop on
+`--batch` samples (loss of :107-200, loss.backward(), Adam).  Synthetic data:
+the reference dataset recipe (DATASET_CONFIG: 50 ICs x 40 steps, nx=64)
+generated on the GPU by hybridflux.datagen; random-init FluxGNN(4,128,4).
+
+Prints one JSON line: samples/s for each batch size, the dominant kernels'
+share, and the CPU baseline = the oracle's reference-faithful per-sample loop
+(torch-CPU autograd + Adam, batch size 1) on a bounded sample.
+
+    python tools/bench_train.py [--config physics] [--batches 1,64,256] [--steps 30]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gnn-plasma-flux_amd"))
+sys.path.insert(0, ROOT)
+
+
+def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver):
+    from hybridflux.training import train_steps
+    torch.manual_seed(0)
+    m = hf.FluxGNN(4, 128, 4).to("cuda")
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    cfg = hf.ABLATION_CONFIGS[cfg_name]
+    gen = torch.Generator().manual_seed(1)
+
+    def run(n):
+        order = torch.randint(0, len(data), (n * batch,), generator=gen).to("cuda")
+        return train_steps(m, opt, data, order, batch, x, solver.dt, solver.dx, cfg, solver.grid)
+
+    run(warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return steps * batch / dt, dt / steps * 1e3
+
+
+def cpu_rate(cfg_name, samples, st, ft, sn):
+    from oracle import hybrid_oracle as O
+    from hybridflux.config import ABLATION_CONFIGS
+    torch.set_num_threads(16)
+    torch.manual_seed(0)
+    import hybridflux
+    ref = hybridflux.FluxGNN(4, 128, 4)  # parameters only (CPU tensors); the oracle computes
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in ref.state_dict().items()}
+    opt = torch.optim.Adam(list(p.values()), lr=1e-3)
+    grid = O.Grid(64)
+    t0 = time.perf_counter()
+    for i in range(samples):
+        loss, _ = O.ablation_loss(p, grid, st[i], ft[i], sn[i], ABLATION_CONFIGS[cfg_name])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    return samples / (time.perf_counter() - t0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="physics")
+    ap.add_argument("--batches", default="1,64,256,2000")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-samples", type=int, default=100)
+    args = ap.parse_args()
+    import hybridflux as hf
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import FluxDataset
+    st, ft, sn, x, dt, dx, nu = generate_dataset(out_path=None, device="cuda", num_initial_conditions=50,
+                                                 steps_per_ic=40)
+    data = FluxDataset(st, ft, sn, "cuda")
+    solver = hf.BaselineSolver(64, device="cuda")
+    x_dev = torch.as_tensor(x, device="cuda")
+    rates = {}
+    for b in [int(v) for v in args.batches.split(",") if v]:
+        steps = max(2, args.steps if b > 1 else args.steps * 5)
+        r, ms = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver)
+        rates[str(b)] = {"samples_per_s": round(r, 1), "ms_per_step": round(ms, 3), "steps": steps}
+        print(f"batch {b}: {r:.1f} samples/s, {ms:.3f} ms/step", file=sys.stderr, flush=True)
+    cpu = None
+    if args.cpu_samples > 0:
+        cpu = {"value": round(cpu_rate(args.config, args.cpu_samples, st, ft, sn), 2), "unit": "samples/s",
+               "cores": 16, "kind": "port",
+               "sample": f"{args.cpu_samples} samples, batch size 1, oracle ablation_loss + torch-CPU autograd + Adam "
+                         "(the reference trainer's loop)"}
+    print(json.dumps({"metric": f"FluxGNN training samples/s ('{args.config}' ablation loss, Adam)",
+                      "unit": "samples/s", "config": {"dataset": "DATASET_CONFIG: 50 ICs x 40 steps, nx=64",
+                                                       "model": "FluxGNN(4,128,4) f32"},
+                      "gpu": rates, "cpu_baseline": cpu}))
+
+
+if __name__ == "__main__":
+    main()
