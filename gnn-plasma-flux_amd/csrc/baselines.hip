@@ -1,0 +1,265 @@
+// The reference's other rollout models, inference on the
+// MI355X: PureGNN (scripts/training/train_pure_gnn.py:35-76) and PINN
+// (scripts/training/train_pinn.py:36-61), batched over ICs, with the rollout
+// loops of scripts/evaluation/evaluate_multi_ic.py:45-83 and
+// benchmark_timing.py:100-203 (state <- state + model(state)).
+//
+// Both are built on the generic MFMA GEMM of graph.hip (gemm_linear: fused
+// bias, tanh and residual epilogues).  PureGNN's edge message
+// tanh(W [h_src ; h_dst] + b) is evaluated through the split
+// W_a h_src + W_b h_dst: two per-node GEMMs (P = W_a h, Q = W_b h) and one
+// fused gather kernel that forms every incoming message of a node, sums them
+// in edge order (index_add_, :64-66) and adds the residual (:67) — half the
+// FLOPs of an edge-wise GEMM and no [E][H] message tensor in HBM.
+#include "hf_device.h"
+#include "hf_internal.h"
+
+namespace hf {
+namespace {
+
+inline size_t a256(size_t v) { return (v + 255) & ~size_t(255); }
+
+__device__ __forceinline__ float message(const float *P, int64_t s, int H, int f, float q, float b) {
+  return tanhf(__fadd_rn(__fadd_rn(P[s * H + f], q), b));
+}
+
+// h_out[d] = h[d] + sum_{e: dst[e] = d, ascending e} tanh(P[src[e]] + Q[d] + b).
+// chain_nx > 0: B periodic chains in build_chain_graph order, where the
+// messages into cell i come from i-1 (edge i-1) then i+1 (edge nx+i).
+__global__ void message_sum_kernel(const float *__restrict__ h, const float *__restrict__ P,
+                                   const float *__restrict__ Q, const float *__restrict__ b,
+                                   const int64_t *__restrict__ src, const int *__restrict__ off,
+                                   const int *__restrict__ perm, int chain_nx, int64_t N, int H,
+                                   float *__restrict__ h_out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * H) return;
+  const int64_t d = t / H;
+  const int f = (int)(t - d * H);
+  const float q = Q[t], bf = b[f];
+  float acc = 0.f;
+  if (chain_nx > 0) {
+    const int64_t c0 = d / chain_nx * chain_nx;
+    const int i = (int)(d - c0);
+    acc = __fadd_rn(acc, message(P, c0 + (i + chain_nx - 1) % chain_nx, H, f, q, bf));
+    acc = __fadd_rn(acc, message(P, c0 + (i + 1) % chain_nx, H, f, q, bf));
+  } else {
+    for (int p = off[d]; p < off[d + 1]; ++p) acc = __fadd_rn(acc, message(P, src[perm[p]], H, f, q, bf));
+  }
+  h_out[t] = __fadd_rn(h[t], acc);
+}
+
+// node features [n, u, E, x] of every cell (benchmark_timing.py:121-125)
+__global__ void chain_features_kernel(const float *__restrict__ state, const float *__restrict__ x, int64_t B, int nx,
+                                      float *__restrict__ nf) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * nx) return;
+  const int64_t b = t / nx;
+  const int i = (int)(t - b * nx);
+  const float *s = state + b * 3 * nx;
+  reinterpret_cast<float4 *>(nf)[t] = make_float4(s[i], s[nx + i], s[2 * nx + i], x[i]);
+}
+
+// state' = state + delta^T  (delta [B*nx][3], benchmark_timing.py:128-130), written to
+// out (contiguous [B][3][nx]) and, when given, to a trajectory slot of per-IC stride ld2.
+__global__ void add_delta_kernel(const float *__restrict__ state, const float *__restrict__ delta, int64_t B, int nx,
+                                 float *__restrict__ out, float *__restrict__ out2, int64_t ld2) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * 3 * nx) return;
+  const int64_t b = t / (3 * nx);
+  const int r = (int)(t - b * 3 * nx), c = r / nx, i = r - c * nx;
+  const float v = __fadd_rn(state[t], delta[(b * nx + i) * 3 + c]);
+  out[t] = v;
+  if (out2) out2[b * ld2 + r] = v;
+}
+
+struct PureW {
+  const float *w_in, *b_in;  // [H][in], [H]
+  const float *w_l, *b_l;    // layer l at + l*(2H*H + H): [H][2H], [H]
+  const float *w_o1, *b_o1;  // [H][H], [H]
+  const float *w_o2, *b_o2;  // [3][H], [3]
+  int in_dim, H, L;
+  int64_t ls;
+};
+
+PureW pure_view(const float *p, int in_dim, int H, int L) {
+  PureW w{};
+  int64_t o = 0;
+  w.in_dim = in_dim;
+  w.H = H;
+  w.L = L;
+  w.w_in = p + o; o += (int64_t)H * in_dim;
+  w.b_in = p + o; o += H;
+  w.w_l = p + o;
+  w.b_l = p + o + 2LL * H * H;
+  w.ls = 2LL * H * H + H;
+  o += L * w.ls;
+  w.w_o1 = p + o; o += (int64_t)H * H;
+  w.b_o1 = p + o; o += H;
+  w.w_o2 = p + o; o += 3LL * H;
+  w.b_o2 = p + o;
+  return w;
+}
+
+struct PureWs {
+  float *h0, *h1, *P, *Q, *nf, *delta;
+  void *buckets;
+};
+
+PureWs carve_pure(void *ws, int H, int64_t N) {
+  char *p = static_cast<char *>(ws);
+  auto take = [&](size_t bytes) {
+    char *r = p;
+    p += a256(bytes);
+    return r;
+  };
+  PureWs w{};
+  w.h0 = reinterpret_cast<float *>(take(sizeof(float) * N * H));
+  w.h1 = reinterpret_cast<float *>(take(sizeof(float) * N * H));
+  w.P = reinterpret_cast<float *>(take(sizeof(float) * N * H));
+  w.Q = reinterpret_cast<float *>(take(sizeof(float) * N * H));
+  w.nf = reinterpret_cast<float *>(take(sizeof(float) * N * 4));
+  w.delta = reinterpret_cast<float *>(take(sizeof(float) * N * 3));
+  w.buckets = p;
+  return w;
+}
+
+// PureGNN.forward (train_pure_gnn.py:57-76) over buckets already built.
+hipError_t pure_forward(const PureW &w, const float *nf, int64_t N, const int64_t *src, const int *off,
+                        const int *perm, int chain_nx, PureWs &b, float *delta, hipStream_t s) {
+  const int H = w.H;
+  hipError_t e;
+  if ((e = gemm_linear(nf, w.in_dim, nullptr, nullptr, 0, nullptr, wv_rows(w.w_in, w.in_dim, w.in_dim), w.b_in, b.h0,
+                       N, H, kActTanh, nullptr, s)))
+    return e;
+  float *h = b.h0, *hn = b.h1;
+  const unsigned nb = (unsigned)((N * H + 255) / 256);
+  for (int l = 0; l < w.L; ++l) {
+    const float *W = w.w_l + l * w.ls;
+    if ((e = gemm_linear(h, H, nullptr, nullptr, 0, nullptr, WView{W, W, 2LL * H, 1}, nullptr, b.P, N, H, kActNone,
+                         nullptr, s)))
+      return e;
+    if ((e = gemm_linear(h, H, nullptr, nullptr, 0, nullptr, WView{W + H, W + H, 2LL * H, 1}, nullptr, b.Q, N, H,
+                         kActNone, nullptr, s)))
+      return e;
+    hipLaunchKernelGGL(message_sum_kernel, dim3(nb), dim3(256), 0, s, h, b.P, b.Q, w.b_l + l * w.ls, src, off, perm,
+                       chain_nx, N, H, hn);
+    float *t = h;
+    h = hn;
+    hn = t;
+  }
+  if ((e = gemm_linear(h, H, nullptr, nullptr, 0, nullptr, wv_rows(w.w_o1, H, H), w.b_o1, hn, N, H, kActTanh, nullptr,
+                       s)))
+    return e;
+  return gemm_linear(hn, H, nullptr, nullptr, 0, nullptr, wv_rows(w.w_o2, H, H), w.b_o2, delta, N, 3, kActNone,
+                     nullptr, s);
+}
+
+// PINN: layers 0..L-1 are net.{0,2,4,..}: D->H tanh, (L-2) x H->H tanh, H->D (+ state)
+struct PinnW {
+  const float *w[kMaxChainLayers], *b[kMaxChainLayers];
+  int D, H, L;
+};
+PinnW pinn_view(const float *p, int D, int H, int L) {
+  PinnW w{};
+  w.D = D;
+  w.H = H;
+  w.L = L;
+  int64_t o = 0;
+  for (int l = 0; l < L; ++l) {
+    const int64_t in = l == 0 ? D : H, out = l == L - 1 ? D : H;
+    w.w[l] = p + o; o += in * out;
+    w.b[l] = p + o; o += out;
+  }
+  return w;
+}
+
+}  // namespace
+
+int64_t pure_gnn_ws_bytes(int H, int64_t N, int64_t E) {
+  return (int64_t)(4 * a256(sizeof(float) * N * H) + a256(sizeof(float) * N * 4) + a256(sizeof(float) * N * 3) +
+                   2 * a256(sizeof(float) * N * 3)) +
+         edge_buckets_bytes(N, E);
+}
+
+hipError_t launch_pure_gnn_forward(const float *params, int in_dim, int H, int L, const float *nf, int64_t N,
+                                   const int64_t *ei, int64_t E, int chain_nx, float *delta, void *ws, hipStream_t s) {
+  const PureW w = pure_view(params, in_dim, H, L);
+  PureWs b = carve_pure(ws, H, N);
+  int *off = nullptr, *perm = nullptr;
+  hipError_t e;
+  if (!chain_nx && (e = edge_buckets(ei + E, E, N, 0, true, b.buckets, &off, &perm, s))) return e;  // by dst (:65)
+  return pure_forward(w, nf, N, ei, off, perm, chain_nx, b, delta, s);
+}
+
+// evaluate_multi_ic.py:45-66 for B ICs at once: traj [B][T+1][3][nx] (optional).
+hipError_t launch_pure_gnn_run(const float *params, int H, int L, const float *state0, float *final_state,
+                               const float *x, int B, int nx, int T, float *traj, void *ws, hipStream_t s) {
+  const PureW w = pure_view(params, 4, H, L);
+  const int64_t N = (int64_t)B * nx, S = 3LL * nx;
+  PureWs b = carve_pure(ws, H, N);
+  float *st[2] = {reinterpret_cast<float *>(b.buckets),
+                  reinterpret_cast<float *>(static_cast<char *>(b.buckets) + a256(sizeof(float) * N * 3))};
+  const int64_t ldt = (T + 1) * S;
+  hipError_t e;
+  if (traj && (e = hipMemcpy2DAsync(traj, sizeof(float) * ldt, state0, sizeof(float) * S, sizeof(float) * S, B,
+                                    hipMemcpyDeviceToDevice, s)))
+    return e;
+  if (T == 0) return hipMemcpyAsync(final_state, state0, sizeof(float) * N * 3, hipMemcpyDeviceToDevice, s);
+  const unsigned nb = (unsigned)((N + 255) / 256), sb = (unsigned)((N * 3 + 255) / 256);
+  const float *cur = state0;
+  for (int t = 0; t < T; ++t) {
+    hipLaunchKernelGGL(chain_features_kernel, dim3(nb), dim3(256), 0, s, cur, x, (int64_t)B, nx, b.nf);
+    if ((e = pure_forward(w, b.nf, N, nullptr, nullptr, nullptr, nx, b, b.delta, s))) return e;
+    float *nxt = t == T - 1 ? final_state : st[t & 1];
+    hipLaunchKernelGGL(add_delta_kernel, dim3(sb), dim3(256), 0, s, cur, b.delta, (int64_t)B, nx, nxt,
+                       traj ? traj + (t + 1) * S : nullptr, ldt);
+    cur = nxt;
+  }
+  return hipGetLastError();
+}
+
+int64_t pinn_ws_bytes(int D, int H, int64_t B) {
+  return (int64_t)(2 * a256(sizeof(float) * B * H) + 2 * a256(sizeof(float) * B * D));
+}
+
+hipError_t launch_pinn_forward(const float *params, int D, int H, int L, const float *state, float *out, int64_t B,
+                               void *ws, hipStream_t s) {
+  const PinnW w = pinn_view(params, D, H, L);
+  float *buf[2] = {static_cast<float *>(ws),
+                   reinterpret_cast<float *>(static_cast<char *>(ws) + a256(sizeof(float) * B * H))};
+  const float *in = state;
+  hipError_t e;
+  for (int l = 0; l < L; ++l) {
+    const int K = l == 0 ? D : H;
+    const bool last = l == L - 1;
+    float *o = last ? out : buf[l & 1];
+    if ((e = gemm_linear(in, K, nullptr, nullptr, 0, nullptr, wv_rows(w.w[l], K, K), w.b[l], o, B, last ? D : H,
+                         last ? kActNone : kActTanh, last ? state : nullptr, s)))
+      return e;
+    in = o;
+  }
+  return hipSuccess;
+}
+
+// evaluate_multi_ic.py:70-83 for B ICs at once: traj [B][T+1][D] (optional).
+hipError_t launch_pinn_run(const float *params, int D, int H, int L, const float *state0, float *final_state,
+                           int64_t B, int T, float *traj, void *ws, hipStream_t s) {
+  char *p = static_cast<char *>(ws) + 2 * a256(sizeof(float) * B * H);
+  float *st[2] = {reinterpret_cast<float *>(p), reinterpret_cast<float *>(p + a256(sizeof(float) * B * D))};
+  const size_t row = sizeof(float) * D, ldt = row * (T + 1);
+  hipError_t e;
+  if (traj && (e = hipMemcpy2DAsync(traj, ldt, state0, row, row, B, hipMemcpyDeviceToDevice, s))) return e;
+  if (T == 0) return hipMemcpyAsync(final_state, state0, row * B, hipMemcpyDeviceToDevice, s);
+  const float *cur = state0;
+  for (int t = 0; t < T; ++t) {
+    float *nxt = t == T - 1 ? final_state : st[t & 1];
+    if ((e = launch_pinn_forward(params, D, H, L, cur, nxt, B, ws, s))) return e;
+    if (traj && (e = hipMemcpy2DAsync(reinterpret_cast<char *>(traj) + (t + 1) * row, ldt, nxt, row, row, B,
+                                      hipMemcpyDeviceToDevice, s)))
+      return e;
+    cur = nxt;
+  }
+  return hipSuccess;
+}
+
+}  // namespace hf

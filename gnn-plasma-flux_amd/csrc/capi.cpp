@@ -419,6 +419,83 @@ int hf_graph_backward(const float *params, int in_dim, int hidden, int layers, c
   return HF_OK;
 }
 
+// ------------------------------------------------------- PureGNN / PINN
+int64_t hf_pure_gnn_param_count(int in_dim, int hidden, int layers) {
+  if (in_dim < 1 || hidden < 1 || layers < 0) return -1;
+  const int64_t H = hidden;
+  return H * in_dim + H + layers * (2 * H * H + H) + H * H + H + 3 * H + 3;
+}
+
+int64_t hf_pure_gnn_workspace_bytes(int hidden, int64_t N, int64_t E) {
+  if (hidden < 1 || N < 0 || E < 0) return -1;
+  return hf::pure_gnn_ws_bytes(hidden, N, E);
+}
+
+int hf_pure_gnn_forward(const float *params, int in_dim, int hidden, int layers, const float *nf, int64_t N,
+                        const int64_t *ei, int64_t E, int chain_nx, float *delta, void *ws, void *stream) {
+  if (in_dim < 1 || hidden < 1 || layers < 0) return fail(HF_EINVAL, "hf_pure_gnn_forward: bad model dimensions");
+  if (N < 0 || E < 0) return fail(HF_EINVAL, "hf_pure_gnn_forward: negative size");
+  if (E > 0 && N == 0) return fail(HF_EINVAL, "hf_pure_gnn_forward: edges without nodes");
+  if (int rc = chain_args("hf_pure_gnn_forward", chain_nx, N, E)) return rc;
+  if (N == 0) return HF_OK;
+  if (!params || !nf || !delta || !ws || (E > 0 && !ei)) return fail(HF_EINVAL, "hf_pure_gnn_forward: NULL pointer");
+  HF_CHECK_HIP(hf::launch_pure_gnn_forward(params, in_dim, hidden, layers, nf, N, ei, E, chain_nx, delta, ws,
+                                           as_stream(stream)),
+               "hf_pure_gnn_forward");
+  return HF_OK;
+}
+
+int hf_pure_gnn_run(const float *params, int hidden, int layers, const float *state0, float *final_state,
+                    const float *x, int B, int nx, int T, float *traj, void *ws, void *stream) {
+  if (hidden < 1 || layers < 0 || B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_pure_gnn_run: bad argument");
+  if (B == 0) return HF_OK;
+  if (!params || !state0 || !final_state || !x || !ws) return fail(HF_EINVAL, "hf_pure_gnn_run: NULL pointer");
+  HF_CHECK_HIP(hf::launch_pure_gnn_run(params, hidden, layers, state0, final_state, x, B, nx, T, traj, ws,
+                                       as_stream(stream)),
+               "hf_pure_gnn_run");
+  return HF_OK;
+}
+
+int64_t hf_pinn_param_count(int dim, int hidden, int layers) {
+  if (dim < 1 || hidden < 1 || layers < 2 || layers > hf::kMaxChainLayers) return -1;
+  const int64_t D = dim, H = hidden;
+  return (D * H + H) + (layers - 2) * (H * H + H) + (H * D + D);
+}
+
+int64_t hf_pinn_workspace_bytes(int dim, int hidden, int64_t B) {
+  if (dim < 1 || hidden < 1 || B < 0) return -1;
+  return hf::pinn_ws_bytes(dim, hidden, B);
+}
+
+static int pinn_args(const char *fn, int dim, int hidden, int layers, int64_t B) {
+  if (dim < 1 || hidden < 1 || layers < 2 || layers > hf::kMaxChainLayers || B < 0)
+    return fail(HF_EINVAL, std::string(fn) + ": bad argument (2 <= layers <= 8)");
+  return HF_OK;
+}
+
+int hf_pinn_forward(const float *params, int dim, int hidden, int layers, const float *state, float *out, int64_t B,
+                    void *ws, void *stream) {
+  if (int rc = pinn_args("hf_pinn_forward", dim, hidden, layers, B)) return rc;
+  if (B == 0) return HF_OK;
+  if (!params || !state || !out || !ws) return fail(HF_EINVAL, "hf_pinn_forward: NULL pointer");
+  if (state == out) return fail(HF_EINVAL, "hf_pinn_forward: state and out must not alias");
+  HF_CHECK_HIP(hf::launch_pinn_forward(params, dim, hidden, layers, state, out, B, ws, as_stream(stream)),
+               "hf_pinn_forward");
+  return HF_OK;
+}
+
+int hf_pinn_run(const float *params, int dim, int hidden, int layers, const float *state0, float *final_state,
+                int64_t B, int T, float *traj, void *ws, void *stream) {
+  if (int rc = pinn_args("hf_pinn_run", dim, hidden, layers, B)) return rc;
+  if (T < 0) return fail(HF_EINVAL, "hf_pinn_run: T < 0");
+  if (B == 0) return HF_OK;
+  if (!params || !state0 || !final_state || !ws) return fail(HF_EINVAL, "hf_pinn_run: NULL pointer");
+  HF_CHECK_HIP(hf::launch_pinn_run(params, dim, hidden, layers, state0, final_state, B, T, traj, ws,
+                                   as_stream(stream)),
+               "hf_pinn_run");
+  return HF_OK;
+}
+
 int hf_poisson_plan_len(int nx) { return nx < 1 ? -1 : hf::poisson_plan_len(nx); }
 
 int hf_poisson_coeffs(int nx, double length, double *c) {

@@ -28,13 +28,6 @@ namespace hf {
 namespace {
 
 
-// weight(o, k) = k < K1 ? w1[o*so + k*si] : w2[o*so + (k-K1)*si]
-struct WView {
-  const float *w1, *w2;
-  int64_t so, si;
-};
-inline WView wv_rows(const float *W, int K1, int K) { return {W, W + K1, K, 1}; }  // nn.Linear [O][K]
-inline WView wv_t(const float *W, int Kf) { return {W, W, 1, Kf}; }              // W^T of [Kf'][Kf]
 
 // ------------------------------------------------------------ MFMA GEMM core
 // C[i][j] = sum_{r in [rb, re)} A(i, r) * B(j, r) for a 64 x 64 tile, on
@@ -154,10 +147,11 @@ __device__ __forceinline__ void gemm_tile(const OA &A, const OB &B, int64_t i0, 
   }
 }
 
-// out[m][o] = act(bias[o] + sum_k weight(o,k) * in(m,k)) [* (mask[m][o] > 0)].
+// out[m][o] = resid[m][o] + act(bias[o] + sum_k weight(o,k) * in(m,k)) [* (mask[m][o] > 0)].
 template <bool WRF>
 __global__ __launch_bounds__(256) void linear_kernel(OpIn in, OpW<WRF> w, const float *__restrict__ bias,
-                                                     float *out, int relu_out, const float *__restrict__ mask) {
+                                                     float *out, int act, const float *__restrict__ mask,
+                                                     const float *__restrict__ resid) {
   const int64_t m0 = (int64_t)blockIdx.x * kT;
   const int o0 = blockIdx.y * kT;
   f4v acc[2][2];
@@ -176,8 +170,10 @@ __global__ __launch_bounds__(256) void linear_kernel(OpIn in, OpW<WRF> w, const 
         const int64_t m = m0 + 32 * (wave >> 1) + 16 * ta + 4 * (lane >> 4) + x;
         if (m >= in.M) continue;
         float v = bias ? __fadd_rn(acc[ta][tb][x], bo) : acc[ta][tb][x];
-        if (relu_out) v = relu(v);
+        if (act == kActRelu) v = relu(v);
+        else if (act == kActTanh) v = tanhf(v);
         if (mask && !(mask[m * O + o] > 0.f)) v = 0.f;
+        if (resid) v = __fadd_rn(resid[m * O + o], v);
         out[m * O + o] = v;
       }
     }
@@ -357,17 +353,17 @@ struct Carve {
 };
 
 hipError_t linear(const float *A1, int K1, const int64_t *i1, const float *A2, int K2, const int64_t *i2,
-                  WView W, const float *b, float *out, int64_t M, int O, bool act, hipStream_t s,
-                  const float *mask = nullptr) {
+                  WView W, const float *b, float *out, int64_t M, int O, int act, hipStream_t s,
+                  const float *mask = nullptr, const float *resid = nullptr) {
   if (M <= 0) return hipSuccess;
   dim3 grid((unsigned)((M + kT - 1) / kT), (unsigned)((O + kT - 1) / kT));
   const OpIn in{A1, A2, i1, i2, K1, K2, M};
   if (W.si == 1)
     hipLaunchKernelGGL(linear_kernel<false>, grid, dim3(256), 0, s, in, OpW<false>{W, O, K1 + K2, K1}, b, out,
-                       act ? 1 : 0, mask);
+                       act, mask, resid);
   else
     hipLaunchKernelGGL(linear_kernel<true>, grid, dim3(256), 0, s, in, OpW<true>{W, O, K1 + K2, K1}, b, out,
-                       act ? 1 : 0, mask);
+                       act, mask, resid);
   return hipGetLastError();
 }
 
@@ -453,7 +449,7 @@ hipError_t forward_core(const GraphW &w, const float *nf, int64_t N, const int64
   hipError_t err;
   // input MLP (src/flux_gnn.py:49)
   if ((err = linear(nf, w.in_dim, nullptr, nullptr, 0, nullptr, wv_rows(w.w_in, w.in_dim, w.in_dim), w.b_in, h[0],
-                    N, H, true, s)))
+                    N, H, kActRelu, s)))
     return err;
   int cur = 0;
   for (int l = 0; l < w.layers; ++l) {  // :53-60
@@ -462,13 +458,13 @@ hipError_t forward_core(const GraphW &w, const float *nf, int64_t N, const int64
     const unsigned ab = (unsigned)((N * H + 255) / 256);
     hipLaunchKernelGGL(aggregate_kernel, dim3(ab), dim3(256), 0, s, h[cur], col, off, perm, N, H, a);
     if ((err = linear(h[cur], H, nullptr, a, H, nullptr, wv_rows(w.w_l + l * w.lsw, H, 2 * H), w.b_l + l * w.lsb,
-                      h[nxt], N, H, true, s)))
+                      h[nxt], N, H, kActRelu, s)))
       return err;
     cur = nxt;
   }
   // edge readout (:62-66): z = ReLU(W_e [h[row] ; h[col]] + b_e); flux = w2 z + b2
-  if ((err = linear(h[cur], H, row, h[cur], H, col, wv_rows(w.w_e, H, 2 * H), w.b_e, z, E, H, true, s))) return err;
-  return linear(z, H, nullptr, nullptr, 0, nullptr, wv_rows(w.w_2, H, H), w.b_2, flux, E, 1, false, s);
+  if ((err = linear(h[cur], H, row, h[cur], H, col, wv_rows(w.w_e, H, 2 * H), w.b_e, z, E, H, kActRelu, s))) return err;
+  return linear(z, H, nullptr, nullptr, 0, nullptr, wv_rows(w.w_2, H, H), w.b_2, flux, E, 1, kActNone, s);
 }
 
 inline int64_t param_count(const GraphW &w) {
@@ -497,6 +493,25 @@ Tape carve_tape(const GraphW &w, int64_t N, int64_t E, void *base) {
 }
 
 }  // namespace
+
+hipError_t gemm_linear(const float *A1, int K1, const int64_t *i1, const float *A2, int K2, const int64_t *i2,
+                       WView W, const float *b, float *out, int64_t M, int O, int act, const float *resid,
+                       hipStream_t s) {
+  return linear(A1, K1, i1, A2, K2, i2, W, b, out, M, O, act, s, nullptr, resid);
+}
+
+hipError_t edge_buckets(const int64_t *key, int64_t E, int64_t N, int chain_nx, bool by_col, void *ws,
+                        int **off, int **perm, hipStream_t s) {
+  Carve c{static_cast<char *>(ws)};
+  int *deg = c.take<int>(N), *o = c.take<int>(N + 1), *cur = c.take<int>(N), *p = c.take<int>(E);
+  *off = o;
+  *perm = p;
+  return build_csr(key, E, N, deg, o, cur, p, s, chain_nx, by_col);
+}
+
+int64_t edge_buckets_bytes(int64_t N, int64_t E) {
+  return (int64_t)(2 * align256(sizeof(int) * N) + align256(sizeof(int) * (N + 1)) + align256(sizeof(int) * E));
+}
 
 GraphW graph_view_state_dict(const float *p, int in_dim, int hidden, int layers) {
   GraphW g{};
@@ -609,7 +624,7 @@ hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, co
                      buf[1]);
   // dh_L = W_a^T S_row + W_b^T S_col, masked by relu'(h_L): the delta of layer L-1 (or of the input MLP)
   const WView wet{w.w_e, w.w_e + H, 1, 2 * H};
-  if ((err = linear(buf[0], H, nullptr, buf[1], H, nullptr, wet, nullptr, buf[2], N, H, false, s, t.h[L])))
+  if ((err = linear(buf[0], H, nullptr, buf[1], H, nullptr, wet, nullptr, buf[2], N, H, kActNone, s, t.h[L])))
     return err;
   int cur = 2;
   // update layers, last to first                                                 (:53-60)
@@ -618,7 +633,7 @@ hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, co
     if ((err = wgrad(buf[cur], H, t.h[l], H, nullptr, t.agg[l], H, nullptr, N, gw_l, gb_l, part, s))) return err;
     // [d h_l ; d agg_l] = W_l^T delta                                             ([N][2H])
     if ((err = linear(buf[cur], H, nullptr, nullptr, 0, nullptr, wv_t(w.w_l + l * w.lsw, 2 * H), nullptr, dX, N,
-                      2 * H, false, s)))
+                      2 * H, kActNone, s)))
       return err;
     const int nxt = cur == 0 ? 1 : 0;
     hipLaunchKernelGGL(agg_backward_kernel, dim3(nb), dim3(256), 0, s, dX, row, t.off, off_c, perm_c, t.h[l], N, H,
@@ -630,7 +645,7 @@ hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, co
   if ((err = wgrad(delta, H, nf, w.in_dim, nullptr, nullptr, 0, nullptr, N, gw_in, gb_in, part, s))) return err;
   if (grad_nf &&
       (err = linear(delta, H, nullptr, nullptr, 0, nullptr, wv_t(w.w_in, w.in_dim), nullptr, grad_nf, N, w.in_dim,
-                    false, s)))
+                    kActNone, s)))
     return err;
   return hipGetLastError();
 }

@@ -69,6 +69,36 @@ struct GraphW {
   int in_dim, hidden, layers;
   int64_t lsw, lsb;                // per-layer strides (grouped or state-dict order)
 };
+// Strided weight view for the generic MFMA GEMM (graph.hip):
+// weight(o, k) = k < K1 ? w1[o*so + k*si] : w2[o*so + (k-K1)*si].
+struct WView {
+  const float *w1, *w2;
+  int64_t so, si;
+};
+inline WView wv_rows(const float *W, int K1, int K) { return {W, W + K1, K, 1}; }  // nn.Linear [O][K]
+inline WView wv_t(const float *W, int Kf) { return {W, W, 1, Kf}; }              // W^T of [Kf'][Kf]
+enum { kActNone = 0, kActRelu = 1, kActTanh = 2 };
+// out[m][o] = resid[m][o] + act(b[o] + sum_k weight(o,k) in(m,k)), in(m,k) = [A1[i1(m)] ; A2[i2(m)]][k].
+hipError_t gemm_linear(const float *A1, int K1, const int64_t *i1, const float *A2, int K2, const int64_t *i2,
+                       WView W, const float *b, float *out, int64_t M, int O, int act, const float *resid,
+                       hipStream_t s);
+// Edges bucketed by key (row or col), ascending edge id per bucket; chain_nx > 0: arithmetic buckets.
+int64_t edge_buckets_bytes(int64_t N, int64_t E);
+hipError_t edge_buckets(const int64_t *key, int64_t E, int64_t N, int chain_nx, bool by_col, void *ws, int **off,
+                        int **perm, hipStream_t s);
+
+// PureGNN / PINN inference (baselines.hip).
+int64_t pure_gnn_ws_bytes(int H, int64_t N, int64_t E);
+hipError_t launch_pure_gnn_forward(const float *params, int in_dim, int H, int L, const float *nf, int64_t N,
+                                   const int64_t *ei, int64_t E, int chain_nx, float *delta, void *ws, hipStream_t s);
+hipError_t launch_pure_gnn_run(const float *params, int H, int L, const float *state0, float *final_state,
+                               const float *x, int B, int nx, int T, float *traj, void *ws, hipStream_t s);
+int64_t pinn_ws_bytes(int D, int H, int64_t B);
+hipError_t launch_pinn_forward(const float *params, int D, int H, int L, const float *state, float *out, int64_t B,
+                               void *ws, hipStream_t s);
+hipError_t launch_pinn_run(const float *params, int D, int H, int L, const float *state0, float *final_state,
+                           int64_t B, int T, float *traj, void *ws, hipStream_t s);
+
 // View of a flat float32 parameter buffer in state-dict order (the host_params
 // order of hf_model_create): update layers interleave weight and bias.
 GraphW graph_view_state_dict(const float *p, int in_dim, int hidden, int layers);

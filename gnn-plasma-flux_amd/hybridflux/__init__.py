@@ -6,6 +6,7 @@ points (step_batch / run_batch), the engine module and the multi-GPU
 IC-sharded rollout driver.
 """
 from .baseline_solver import BaselineSolver
+from .baselines import PINN, PureGNN
 from .config import ABLATION_CONFIGS, DATASET_CONFIG, EVAL_CONFIG, MODEL_CONFIG, STENCIL_RADII, TRAIN_CONFIG
 from .flux_gnn import FluxGNN
 from .graph_constructor import build_chain_graph, build_chain_graph_batch, chain_edge_index
@@ -13,6 +14,8 @@ from .hybrid_solver import HybridSolver
 
 __all__ = [
     "BaselineSolver",
+    "PureGNN",
+    "PINN",
     "FluxGNN",
     "HybridSolver",
     "build_chain_graph",

@@ -38,6 +38,17 @@ SIGNATURES = {
                                        c_void_p, c_void_p, c_void_p]),
     "hf_graph_backward": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hf_pure_gnn_param_count": (c_int64, [c_int, c_int, c_int]),
+    "hf_pure_gnn_workspace_bytes": (c_int64, [c_int, c_int64, c_int64]),
+    "hf_pure_gnn_forward": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
+                                    c_void_p, c_void_p, c_void_p]),
+    "hf_pure_gnn_run": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                c_void_p, c_void_p]),
+    "hf_pinn_param_count": (c_int64, [c_int, c_int, c_int]),
+    "hf_pinn_workspace_bytes": (c_int64, [c_int, c_int, c_int64]),
+    "hf_pinn_forward": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "hf_pinn_run": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p,
+                            c_void_p]),
     "hf_poisson_plan_len": (c_int, [c_int]),
     "hf_poisson_coeffs": (c_int, [c_int, c_double, c_void_p]),
     "hf_poisson": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p]),

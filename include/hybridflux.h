@@ -136,6 +136,40 @@ int hf_graph_backward(const float *dev_params, int in_dim, int hidden, int layer
                       float *dev_grad_node_features, void *dev_workspace, void *stream);
 
 /*
+ * The reference's other rollout models, inference.
+ * dev_params: every parameter, float32, state-dict order, on the device.
+ *
+ * PureGNN (scripts/training/train_pure_gnn.py:35-76): input_mlp.0 [H][in],
+ * update_mlps.l.0 [H][2H] (+bias) for each layer, output_mlp.0 [H][H],
+ * output_mlp.2 [3][H] (+biases); tanh activations, residual message passing.
+ * hf_pure_gnn_forward = PureGNN.forward(node_features [N][in], edge_index
+ * [2][E]) -> delta [N][3]; chain_nx as for hf_graph_forward_train.
+ * hf_pure_gnn_run = the rollout of scripts/evaluation/evaluate_multi_ic.py:45-66
+ * (state <- state + delta, node features [n,u,E,x]) for B ICs on chains of nx
+ * cells: state0/final [B][3][nx], traj [B][T+1][3][nx] or NULL; x [nx].
+ * Workspace: hf_pure_gnn_workspace_bytes(H, N = B*nx, E = 2N).
+ *
+ * PINN (scripts/training/train_pinn.py:36-61): net.0 [H][D], (layers-2) x
+ * [H][H], net.last [D][H] (+biases), tanh between; out = state + net(state)
+ * on states flattened to D = 3*nx.  hf_pinn_run = evaluate_multi_ic.py:70-83
+ * for B ICs: state0/final [B][D], traj [B][T+1][D] or NULL.
+ */
+int64_t hf_pure_gnn_param_count(int in_dim, int hidden, int layers);
+int64_t hf_pure_gnn_workspace_bytes(int hidden, int64_t N, int64_t E);
+int hf_pure_gnn_forward(const float *dev_params, int in_dim, int hidden, int layers,
+                        const float *dev_node_features, int64_t N, const int64_t *dev_edge_index, int64_t E,
+                        int chain_nx, float *dev_delta, void *dev_workspace, void *stream);
+int hf_pure_gnn_run(const float *dev_params, int hidden, int layers, const float *dev_state0,
+                    float *dev_final, const float *dev_x, int B, int nx, int T, float *dev_traj,
+                    void *dev_workspace, void *stream);
+int64_t hf_pinn_param_count(int dim, int hidden, int layers);
+int64_t hf_pinn_workspace_bytes(int dim, int hidden, int64_t B);
+int hf_pinn_forward(const float *dev_params, int dim, int hidden, int layers, const float *dev_state,
+                    float *dev_out, int64_t B, void *dev_workspace, void *stream);
+int hf_pinn_run(const float *dev_params, int dim, int hidden, int layers, const float *dev_state0,
+                float *dev_final, int64_t B, int T, float *dev_traj, void *dev_workspace, void *stream);
+
+/*
  * Host helper (no device work): the Poisson "plan" for nx cells, length
  * hf_poisson_plan_len(nx) doubles.  plan[0..nx) is the first column c of the
  * real circulant matrix equal to the reference's spectral Poisson operator

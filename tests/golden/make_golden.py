@@ -37,7 +37,15 @@ grads.npz             autograd of the reference FluxGNN (src/flux_gnn.py:40-67):
                       Adam run ('physics' config, fixed sample order): per-step
                       losses and final weights.
 
-    python tests/golden/make_golden.py grads     # regenerate grads.npz only
+baselines.npz         the reference's other rollout models:
+                      PureGNN(4,128,4) (seed 11) and PINN(192,256,4) (seed 12)
+                      from scripts/training/train_pure_gnn.py:35-76 and
+                      train_pinn.py:36-61 — their weights, PureGNN on a random
+                      graph, and 10-step rollouts of ICs 1000..1003 with the
+                      loops of scripts/evaluation/evaluate_multi_ic.py:45-83.
+
+    python tests/golden/make_golden.py grads       # regenerate grads.npz only
+    python tests/golden/make_golden.py baselines   # regenerate baselines.npz only
 """
 import json
 import os
@@ -306,9 +314,61 @@ def make_grads():
     save("grads.npz", **arrs)
 
 
+def make_baselines():
+    from train_pure_gnn import PureGNN
+    from train_pinn import PINN
+    arrs = {}
+    solver = BaselineSolver(nx=64)
+    x = solver.x
+    seeds = [1000, 1001, 1002, 1003]
+    ics = np.stack([solver.initial_condition(seed=s) for s in seeds])
+    torch.manual_seed(11)
+    pg = PureGNN(input_dim=4, hidden_dim=128, num_layers=4).eval()
+    torch.manual_seed(12)
+    pinn = PINN(input_dim=3 * 64, hidden_dim=256, num_layers=4).eval()
+    arrs.update({f"pure_gnn.{k}": v for k, v in sd_to_np(pg.state_dict()).items()})
+    arrs.update({f"pinn.{k}": v for k, v in sd_to_np(pinn.state_dict()).items()})
+    x_torch = torch.FloatTensor(x)
+    traj_g, traj_p = [], []
+    with torch.no_grad():
+        for ic in ics:                       # evaluate_multi_ic.py:45-66
+            state = ic.copy()
+            st = [state.copy()]
+            for _ in range(10):
+                _, edge_index = build_chain_graph(state, x, "cpu")
+                nf = torch.FloatTensor(state).permute(1, 0)
+                nf = torch.cat([nf, x_torch.unsqueeze(1)], dim=1)
+                delta = pg(nf, edge_index)
+                state = (torch.FloatTensor(state).permute(1, 0) + delta).permute(1, 0).numpy()
+                st.append(state.copy())
+            traj_g.append(np.array(st))
+        for ic in ics:                       # evaluate_multi_ic.py:70-83
+            state = ic.copy()
+            st = [state.copy()]
+            for _ in range(10):
+                state = pinn(torch.FloatTensor(state).unsqueeze(0))[0].numpy()
+                st.append(state.copy())
+            traj_p.append(np.array(st))
+        g = torch.Generator().manual_seed(13)
+        nf = torch.randn(50, 4, generator=g)
+        ei = torch.randint(0, 50, (2, 170), generator=g)
+        arrs["pure_gnn_graph_nf"], arrs["pure_gnn_graph_ei"] = nf.numpy(), ei.numpy()
+        arrs["pure_gnn_graph_delta"] = pg(nf, ei).numpy()
+        batch = torch.from_numpy(ics[:3])
+        arrs["pinn_batch_out"] = pinn(batch).numpy()   # batched forward, [3,3,64]
+    arrs["seeds"] = np.array(seeds)
+    arrs["ics"] = ics
+    arrs["pure_gnn_traj"] = np.stack(traj_g).astype(np.float32)
+    arrs["pinn_traj"] = np.stack(traj_p).astype(np.float32)
+    save("baselines.npz", **arrs)
+
+
 def main():
     if sys.argv[1:] == ["grads"]:
         make_grads()
+        return
+    if sys.argv[1:] == ["baselines"]:
+        make_baselines()
         return
     with tempfile.TemporaryDirectory() as wd:
         make_weights(wd)
@@ -323,6 +383,7 @@ def main():
         make_hybrid(pts)
         make_random_graph()
         make_grads()
+        make_baselines()
     meta = {"torch": torch.__version__, "numpy": np.__version__,
             "reference": "shanedirksen/gnn-plasma-flux @ /root/reference (2026-01-02 snapshot)",
             "generator": "tests/golden/make_golden.py"}

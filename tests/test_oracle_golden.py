@@ -115,3 +115,29 @@ def test_oracle_ablation_loss_vs_reference():
         assert abs(fl.item() - float(g[f"loss{j}_flux"])) <= 1e-6 * abs(float(g[f"loss{j}_flux"]))
         for k, v in p.items():
             _grads_close(v.grad.numpy(), g[f"loss{j}_grad.{k}"])
+
+
+# ------------------------------------------------------------ PureGNN / PINN
+def _sub(d, prefix):
+    return O.params_from({k[len(prefix):]: d[k] for k in d.files if k.startswith(prefix)})
+
+
+def test_oracle_pure_gnn_and_pinn_vs_reference():
+    """Oracle restatements of PureGNN / PINN == the reference classes' outputs
+    (rollouts of evaluate_multi_ic.py:45-83, a random graph, a batched PINN call)."""
+    b = golden("baselines.npz")
+    grid = O.Grid(64)
+    pg, pn = _sub(b, "pure_gnn."), _sub(b, "pinn.")
+    with torch.no_grad():
+        d = O.pure_gnn_forward(pg, torch.from_numpy(b["pure_gnn_graph_nf"]), torch.from_numpy(b["pure_gnn_graph_ei"]))
+        np.testing.assert_allclose(d.numpy(), b["pure_gnn_graph_delta"], atol=2e-6, rtol=1e-5)
+        out = O.pinn_forward(pn, torch.from_numpy(b["ics"][:3]))
+        np.testing.assert_allclose(out.numpy(), b["pinn_batch_out"], atol=2e-6, rtol=1e-5)
+        for j, ic in enumerate(b["ics"]):
+            np.testing.assert_allclose(O.pure_gnn_rollout(pg, grid, ic, 10), b["pure_gnn_traj"][j], atol=1e-5, rtol=1e-5)
+            s = torch.from_numpy(ic)
+            traj = [ic]
+            for _ in range(10):
+                s = O.pinn_forward(pn, s[None])[0]
+                traj.append(s.numpy())
+            np.testing.assert_allclose(np.array(traj), b["pinn_traj"][j], atol=1e-5, rtol=1e-5)
