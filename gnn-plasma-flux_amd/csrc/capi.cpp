@@ -130,6 +130,9 @@ void pack_chain(const float *p, int L, int prec, ChainPack &P) {
               const int s = 4 * gi + (j >> 1), nt = 4 * (j & 1) + cc;
               const int k = (s < kKS ? 0 : kH) + kperm(s % kKS, lane);
               v = layer_w(l)[(int64_t)(16 * nt + (lane & 15)) * 2 * kH + k];
+              // the 1/deg = 1/2 of the mean aggregation is folded into W_b (an exact
+              // power-of-two scaling: w*(s/2) == (w/2)*s bit for bit)
+              if (s >= kKS) v *= 0.5f;
             } else {
               const int r = c - 16 * L, ot = r / 2, hh = r % 2;
               const int s = 16 * hh + 2 * j + (cc >> 1), pq = cc & 1;

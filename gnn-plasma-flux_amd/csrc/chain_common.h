@@ -3,12 +3,16 @@
 // (FluxGNN.forward on B chains; the persistent hybrid rollout) written once
 // over a precision "core" that supplies the GNN forward.
 //
-// Layout conventions shared by every core (one wave = 64 cells of one IC):
+// Layout conventions shared by every core (one wave = 16*MT cells of one IC):
 //   A 16x16 MFMA accumulator tile of a transposed GEMM Out^T = W X^T holds, in
-//   lane l, cell m = 16*mt + (l&15) and features n = 16*nt + 4*(l>>4) + r,
-//   r = 0..3.  Cells therefore lie along the 16 lanes of a DPP row: the chain
-//   neighbours m-1 / m+1 are row_shr:1 / row_shl:1, with the lane that falls
-//   off the row patched from the adjacent m-tile by row_ror (periodic wrap).
+//   lane l, features n = 16*nt + 4*(l>>4) + r (r = 0..3) of one cell per lane
+//   column j = l&15.  The MT m-tiles are INTERLEAVED along the chain: tile mt,
+//   column j holds cell MT*j + mt (cell_of).  The chain neighbours of a cell
+//   are then the same lane of the adjacent tile, except across the tile-0 /
+//   tile-(MT-1) seam, where they are one lane over: row_ror:1 / row_ror:15 of
+//   that tile, which is also exactly the periodic wrap.  The neighbour mean
+//   therefore costs one VALU per value (a plain add, or an add with a DPP
+//   operand) instead of a shift, two seam patches and the add.
 //
 // Weight ring: a workgroup is 4 waves (4 ICs or windows, one per SIMD) that
 // consume the same packed weight stream in lockstep.  The stream is a list of
@@ -50,44 +54,42 @@ __device__ __forceinline__ float dpp_over(float old, float v) {
       __builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
-// Value of cell m+1 for every lane (periodic over the MT m-tiles of the wave).
-template <int MT>
-__device__ __forceinline__ void right_nb(const float (&v)[MT], float (&r)[MT]) {
-  float rot[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) rot[mt] = dpp_mov<kRowRor15>(v[mt]);
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) r[mt] = dpp_over<kRowShl1>(rot[(mt + 1) % MT], v[mt]);
-}
-// Value of cell m-1 for every lane.
-template <int MT>
-__device__ __forceinline__ void left_nb(const float (&v)[MT], float (&l)[MT]) {
-  float rot[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) rot[mt] = dpp_mov<kRowRor1>(v[mt]);
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) l[mt] = dpp_over<kRowShr1>(rot[(mt + MT - 1) % MT], v[mt]);
-}
-
-// Lanes whose DPP source falls outside their row read 0 (bound_ctrl), so the
-// mov folds into the consuming v_add_f32 as a DPP operand.
+// Lanes read the DPP source without masking (row rotations have no
+// out-of-row lanes), so the mov folds into a consuming VALU op as its DPP operand.
 template <int CTRL>
 __device__ __forceinline__ float dpp_zero(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
-// v[i+1] + v[i-1] for every cell (periodic over the MT m-tiles), 4 VALU per
-// value: the in-row pair, then the wrap lane from each neighbouring tile.  The
-// extra terms are exact +0s, so the result is bit-identical to the two-term
-// sum the reference's index_add_ forms (src/flux_gnn.py:57).
+// Cell held by column j of m-tile mt (interleaved layout, see above).
+template <int MT>
+__device__ __forceinline__ int cell_of(int mt, int j) { return MT * j + mt; }
+
+// Value of cell m+1 for every lane (periodic over the 16*MT cells of the wave).
+template <int MT>
+__device__ __forceinline__ void right_nb(const float (&v)[MT], float (&r)[MT]) {
+#pragma unroll
+  for (int mt = 0; mt < MT - 1; ++mt) r[mt] = v[mt + 1];
+  r[MT - 1] = dpp_zero<kRowRor15>(v[0]);  // cell MT*j + MT = MT*(j+1) + 0
+}
+// Value of cell m-1 for every lane.
+template <int MT>
+__device__ __forceinline__ void left_nb(const float (&v)[MT], float (&l)[MT]) {
+  l[0] = dpp_zero<kRowRor1>(v[MT - 1]);  // cell MT*j - 1 = MT*(j-1) + MT-1
+#pragma unroll
+  for (int mt = 1; mt < MT; ++mt) l[mt] = v[mt - 1];
+}
+
+// v[i+1] + v[i-1] for every cell, one VALU per value: a single fp32 add of the
+// two neighbours, bit-identical to the two-term sum the reference's
+// index_add_ forms (src/flux_gnn.py:57; fp add is commutative).
 template <int MT>
 __device__ __forceinline__ void nb_sum(const float (&v)[MT], float (&s)[MT]) {
+  float l[MT], r[MT];
+  left_nb<MT>(v, l);
+  right_nb<MT>(v, r);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    float t = __fadd_rn(dpp_zero<kRowShl1>(v[mt]), dpp_zero<kRowShr1>(v[mt]));  // lane 15 / lane 0 get 0
-    t = __fadd_rn(t, dpp_zero<kRowShl15>(v[(mt + MT - 1) % MT]));              // lane 0 += tile mt-1, lane 15
-    s[mt] = __fadd_rn(t, dpp_zero<kRowShr15>(v[(mt + 1) % MT]));               // lane 15 += tile mt+1, lane 0
-  }
+  for (int mt = 0; mt < MT; ++mt) s[mt] = __fadd_rn(l[mt], r[mt]);
 }
 
 __device__ __forceinline__ f4 relu4(f4 v) { return f4{relu(v.x), relu(v.y), relu(v.z), relu(v.w)}; }
@@ -133,13 +135,24 @@ struct Ring {
   int pos;           // stream position being consumed (slot = pos & 3)
   int ahead;         // chunk id of stream position pos + 2
 
+  // The DMA is issued from inline asm, hidden from hipcc's s_waitcnt
+  // bookkeeping: with a visible LDS-DMA in the kernel hipcc gives every
+  // ds_read an lgkmcnt(0) wait, which serialises the fragment prefetch.  The
+  // ring's own counted vmcnt + barrier in next() order the DMA for readers.
   __device__ __forceinline__ void issue(int chunk, int slot) const {
     const float *g = src + (size_t)chunk * CF + lane * 4;
-    float *d = lds + slot * CF;
+    const unsigned d = (unsigned)(uintptr_t)(lds_void *)(lds + slot * CF);
 #pragma unroll
     for (int jj = 0; jj < kPerWave; ++jj) {
       const int j = kPerWave * wave + jj;  // this wave's quarter of the chunk
-      __builtin_amdgcn_global_load_lds(g + j * 256, (lds_void *)(d + j * 256), 16, 0, 0);
+      const unsigned dst = __builtin_amdgcn_readfirstlane(d + j * 1024);
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(g + j * 256), "s"(dst)
+          : "memory");
     }
   }
   // Start the stream at chunk 0 (positions 0 and 1 in flight).
@@ -154,10 +167,18 @@ struct Ring {
     // own DMA for `pos` done (only pos+1's instructions may remain), every
     // ds_read of this wave retired, then every wave has passed: the slot of
     // pos-2, which pos+2 is about to overwrite, is no longer read by anyone.
+    // sched_barrier(0) on both sides: the compiler may otherwise move register-only
+    // MFMAs across the asm, which orders memory operations only.
+    __builtin_amdgcn_sched_barrier(0);
+#ifdef HF_DIAG_NOBAR  // timing diagnostic only: results are wrong
+    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+#else
     if constexpr (kPerWave == 2)
       asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+    __builtin_amdgcn_sched_barrier(0);
     issue(ahead, (pos + 2) & (kRingSlots - 1));
     ahead = ahead + 1 == chunks ? 0 : ahead + 1;
     const float *slot = lds + (pos & (kRingSlots - 1)) * CF;
@@ -266,6 +287,8 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
   const int lane = R.lane, j = lane & 15, g = lane >> 4;
   __syncthreads();  // small weights staged (no DMA in flight yet)
   R.prime();
+  typename Core::Feed F;
+  Core::begin(R, F);
   // Persistent over groups of 4 items: the weight stream keeps flowing from one
   // group's forward pass into the next, so the ring fill is paid once per workgroup.
   const int64_t groups = (items + kWaves - 1) / kWaves;
@@ -280,18 +303,18 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
     int cell[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      int cidx = (start + 16 * mt + j) % nx;
+      int cidx = (start + cell_of<MT>(mt, j)) % nx;
       if (cidx < 0) cidx += nx;
       cell[mt] = cidx;
       feat[mt] = nf ? nf[(b * nx + cidx) * kIn + g]
                     : (g < 3 ? state[b * ld_state + (int64_t)g * nx + cidx] : x[cidx]);
     }
     float f_fwd[MT], f_bwd[MT];
-    Core::template gnn<MT>(W, S, R, park_of<Core>(lds, R.wave), feat, f_fwd, f_bwd);
+    Core::template gnn<MT>(W, S, R, F, park_of<Core>(lds, R.wave), feat, f_fwd, f_bwd);
     if (live) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int wc = 16 * mt + j;
+        const int wc = cell_of<MT>(mt, j);
         int face = cell[mt];
         bool ok = true;
         if (!EXACT) {
@@ -387,15 +410,17 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
   };
   emit(0);
   R.prime();
+  typename Core::Feed F;
+  Core::begin(R, F);
   for (int t = 0; t < T; ++t) {
     float feat[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) feat[mt] = s_st[g * 64 + 16 * mt + j];
+    for (int mt = 0; mt < MT; ++mt) feat[mt] = s_st[g * 64 + cell_of<MT>(mt, j)];
     float f_fwd[MT], f_bwd[MT];
-    Core::template gnn<MT>(W, S, R, park, feat, f_fwd, f_bwd);
+    Core::template gnn<MT>(W, S, R, F, park, feat, f_fwd, f_bwd);
     if (g == 0) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) s_F[16 * mt + j] = face_flux(f_fwd[mt], f_bwd[mt]);
+      for (int mt = 0; mt < MT; ++mt) s_F[cell_of<MT>(mt, j)] = face_flux(f_fwd[mt], f_bwd[mt]);
     }
     if (twin && lane < NX) s_Fc[lane] = __fmul_rn(s_cl[lane], s_cl[64 + lane]);  // F_n = n*u
     wave_lds_sync();

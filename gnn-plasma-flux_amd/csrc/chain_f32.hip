@@ -22,50 +22,108 @@ namespace {
 using namespace chain;
 
 struct CoreF32 {
-  static constexpr int kChunkFloats = 2048;  // 8 KiB: 4 k-steps x 8 tiles, or 16 k-steps x (P, Q)
+  static constexpr int kChunkFloats = 2048;  // 8 KiB: 4 units of 2 KiB (2 ds_read_b128 per lane)
   static constexpr int kParkFloats = 0;
   using R_t = Ring<kChunkFloats>;
 
-  static __device__ __forceinline__ void read_chunk(const float *slot, int lane, f4 (&v)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = ldf4(slot + (j * 64 + lane) * 4);
+  // Register-prefetched weight feed.  A chunk is 4 units; unit u is the lane's
+  // fragments 2u, 2u+1 and feeds 32 MFMAs (one update k-step, or four readout
+  // k-steps of P and Q).  The ds_reads of unit u+1 are issued before the MFMAs
+  // of unit u, so LDS latency hides under a whole unit of matrix work; the
+  // ring's wait + barrier for chunk p+1 moves to before the last unit of p.
+  // The feed runs continuously over forward passes (begin() once per kernel).
+  struct Feed {
+    const float *slot;
+    f4 cur[2];
+  };
+  static __device__ __forceinline__ void load_unit(Feed &F, int u, int lane) {
+    F.cur[0] = ldf4(F.slot + ((2 * u) * 64 + lane) * 4);
+    F.cur[1] = ldf4(F.slot + ((2 * u + 1) * 64 + lane) * 4);
   }
-
-  // One update-layer chunk: k-steps s = 4*gi + q.  The first 8 chunks of a
-  // layer read h itself, the last 8 the neighbour mean (h[i+1] + h[i-1]) / 2.
-  template <int MT, int GI>
-  static __device__ __forceinline__ void layer_chunk(R_t &R, const f4 (&h)[MT][kNT], f4 (&acc)[MT][kNT]) {
-    f4 v[8];
-    read_chunk(R.next(), R.lane, v);
+  static __device__ __forceinline__ void begin(R_t &R, Feed &F) {
+    F.slot = R.next();
+    load_unit(F, 0, R.lane);
+  }
+  // Hand out unit U of the current chunk and start reading the next unit.
+  template <int U>
+  static __device__ __forceinline__ void take(R_t &R, Feed &F, f4 (&a)[2]) {
+    a[0] = F.cur[0];
+    a[1] = F.cur[1];
+    if constexpr (U == 3) F.slot = R.next();
+#ifndef HF_DIAG_NODS  // timing diagnostic only: results are wrong
+    load_unit(F, (U + 1) & 3, R.lane);
+#endif
+  }
+  // B operand of flat k-step KS (0..63) of an update layer: k-steps 0..31 read
+  // h itself, 32..63 the neighbour mean (h[i+1] + h[i-1]) / 2.
+  template <int MT, int KS>
+  static __device__ __forceinline__ void b_operand(const f4 (&h)[MT][kNT], float (&b)[MT]) {
+    constexpr int s = KS % kKS;  // k-step within its 128-wide half
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      constexpr int kHalf = kKS / 4;
-      const int s = (GI % kHalf) * 4 + q;  // k-step within its 128-wide half
-      float b[MT];
+    for (int mt = 0; mt < MT; ++mt) b[mt] = h[mt][s >> 2][s & 3];
+#ifdef HF_DIAG_NONB  // timing diagnostic only: results are wrong
+    if constexpr (false) {
+#else
+    if constexpr (KS >= kKS) {
+#endif
+      float sum[MT];
+      nb_sum<MT>(b, sum);  // index_add_ of h[i+1], h[i-1]; the / deg 2 is folded into W_b
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) b[mt] = h[mt][s >> 2][s & 3];
-      if (GI >= kHalf) {
-        float sum[MT];
-        nb_sum<MT>(b, sum);  // index_add_ of h[i+1], h[i-1]
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) b[mt] = __fmul_rn(sum[mt], 0.5f);  // / deg 2 (exact)
-      }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = mfma4(v[2 * q + (nt >> 2)][nt & 3], b[mt], acc[mt][nt]);
+      for (int mt = 0; mt < MT; ++mt) b[mt] = sum[mt];
     }
   }
 
-  // One readout chunk: k-steps s = 16*HH + qq for P (W_e[:, :H]) and Q (W_e[:, H:]).
-  template <int MT, int HH>
-  static __device__ __forceinline__ void readout_chunk(R_t &R, const f4 (&h)[MT][kNT], f4 (&P)[MT], f4 (&Q)[MT]) {
-    f4 v[8];
-    read_chunk(R.next(), R.lane, v);
+  // Update-layer k-step KS (unit KS & 3 of its chunk).  b holds this k-step's
+  // B operand on entry and the next k-step's on exit: the next operand's lane
+  // shifts are interleaved with this k-step's MFMAs instead of stalling the
+  // matrix pipe between m-tiles.
+  template <int MT, int KS>
+  static __device__ __forceinline__ void layer_step(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
+                                                    f4 (&acc)[MT][kNT]) {
+    f4 a[2];
+    take<KS & 3>(R, F, a);
+    float bn[MT];
+    if constexpr (KS + 1 < 2 * kKS) b_operand<MT, KS + 1>(h, bn);
 #pragma unroll
-    for (int qq = 0; qq < 16; ++qq) {
-      const int s = 16 * HH + qq;
-      const float ap = v[qq >> 1][2 * (qq & 1)], aq = v[qq >> 1][2 * (qq & 1) + 1];
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = mfma4(a[nt >> 2][nt & 3], b[mt], acc[mt][nt]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // next unit's ds_reads first
+    if constexpr (KS + 1 >= kKS && KS + 1 < 2 * kKS) {
+      // one VALU per m-tile for the next operand, after every other MFMA
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, MT * kNT - 2 * MT, 0);
+    } else {
+      __builtin_amdgcn_sched_group_barrier(0x008, MT * kNT, 0);
+    }
+    if constexpr (KS + 1 < 2 * kKS) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) b[mt] = bn[mt];
+    }
+  }
+  template <int MT, int KS0>
+  static __device__ __forceinline__ void layer_chunk(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
+                                                     f4 (&acc)[MT][kNT]) {
+    layer_step<MT, KS0 + 0>(R, F, h, b, acc);
+    layer_step<MT, KS0 + 1>(R, F, h, b, acc);
+    layer_step<MT, KS0 + 2>(R, F, h, b, acc);
+    layer_step<MT, KS0 + 3>(R, F, h, b, acc);
+  }
+
+  // One readout unit: k-steps s = 16*HH + 4*U + i for P (W_e[:, :H]) and Q (W_e[:, H:]).
+  template <int MT, int HH, int U>
+  static __device__ __forceinline__ void readout_unit(R_t &R, Feed &F, const f4 (&h)[MT][kNT], f4 (&P)[MT],
+                                                      f4 (&Q)[MT]) {
+    f4 a[2];
+    take<U>(R, F, a);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = 16 * HH + 4 * U + i;
+      const float ap = a[i >> 1][2 * (i & 1)], aq = a[i >> 1][2 * (i & 1) + 1];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const float b = h[mt][s >> 2][s & 3];
@@ -73,16 +131,25 @@ struct CoreF32 {
         Q[mt] = mfma4(aq, b, Q[mt]);
       }
     }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // next unit's ds_reads first
+    __builtin_amdgcn_sched_group_barrier(0x008, 8 * MT, 0);
+  }
+  template <int MT, int HH>
+  static __device__ __forceinline__ void readout_chunk(R_t &R, Feed &F, const f4 (&h)[MT][kNT], f4 (&P)[MT],
+                                                       f4 (&Q)[MT]) {
+    readout_unit<MT, HH, 0>(R, F, h, P, Q);
+    readout_unit<MT, HH, 1>(R, F, h, P, Q);
+    readout_unit<MT, HH, 2>(R, F, h, P, Q);
+    readout_unit<MT, HH, 3>(R, F, h, P, Q);
   }
 
   // FluxGNN forward for the MT*16 cells of this wave.  feat[mt] is the lane's
-  // input feature (index l>>4 of [n,u,E,x]) of cell 16*mt + (l&15).  Returns
+  // input feature (index l>>4 of [n,u,E,x]) of cell cell_of<MT>(mt, l&15).  Returns
   // the edge fluxes of (i -> i+1) in ffwd and of (i+1 -> i) in fbwd for cell
   // i, on every lane of the cell's column.  Consumes one pass of the stream.
   template <int MT>
-  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, float * /*park*/,
-                                             const float (&feat)[MT],
-                                             float (&ffwd)[MT], float (&fbwd)[MT]) {
+  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &F, float * /*park*/,
+                                             const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
     const int lane = R.lane;
     const int g4 = 4 * (lane >> 4);
     f4 h[MT][kNT];
@@ -95,22 +162,24 @@ struct CoreF32 {
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
-      layer_chunk<MT, 0>(R, h, acc);
-      layer_chunk<MT, 1>(R, h, acc);
-      layer_chunk<MT, 2>(R, h, acc);
-      layer_chunk<MT, 3>(R, h, acc);
-      layer_chunk<MT, 4>(R, h, acc);
-      layer_chunk<MT, 5>(R, h, acc);
-      layer_chunk<MT, 6>(R, h, acc);
-      layer_chunk<MT, 7>(R, h, acc);
-      layer_chunk<MT, 8>(R, h, acc);
-      layer_chunk<MT, 9>(R, h, acc);
-      layer_chunk<MT, 10>(R, h, acc);
-      layer_chunk<MT, 11>(R, h, acc);
-      layer_chunk<MT, 12>(R, h, acc);
-      layer_chunk<MT, 13>(R, h, acc);
-      layer_chunk<MT, 14>(R, h, acc);
-      layer_chunk<MT, 15>(R, h, acc);
+      float b[MT];
+      b_operand<MT, 0>(h, b);
+      layer_chunk<MT, 0>(R, F, h, b, acc);
+      layer_chunk<MT, 4>(R, F, h, b, acc);
+      layer_chunk<MT, 8>(R, F, h, b, acc);
+      layer_chunk<MT, 12>(R, F, h, b, acc);
+      layer_chunk<MT, 16>(R, F, h, b, acc);
+      layer_chunk<MT, 20>(R, F, h, b, acc);
+      layer_chunk<MT, 24>(R, F, h, b, acc);
+      layer_chunk<MT, 28>(R, F, h, b, acc);
+      layer_chunk<MT, 32>(R, F, h, b, acc);
+      layer_chunk<MT, 36>(R, F, h, b, acc);
+      layer_chunk<MT, 40>(R, F, h, b, acc);
+      layer_chunk<MT, 44>(R, F, h, b, acc);
+      layer_chunk<MT, 48>(R, F, h, b, acc);
+      layer_chunk<MT, 52>(R, F, h, b, acc);
+      layer_chunk<MT, 56>(R, F, h, b, acc);
+      layer_chunk<MT, 60>(R, F, h, b, acc);
 #pragma unroll
       for (int nt = 0; nt < kNT; ++nt) {
         const f4 bias = ldf4(S.bl + l * kH + 16 * nt + g4);
@@ -127,8 +196,8 @@ struct CoreF32 {
       f4 P[MT], Q[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) P[mt] = Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
-      readout_chunk<MT, 0>(R, h, P, Q);
-      readout_chunk<MT, 1>(R, h, P, Q);
+      readout_chunk<MT, 0>(R, F, h, P, Q);
+      readout_chunk<MT, 1>(R, F, h, P, Q);
       readout_epilogue<MT>(P, Q, ldf4(S.be + 16 * ot + g4), ldf4(S.w2 + 16 * ot + g4), pf, pb);
     }
     readout_finish<MT>(pf, pb, W.b2, ffwd, fbwd);

@@ -73,6 +73,8 @@ struct CoreK32 {
   struct Frag {
     T v[kNS];
   };
+  struct Feed {};  // fragments are read per chunk (no register prefetch)
+  static __device__ __forceinline__ void begin(R_t &, Feed &) {}
 
   static __device__ __forceinline__ Frag lds_frag(const float *slot, int j, int lane) {
     Frag f;
@@ -168,7 +170,7 @@ struct CoreK32 {
   }
 
   template <int MT>
-  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, float *park,
+  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &, float *park,
                                              const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
     const int lane = R.lane;
     const int g4 = 4 * (lane >> 4);

@@ -9,6 +9,8 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_void_p
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libhybridflux.so")
+# Diagnostic builds only (tools/diag_*.py): load another build of the same ABI.
+LIB_PATH = os.environ.get("HYBRIDFLUX_LIB", LIB_PATH)
 
 HF_OK = 0
 HF_EINVAL = -1

@@ -1,0 +1,92 @@
+"""Where the f32 rollout kernel's time goes (diagnostic, not a bench line).
+
+Times, on cfg3 shapes (4096 ICs x 64 cells, 50 steps):
+  * the headline rollout (trajectory + metrics) and a bare rollout (no outputs);
+  * hf_chain_flux (GNN only, no FV/Poisson) called once per step;
+  * bare rollouts of FluxGNN(4,128,L) for L = 0,1,2,4: the per-layer slope is
+    the message-passing loop's cost, the intercept input layer + readout + FV.
+Every figure is kernel time from HIP events on the launch stream.
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gnn-plasma-flux_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from hybridflux import engine  # noqa: E402
+
+FLOP_LAYER = 65_536          # per cell-step, one update layer
+FLOP_FIXED = 1_024 + 66_048  # input MLP + P/Q readout
+
+
+def rand_sd(layers, seed=0):
+    g = np.random.default_rng(seed)
+    sd = {"input_mlp.0.weight": g.normal(0, 0.5, (128, 4)), "input_mlp.0.bias": g.normal(0, 0.1, 128)}
+    for l in range(layers):
+        sd[f"update_mlps.{l}.0.weight"] = g.normal(0, 1 / 16, (128, 256))
+        sd[f"update_mlps.{l}.0.bias"] = g.normal(0, 0.1, 128)
+    sd["edge_mlp.0.weight"] = g.normal(0, 1 / 16, (128, 256))
+    sd["edge_mlp.0.bias"] = g.normal(0, 0.1, 128)
+    sd["edge_mlp.2.weight"] = g.normal(0, 1 / 11, (1, 128))
+    sd["edge_mlp.2.bias"] = g.normal(0, 0.1, 1)
+    return {k: np.asarray(v, np.float32) for k, v in sd.items()}
+
+
+def timed(fn, reps=3):
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        fn()
+        b.record(s)
+        torch.cuda.synchronize()
+        best = min(best, a.elapsed_time(b))
+    return best
+
+
+def main():
+    B, nx, T = int(os.environ.get("DIAG_B", 4096)), 64, 50
+    prec = os.environ.get("DIAG_PREC", "f32")
+    dev = torch.device("cuda", 0)
+    grid = engine.Grid(nx)
+    g = np.random.default_rng(1)
+    st = np.empty((B, 3, nx), np.float32)
+    xx = np.arange(nx) * 2 * np.pi / nx
+    for i in range(B):
+        st[i, 0] = 1 + 0.2 * np.sin(xx + g.uniform(0, 6))
+        st[i, 1] = 0.1 * np.cos(xx + g.uniform(0, 6))
+        st[i, 2] = 0.05 * np.sin(xx)
+    s0 = torch.as_tensor(st, device=dev)
+    out = {}
+    m4 = engine.DeviceModel(rand_sd(4), dev, prec)
+    tr = torch.empty(B, T + 1, 3, nx, device=dev)
+    me = torch.empty(B, T + 1, 4, device=dev)
+    fin = torch.empty_like(s0)
+    out["headline_ms"] = timed(lambda: engine.run(m4, grid, s0, T, traj=tr, metrics=me, out=fin))
+    out["bare_ms"] = timed(lambda: engine.run(m4, grid, s0, T, traj=False, metrics=False, out=fin))
+    nf = torch.randn(B * nx, 4, device=dev)
+    out["flux_only_x50_ms"] = timed(lambda: [engine.chain_flux(m4, nf, B, nx) for _ in range(T)])
+    per_l = {}
+    for L in (0, 1, 2, 4):
+        m = engine.DeviceModel(rand_sd(L), dev, prec)
+        per_l[L] = timed(lambda: engine.run(m, grid, s0, T, traj=False, metrics=False, out=fin))
+    out["bare_ms_by_layers"] = per_l
+    slope = (per_l[4] - per_l[0]) / 4
+    cells = B * nx * T
+    out["layer_ms"] = slope
+    out["layer_frac_of_f32_peak"] = FLOP_LAYER * cells / (slope * 1e-3) / 157.3e12
+    out["fixed_ms"] = per_l[0]
+    out["fixed_frac_of_f32_peak"] = FLOP_FIXED * cells / (per_l[0] * 1e-3) / 157.3e12
+    out["precision"] = prec
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
