@@ -188,19 +188,41 @@ struct CoreF32 {
       }
     }
 
-    // edge readout, P/Q split (src/flux_gnn.py:62-66)
-    float pf[MT], pb[MT];
+    // edge readout, P/Q split (src/flux_gnn.py:62-66).  The 128-feature dot
+    // w2 . ReLU(z) is summed as four partial dots over tile pairs (2w, 2w+1),
+    // then added in w order: the order of chain_split.hip, so both rollout
+    // kernels give bit-identical results and a batch is invariant to which
+    // of them its size selects.
+    float sf[MT], sb[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
-    for (int ot = 0; ot < kNT; ++ot) {
-      f4 P[MT], Q[MT];
+    for (int mt = 0; mt < MT; ++mt) sf[mt] = sb[mt] = 0.f;
+    for (int w = 0; w < kNT / 2; ++w) {
+      float pf[MT], pb[MT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) P[mt] = Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
-      readout_chunk<MT, 0>(R, F, h, P, Q);
-      readout_chunk<MT, 1>(R, F, h, P, Q);
-      readout_epilogue<MT>(P, Q, ldf4(S.be + 16 * ot + g4), ldf4(S.w2 + 16 * ot + g4), pf, pb);
+      for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ot = 2 * w + t;
+        f4 P[MT], Q[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) P[mt] = Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
+        readout_chunk<MT, 0>(R, F, h, P, Q);
+        readout_chunk<MT, 1>(R, F, h, P, Q);
+        readout_epilogue<MT>(P, Q, ldf4(S.be + 16 * ot + g4), ldf4(S.w2 + 16 * ot + g4), pf, pb);
+      }
+      float ff[MT], fb[MT];
+      readout_finish<MT>(pf, pb, 0.f, ff, fb);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        sf[mt] = __fadd_rn(sf[mt], ff[mt]);
+        sb[mt] = __fadd_rn(sb[mt], fb[mt]);
+      }
     }
-    readout_finish<MT>(pf, pb, W.b2, ffwd, fbwd);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      ffwd[mt] = __fadd_rn(sf[mt], W.b2);
+      fbwd[mt] = __fadd_rn(sb[mt], W.b2);
+    }
   }
 };
 
@@ -214,6 +236,9 @@ hipError_t launch_chain_flux_f32(const ChainW &w, const float *nf, const float *
 hipError_t launch_chain_rollout_f32(const ChainW &w, const float *state0, float *state_final, const float *x,
                                     const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                     float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
+  // small batches: one IC per workgroup, output features split over its waves
+  if (ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_split(w, B))
+    return launch_chain_rollout_split(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, s);
   return chain::launch_rollout_core<CoreF32>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj,
                                              metrics, ex, s);
 }

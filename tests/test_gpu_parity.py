@@ -281,6 +281,11 @@ def test_full_batch_properties(hf):
     sub = [0, 1, 777, 2048, 4095]
     alone = solver.run_batch(ics[sub], 30, traj=False)["final"]
     assert torch.equal(alone, a["final"][sub])                       # batch invariant
+    # BASELINE config 2 size: 256 ICs take the feature-split kernel
+    # (chain_split.hip), 4096 the IC-per-wave kernel; results are bit-identical
+    cfg2 = solver.run_batch(ics[:256], 30, traj=False, metrics=True)
+    assert torch.equal(cfg2["final"], a["final"][:256])
+    assert torch.equal(cfg2["metrics"], a["metrics"][:256])
     m = a["metrics"].cpu().numpy()
     assert (m[..., 2] == 1).all()
     drift = np.abs(m[:, -1, 1] - m[:, 0, 1]).max()                   # FV telescopes: mean(n) conserved
