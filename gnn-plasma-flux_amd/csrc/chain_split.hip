@@ -33,13 +33,21 @@ constexpr int kSplitDepth = 4;  // units in flight per wave
 
 // Private fragment stream of one wave: units [0, total) of float4 per lane,
 // consumed cyclically (one pass per GNN forward).
+// Buffer loads with the unit offset in an SGPR and the lane offset in a fixed
+// VGPR: no per-load VALU address arithmetic beside the f32 MFMAs.
 struct SplitFeed {
-  const f4 *base;  // this wave's stream, lane offset applied
-  int total;       // units per pass
-  int next;        // unit index of the next load
+  __amdgpu_buffer_rsrc_t rsrc;  // this wave's stream
+  int lane_off;                 // lane * 16 bytes
+  int total;                    // units per pass
+  int next;                     // unit index of the next load
   f4 buf[kSplitDepth];
+  __device__ __forceinline__ void init(const void *wave_base, int units, int lane) {
+    total = units;
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(wave_base), 0, units * 1024, 0x00020000);
+    lane_off = lane * 16;
+  }
   __device__ __forceinline__ void load(int slot) {
-    buf[slot] = base[(int64_t)next * 64];
+    buf[slot] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off, next * 1024, 0));
     next = next + 1 == total ? 0 : next + 1;
   }
   __device__ __forceinline__ void prime() {
@@ -69,42 +77,45 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// B operand of flat update-layer k-step KS: h itself (KS < 32) or the
-// neighbour sum h[i+1] + h[i-1] (1/deg folded into the packed W_b).
-template <int MT, int KS>
-__device__ __forceinline__ void split_b(const f4 (&h)[MT][kNT], float (&b)[MT]) {
-  constexpr int s = KS % kKS;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) b[mt] = h[mt][s >> 2][s & 3];
-  if constexpr (KS >= kKS) {
-    float sum[MT];
-    nb_sum<MT>(b, sum);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) b[mt] = sum[mt];
-  }
-}
-
-// Two k-steps (unit U of the layer) for the wave's two output tiles.
+// Two k-steps (unit U of the layer) for the wave's two output tiles.  k-steps
+// 0..31 multiply h, 32..63 the neighbour sum h[i+1] + h[i-1] (1/deg folded
+// into the packed W_b).  The sums are formed in place, one 16-value burst per
+// feature tile right after the last k-step that needs that tile of h.
+// (Exchanging each wave's own sums through LDS instead, 32 VALU per layer
+// rather than 128, measured slower overall: the extra LDS traffic, barrier
+// and registers outweigh the VALU saved.)
 template <int MT, int U>
-__device__ __forceinline__ void split_layer_unit(SplitFeed &F, const f4 (&h)[MT][kNT], f4 (&acc)[MT][2]) {
+__device__ __forceinline__ void split_layer_unit(SplitFeed &F, f4 (&h)[MT][kNT], f4 (&acc)[MT][2]) {
   const f4 a = F.take<U>();
-  float b0[MT], b1[MT];
-  split_b<MT, 2 * U>(h, b0);
-  split_b<MT, 2 * U + 1>(h, b1);
+  constexpr int s0 = (2 * U) % kKS, s1 = (2 * U + 1) % kKS;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    acc[mt][0] = mfma4(a[0], b0[mt], acc[mt][0]);
-    acc[mt][1] = mfma4(a[1], b0[mt], acc[mt][1]);
+    acc[mt][0] = mfma4(a[0], h[mt][s0 >> 2][s0 & 3], acc[mt][0]);
+    acc[mt][1] = mfma4(a[1], h[mt][s0 >> 2][s0 & 3], acc[mt][1]);
   }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    acc[mt][0] = mfma4(a[2], b1[mt], acc[mt][0]);
-    acc[mt][1] = mfma4(a[3], b1[mt], acc[mt][1]);
+    acc[mt][0] = mfma4(a[2], h[mt][s1 >> 2][s1 & 3], acc[mt][0]);
+    acc[mt][1] = mfma4(a[3], h[mt][s1 >> 2][s1 & 3], acc[mt][1]);
   }
+#ifndef HF_DIAG_NONB  // timing diagnostic only: results are wrong
+  if constexpr (2 * U + 1 < kKS && (s1 & 3) == 3) {  // tile s1/4 of h consumed: h <- neighbour sums
+    constexpr int nt = s1 >> 2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v[MT], sum[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) v[mt] = h[mt][nt][r];
+      nb_sum<MT>(v, sum);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) h[mt][nt][r] = sum[mt];
+    }
+  }
+#endif
 }
 
 template <int MT, int... U>
-__device__ __forceinline__ void split_layer(SplitFeed &F, const f4 (&h)[MT][kNT], f4 (&acc)[MT][2],
+__device__ __forceinline__ void split_layer(SplitFeed &F, f4 (&h)[MT][kNT], f4 (&acc)[MT][2],
                                             std::integer_sequence<int, U...>) {
   (split_layer_unit<MT, U>(F, h, acc), ...);
 }
@@ -144,7 +155,8 @@ __device__ __forceinline__ void split_gnn(const ChainW &W, const Small &S, Split
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt][0] = acc[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
     split_layer<MT>(F, h, acc, std::make_integer_sequence<int, kKS>{});
-    // a wave may write layer l+1's tiles while a slower one still reads layer l's
+    // double-buffered by layer parity: a wave may write layer l+1's tiles
+    // while a slower one still reads layer l's
     f4 *hx4 = reinterpret_cast<f4 *>(hx) + (l & 1) * (kNT * 4 * 64);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -223,8 +235,8 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_split_kernel(
     }
   }
   SplitFeed F;
-  F.total = (W.layers + 1) * kKS;
-  F.base = reinterpret_cast<const f4 *>(W.split) + (int64_t)wave * F.total * 64 + lane;
+  const int units = (W.layers + 1) * kKS;
+  F.init(reinterpret_cast<const char *>(W.split) + (int64_t)wave * units * 1024, units, lane);
   F.prime();
   __syncthreads();
   float *tj = traj ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;

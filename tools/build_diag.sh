@@ -1,9 +1,10 @@
 #!/bin/bash
 # Timing-diagnostic builds of libhybridflux (wrong results by construction; never used by tests or bench):
-#   nobar: no s_barrier in the weight ring; nonb: no neighbour sums; nods: no fragment ds_reads.
+#   nobar: no s_barrier in the weight ring; nonb: no neighbour sums; nods: no fragment ds_reads;
+#   DIAG_VARIANTS="nonb nods" selects a subset.
 set -e
 cd "$(dirname "$0")/../gnn-plasma-flux_amd/csrc"
-for v in nobar nonb nods; do
+for v in ${DIAG_VARIANTS:-nobar nonb nods}; do
   D=$(echo $v | tr a-z A-Z)
   make -s -j8 OUT=../../build/diag/lib_$v.so BUILD=../../build/diag/$v "CXXFLAGS_EXTRA=-DHF_DIAG_$D" >/dev/null
 done
