@@ -54,6 +54,35 @@ def cpu_baseline(weights, nx, T, n_ics, threads):
     return alpha, beta
 
 
+def other_config(weights, dev, name, B, nx, precision, K, W):
+    """Time one more BASELINE.json single-GPU config the same way as the
+    headline (preallocated outputs, HIP events on the launch stream, wall
+    clock around the launches).  Reported next to the headline, never as it."""
+    from hybridflux import HybridSolver
+    dt = 5e-3 * 64.0 / nx
+    solver = HybridSolver(weights, radius=2, nx=nx, dt=dt, device=dev, precision=precision)
+    ics = solver.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True)
+    solver.run_batch(ics, max(W, 1), traj=False)
+    final = torch.empty_like(ics)
+    met = torch.empty(B, K + 1, 4, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    solver.run_batch(ics, K, traj=False, metrics=met, out=final)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kms = e0.elapsed_time(e1)
+    flop = GNN_FLOP_PER_CELL_STEP * B * nx * K
+    peak = PEAK_F32_MFMA_TFLOPS if precision == "f32" else PEAK_F16_MFMA_TFLOPS
+    return {"workload": name, "ics": B, "nx": nx, "dt": dt, "precision": precision, "steps": K,
+            "value": round(B * K / wall, 1), "unit": "IC-steps/s", "ms_per_step": round(wall / K * 1e3, 4),
+            "kernel_ms": round(kms, 3), "mfma_frac": round(flop / (kms * 1e-3) / 1e12 / peak, 4),
+            "finite_fraction": float(met[:, -1, 2].float().mean().item())}
+
+
 def pmc_traffic(K, B, nx, traj):
     """HBM bytes per launch from the committed PMC passes of this same bench
     command (tools/gpu_pmc.sh + tools/pmc_traffic.py), if they match."""
@@ -88,6 +117,9 @@ def main():
                     help="chain-kernel arithmetic of the headline line (f32 = exact float32 MFMA)")
     ap.add_argument("--also", default="f16x3",
                     help="comma list of other precisions to time in the same process (reported under 'alt'); '' = none")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the other single-GPU BASELINE configs (cfg2: 256 ICs f32; cfg4: 4096 ICs x 1024 "
+                         "cells bf16), reported under 'other_configs' at N=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -161,6 +193,12 @@ def main():
                      "max_abs_diff_vs_headline_final_state": dev_err}
         del s2, r2
 
+    others = None
+    if world == 1 and not args.no_other_configs:
+        others = [other_config(weights, dev, "cfg2: 64-cell chain, 256-IC batch, f32", 256, 64, "f32", K, W),
+                  other_config(weights, dev, "cfg4: 1024-cell chain, 4096-IC batch, bf16 MLP weights, dt=3.125e-4",
+                               4096, 1024, "bf16", 30, 3)]
+
     t_max = torch.tensor([wall], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -213,6 +251,7 @@ def main():
             "cpu_baseline": cpu,
             "finite_fraction": finite,
             "alt": alt or None,
+            "other_configs": others,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
