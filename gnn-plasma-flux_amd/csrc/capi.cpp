@@ -144,10 +144,12 @@ void pack_chain(const float *p, int L, int prec, ChainPack &P) {
   } else {
     const int terms = prec == hf::kPrecF16x3 ? 2 : 1;
     // one 16-byte fragment (8 values) of row `row`, k-block kb, column offset kbase
-    auto frag = [&](const float *W, int64_t ld, int row, int kbase, int kb, int lane, int term) {
+    auto frag = [&](const float *W, int64_t ld, int row, int kbase, int kb, int lane, int term, bool halve_b) {
       for (int e = 0; e < 8; ++e) {
         const int k = kbase + 16 * (2 * kb + (e >> 2)) + 4 * (lane >> 4) + (e & 3);
-        const float w = W[(int64_t)row * ld + k];
+        // bf16: the 1/deg = 1/2 of the mean aggregation is folded into W_b
+        // (CoreK32A, input-side aggregation); exact, bf16(w/2) == bf16(w)/2
+        const float w = W[(int64_t)row * ld + k] * (halve_b && kbase == kH ? 0.5f : 1.0f);
         if (prec == hf::kPrecBF16) {
           put(out, to_bf16(w));
         } else {
@@ -164,14 +166,14 @@ void pack_chain(const float *p, int L, int prec, ChainPack &P) {
             for (int t = 0; t < terms; ++t)
               for (int lane = 0; lane < 64; ++lane) {
                 const int nt = 4 * nth + (j >> 1), ab = j & 1;
-                frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, t);
+                frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, t, prec == hf::kPrecBF16);
               }
     for (int ot = 0; ot < kNT; ++ot)
       for (int j = 0; j < 8; ++j)
         for (int t = 0; t < terms; ++t)
           for (int lane = 0; lane < 64; ++lane) {
             const int kb = j >> 1, pq = j & 1;
-            frag(p + lay.w_e, 2 * kH, 16 * ot + (lane & 15), pq * kH, kb, lane, t);
+            frag(p + lay.w_e, 2 * kH, 16 * ot + (lane & 15), pq * kH, kb, lane, t, false);
           }
   }
   std::vector<float> &sm = P.small;

@@ -89,7 +89,12 @@ __device__ __forceinline__ void nb_sum(const float (&v)[MT], float (&s)[MT]) {
   left_nb<MT>(v, l);
   right_nb<MT>(v, r);
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) s[mt] = __fadd_rn(l[mt], r[mt]);
+  for (int mt = 0; mt < MT; ++mt) {
+    // the rotated (DPP) operand first: hipcc folds a row_ror mov into the add
+    // only as src0, and does not commute to get it there
+    if (mt == MT - 1 && MT > 1) s[mt] = __fadd_rn(r[mt], l[mt]);
+    else s[mt] = __fadd_rn(l[mt], r[mt]);
+  }
 }
 
 __device__ __forceinline__ f4 relu4(f4 v) { return f4{relu(v.x), relu(v.y), relu(v.z), relu(v.w)}; }
