@@ -38,11 +38,44 @@ __device__ __forceinline__ void block_metrics(MetricAcc &m, float *dst, int nx) 
   }
 }
 
-// LDS: c[nx] (double) | u, F, rho, E (float) | FFT buffers 2 x nx double2 (FFT nx only)
+// LDS, circulant nx: c[nx] (double) | u, F, rho, E (float).
+// LDS, FFT nx: u, F (float) | FFT buffers 2 x nx double2 | twiddles nx/2 double2
+// (48 KiB at nx = 1024: three workgroups per CU).
+__host__ __device__ inline size_t fv_fft_offset(int nx) { return ((size_t)nx * 2 * sizeof(float) + 15) & ~size_t(15); }
 inline size_t fv_lds_bytes(int nx) {
-  size_t b = (size_t)nx * (sizeof(double) + 4 * sizeof(float));
-  if (poisson_uses_fft(nx)) b = ((b + 15) & ~size_t(15)) + 2 * sizeof(double2) * nx;
-  return b;
+  return poisson_uses_fft(nx) ? fv_fft_offset(nx) + (2 * (size_t)nx + nx / 2) * sizeof(double2)
+                              : (size_t)nx * (sizeof(double) + 4 * sizeof(float));
+}
+
+// Carve of the dynamic LDS (see fv_lds_bytes).
+struct FvLds {
+  double *c;
+  float *u, *F, *rho, *E;
+  double2 *fa, *fb, *tw;
+  __device__ FvLds(double *s_dyn, int nx) {
+    if (poisson_uses_fft(nx)) {
+      c = nullptr;
+      u = reinterpret_cast<float *>(s_dyn);
+      F = u + nx;
+      rho = E = nullptr;
+      fa = reinterpret_cast<double2 *>(reinterpret_cast<char *>(s_dyn) + fv_fft_offset(nx));
+      fb = fa + nx;
+      tw = fb + nx;
+    } else {
+      c = s_dyn;
+      u = reinterpret_cast<float *>(c + nx);
+      F = u + nx;
+      rho = F + nx;
+      E = rho + nx;
+      fa = fb = tw = nullptr;
+    }
+  }
+};
+
+// Stage the plan's twiddles (after the circulant column c[nx]) into LDS.
+__device__ __forceinline__ void stage_twiddles(const double *pc, double2 *s_tw, int nx) {
+  const double2 *tw = reinterpret_cast<const double2 *>(pc + nx);
+  for (int q = threadIdx.x; q < nx / 2; q += blockDim.x) s_tw[q] = tw[q];
 }
 
 template <bool HYBRID>
@@ -52,43 +85,41 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     float nu, float dx2, float *__restrict__ flux_out, int64_t ld_flux, float *__restrict__ metrics,
     int64_t ld_metrics) {
   extern __shared__ double s_dyn[];
-  double *s_c = s_dyn;
-  float *s_u = reinterpret_cast<float *>(s_c + nx);
-  float *s_F = s_u + nx;
-  float *s_rho = s_F + nx;
-  float *s_E = s_rho + nx;
+  const FvLds L(s_dyn, nx);
   const bool fft = poisson_uses_fft(nx);
-  double2 *fa = reinterpret_cast<double2 *>(reinterpret_cast<char *>(s_dyn) +
-                                            (((size_t)nx * (sizeof(double) + 4 * sizeof(float)) + 15) & ~size_t(15)));
   const int64_t b = blockIdx.x;
   const float *st = in + b * ld_in;
   float *so = out + b * ld_out;
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
     const float u = st[nx + i];
-    s_u[i] = u;
-    s_F[i] = HYBRID ? face_flux[b * nx + i] : __fmul_rn(st[i], u);  // F_n = n*u (:70-71)
-    if (!fft) s_c[i] = pc[i];
+    L.u[i] = u;
+    L.F[i] = HYBRID ? face_flux[b * nx + i] : __fmul_rn(st[i], u);  // F_n = n*u (:70-71)
+    if (!fft) L.c[i] = pc[i];
   }
+  if (fft) stage_twiddles(pc, L.tw, nx);
   __syncthreads();
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
     const int im = i == 0 ? nx - 1 : i - 1;
     const int ip = i == nx - 1 ? 0 : i + 1;
-    const float F = s_F[i];
-    const float n_new = continuity(st[i], F, s_F[im], c);
+    const float F = L.F[i];
+    const float n_new = continuity(st[i], F, L.F[im], c);
     const float E = st[2 * nx + i];
-    const float u_new = HYBRID ? velocity_hybrid(s_u[i], s_u[im], E, c, dt)
-                               : velocity_classical(s_u[i], s_u[im], s_u[ip], E, c, dt, nu, dx2);
-    s_rho[i] = __fsub_rn(n_new, 1.0f);
+    const float u_new = HYBRID ? velocity_hybrid(L.u[i], L.u[im], E, c, dt)
+                               : velocity_classical(L.u[i], L.u[im], L.u[ip], E, c, dt, nu, dx2);
+    const float rho = __fsub_rn(n_new, 1.0f);
+    if (fft) L.fa[i] = make_double2((double)rho, 0.0);
+    else L.rho[i] = rho;
     so[i] = n_new;
     so[nx + i] = u_new;
     if (flux_out) flux_out[b * ld_flux + i] = F;
   }
-  __syncthreads();
-  if (fft) poisson_fft(s_rho, fa, fa + nx, pc, nx, s_E);
+  const double2 *X = nullptr;
+  if (fft) X = poisson_fft(L.fa, L.fb, L.tw, pc + 2 * nx, nx);
+  else __syncthreads();
   MetricAcc m;
   m.init();
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-    const float E_new = fft ? s_E[i] : poisson_cell(s_rho, s_c, i, nx);
+    const float E_new = fft ? (float)(X[i].x / nx) : poisson_cell(L.rho, L.c, i, nx);
     so[2 * nx + i] = E_new;
     if (metrics) m.add(so[i], so[nx + i], E_new);
   }
@@ -112,22 +143,27 @@ __global__ __launch_bounds__(kFvThreads) void poisson_kernel(const float *__rest
                                                              const double *__restrict__ pc,
                                                              int nx) {
   extern __shared__ double s_dyn[];
-  double *s_c = s_dyn;
-  float *s_u = reinterpret_cast<float *>(s_c + nx);  // unused: keeps the fv LDS layout
-  float *s_rho = s_u + 2 * nx;
-  float *s_E = s_rho + nx;
+  const FvLds L(s_dyn, nx);
   const bool fft = poisson_uses_fft(nx);
-  double2 *fa = reinterpret_cast<double2 *>(reinterpret_cast<char *>(s_dyn) +
-                                            (((size_t)nx * (sizeof(double) + 4 * sizeof(float)) + 15) & ~size_t(15)));
   const int64_t b = blockIdx.x;
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-    if (!fft) s_c[i] = pc[i];
-    s_rho[i] = __fsub_rn(n[b * ld_n + i], 1.0f);  // rho = n - n0 (:60)
+    const float rho = __fsub_rn(n[b * ld_n + i], 1.0f);  // rho = n - n0 (:60)
+    if (fft) {
+      L.fa[i] = make_double2((double)rho, 0.0);
+    } else {
+      L.c[i] = pc[i];
+      L.rho[i] = rho;
+    }
   }
-  __syncthreads();
-  if (fft) poisson_fft(s_rho, fa, fa + nx, pc, nx, s_E);
+  const double2 *X = nullptr;
+  if (fft) {
+    stage_twiddles(pc, L.tw, nx);
+    X = poisson_fft(L.fa, L.fb, L.tw, pc + 2 * nx, nx);
+  } else {
+    __syncthreads();
+  }
   for (int i = threadIdx.x; i < nx; i += kFvThreads)
-    E[b * ld_E + i] = fft ? s_E[i] : poisson_cell(s_rho, s_c, i, nx);
+    E[b * ld_E + i] = fft ? (float)(X[i].x / nx) : poisson_cell(L.rho, L.c, i, nx);
 }
 
 // Per-step channel MSE of two trajectories (scripts/evaluation/evaluate_multi_ic.py:88-90).

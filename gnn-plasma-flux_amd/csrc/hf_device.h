@@ -71,20 +71,52 @@ __device__ __forceinline__ float poisson_cell(const float *s_rho, const double *
 // with a float64 Stockham radix-2 FFT in LDS instead of the O(nx^2) circulant.
 // The plan buffer (hf_poisson_coeffs) then holds, after the circulant column
 // c[nx]: twiddles exp(-2 pi i m / nx) for m < nx/2 as (re, im), and 1/k_q (0 at q = 0).
-// In-place-style block FFT: returns the buffer holding the result (a or b).
+__device__ __forceinline__ double2 cmul(double2 a, double2 w) {
+  return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+// exp(-+2 pi i m / n) for 0 <= m < n from the half table tw[m < n/2]
+__device__ __forceinline__ double2 twiddle(const double2 *__restrict__ tw, int m, int n, bool inverse) {
+  double2 w = m < n / 2 ? tw[m] : make_double2(-tw[m - n / 2].x, -tw[m - n / 2].y);
+  if (inverse) w.y = -w.y;
+  return w;
+}
+
+// Block FFT, Stockham autosort: radix-4 passes (one radix-2 pass first when
+// log2 n is odd), one barrier per pass.  Returns the buffer holding the
+// result (a or b).  tests/test_abi_cpu.py::_stockham models the same passes.
 __device__ __forceinline__ double2 *fft_block(double2 *a, double2 *b, const double2 *__restrict__ tw, int n,
                                               bool inverse) {
-  for (int ns = 1; ns < n; ns <<= 1) {
+  int ns = 1;
+  if ((__builtin_ctz(n) & 1) != 0) {  // radix-2 pass, ns = 1: twiddle 1
     __syncthreads();
     for (int jj = threadIdx.x; jj < n / 2; jj += blockDim.x) {
       const double2 a0 = a[jj], a1 = a[jj + n / 2];
+      b[2 * jj] = make_double2(a0.x + a1.x, a0.y + a1.y);
+      b[2 * jj + 1] = make_double2(a0.x - a1.x, a0.y - a1.y);
+    }
+    double2 *s = a;
+    a = b;
+    b = s;
+    ns = 2;
+  }
+  for (; ns < n; ns <<= 2) {
+    __syncthreads();
+    for (int jj = threadIdx.x; jj < n / 4; jj += blockDim.x) {
       const int k = jj & (ns - 1);
-      double2 w = tw[k * (n / (2 * ns))];
-      if (inverse) w.y = -w.y;
-      const double2 t = make_double2(a1.x * w.x - a1.y * w.y, a1.x * w.y + a1.y * w.x);
-      const int d = ((jj - k) << 1) + k;
-      b[d] = make_double2(a0.x + t.x, a0.y + t.y);
-      b[d + ns] = make_double2(a0.x - t.x, a0.y - t.y);
+      const int m = k * (n / (4 * ns));
+      const double2 a0 = a[jj];
+      const double2 a1 = cmul(a[jj + n / 4], twiddle(tw, m, n, inverse));
+      const double2 a2 = cmul(a[jj + n / 2], twiddle(tw, 2 * m, n, inverse));
+      const double2 a3 = cmul(a[jj + 3 * n / 4], twiddle(tw, 3 * m, n, inverse));
+      const double2 b0 = make_double2(a0.x + a2.x, a0.y + a2.y), b1 = make_double2(a0.x - a2.x, a0.y - a2.y);
+      const double2 b2 = make_double2(a1.x + a3.x, a1.y + a3.y);
+      const double2 t = make_double2(a1.x - a3.x, a1.y - a3.y);
+      const double2 b3 = inverse ? make_double2(-t.y, t.x) : make_double2(t.y, -t.x);  // (a1 - a3) * (+-i)
+      const int d = (jj - k) * 4 + k;
+      b[d] = make_double2(b0.x + b2.x, b0.y + b2.y);
+      b[d + ns] = make_double2(b1.x + b3.x, b1.y + b3.y);
+      b[d + 2 * ns] = make_double2(b0.x - b2.x, b0.y - b2.y);
+      b[d + 3 * ns] = make_double2(b1.x - b3.x, b1.y - b3.y);
     }
     double2 *s = a;
     a = b;
@@ -94,21 +126,19 @@ __device__ __forceinline__ double2 *fft_block(double2 *a, double2 *b, const doub
   return a;
 }
 
-// E[q] for the whole IC (block-wide): rho (LDS floats) -> out (LDS floats).
-__device__ __forceinline__ void poisson_fft(const float *s_rho, double2 *a, double2 *b, const double *plan, int nx,
-                                           float *out) {
-  const double2 *tw = reinterpret_cast<const double2 *>(plan + nx);
-  const double *inv_k = plan + 2 * nx;
-  for (int q = threadIdx.x; q < nx; q += blockDim.x) a[q] = make_double2((double)s_rho[q], 0.0);
-  double2 *X = fft_block(a, b, tw, nx, false);
+// Spectral Poisson for the whole IC (block-wide).  On entry a[q] = (rho_q, 0),
+// written before the call by any thread (fft_block opens with a barrier);
+// s_tw holds the plan's twiddles (staged in LDS).  Returns the buffer X with
+// E_q = X[q].x / nx (the caller rounds to float32).
+__device__ __forceinline__ double2 *poisson_fft(double2 *a, double2 *b, const double2 *s_tw, const double *inv_k,
+                                               int nx) {
+  double2 *X = fft_block(a, b, s_tw, nx, false);
   double2 *Y = X == a ? b : a;
   for (int q = threadIdx.x; q < nx; q += blockDim.x) {
     const double ik = inv_k[q];                       // 1j * X / k, k = 0 mode zeroed
     X[q] = make_double2(-X[q].y * ik, X[q].x * ik);
   }
-  X = fft_block(X, Y, tw, nx, true);
-  for (int q = threadIdx.x; q < nx; q += blockDim.x) out[q] = (float)(X[q].x / nx);
-  __syncthreads();
+  return fft_block(X, Y, s_tw, nx, true);
 }
 
 // Per-state rollout metrics, partial sums for one cell.

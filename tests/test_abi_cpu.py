@@ -61,19 +61,31 @@ def test_poisson_coefficients_reproduce_spectral_solve(nx):
 
 
 def _stockham(x, tw, inverse):
-    """The radix-2 Stockham passes of fv_poisson.hip fft_block, in numpy."""
+    """The Stockham passes of hf_device.h fft_block, in numpy: one radix-2 pass
+    when log2 n is odd, then radix-4 passes."""
     n = x.size
     w_all = np.conj(tw) if inverse else tw
+
+    def w(m):  # exp(-+2 pi i m / n) for m < n from the half table
+        hi = m >= n // 2
+        v = w_all[np.where(hi, m - n // 2, m)]
+        return np.where(hi, -v, v)
+
     ns = 1
-    j = np.arange(n // 2)
-    while ns < n:
-        a0, a1 = x[: n // 2], x[n // 2:]
-        k = j & (ns - 1)
-        t = a1 * w_all[k * (n // (2 * ns))]
-        d = ((j - k) << 1) + k
+    if (n.bit_length() - 1) % 2 == 1:
         y = np.empty_like(x)
-        y[d], y[d + ns] = a0 + t, a0 - t
-        x, ns = y, ns * 2
+        y[0::2], y[1::2] = x[: n // 2] + x[n // 2:], x[: n // 2] - x[n // 2:]
+        x, ns = y, 2
+    j = np.arange(n // 4)
+    while ns < n:
+        k = j & (ns - 1)
+        m = k * (n // (4 * ns))
+        a0, a1, a2, a3 = x[j], x[j + n // 4] * w(m), x[j + n // 2] * w(2 * m), x[j + 3 * n // 4] * w(3 * m)
+        b0, b1, b2, b3 = a0 + a2, a0 - a2, a1 + a3, (a1 - a3) * (1j if inverse else -1j)
+        d = (j - k) * 4 + k
+        y = np.empty_like(x)
+        y[d], y[d + ns], y[d + 2 * ns], y[d + 3 * ns] = b0 + b2, b1 + b3, b0 - b2, b1 - b3
+        x, ns = y, ns * 4
     return x
 
 
