@@ -86,17 +86,17 @@ struct CoreK32 {
     return f;
   }
 
-  // k-block kb of activation tiles (2kb, 2kb+1) as a split B fragment.
+  // Activation tiles (2kb, 2kb+1) as the split B fragment of k-block kb.
+  static __device__ __forceinline__ void frag_of(const f4 &a, const f4 &b, Frag &o) {
+    const f8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    M::split(v, o.v);
+  }
   template <int MT>
   static __device__ __forceinline__ void to_frags(const f4 (&h)[MT][kNT], Frag (&B)[MT][kKB]) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int kb = 0; kb < kKB; ++kb) {
-        const f4 a = h[mt][2 * kb], b = h[mt][2 * kb + 1];
-        const f8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        M::split(v, B[mt][kb].v);
-      }
+      for (int kb = 0; kb < kKB; ++kb) frag_of(h[mt][2 * kb], h[mt][2 * kb + 1], B[mt][kb]);
   }
 
   // Update-layer chunk (NTH, KB): W_a and W_b fragments of output tiles
@@ -193,21 +193,25 @@ struct CoreK32 {
 #pragma unroll
           for (int n = 0; n < 4; ++n) *reinterpret_cast<f4 *>(park + ((mt * 4 + n) * 64 + lane) * 4) = lo[mt][n];
       }
-      f4 h[MT][kNT];
       {
         f4 hi[MT][4];
         layer_half<MT, 1>(R, B, bias, g4, hi);
+        // new B fragments one k-block at a time (the old ones are dead now):
+        // k-blocks 2, 3 from registers, then 0, 1 from the park, so f32
+        // activations and fragments are never all live at once
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) h[mt][n + 4] = hi[mt][n];
+        for (int mt = 0; mt < MT; ++mt) {
+          frag_of(hi[mt][0], hi[mt][1], B[mt][2]);
+          frag_of(hi[mt][2], hi[mt][3], B[mt][3]);
+        }
       }
       wave_lds_sync();
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) h[mt][n] = ldf4(park + ((mt * 4 + n) * 64 + lane) * 4);
-      to_frags<MT>(h, B);
+        for (int mt = 0; mt < MT; ++mt)
+          frag_of(ldf4(park + ((mt * 4 + 2 * kb) * 64 + lane) * 4),
+                  ldf4(park + ((mt * 4 + 2 * kb + 1) * 64 + lane) * 4), B[mt][kb]);
     }
     // edge readout, P/Q split (src/flux_gnn.py:62-66)
     float pf[MT], pb[MT];
