@@ -25,6 +25,7 @@
 #include "hf_device.h"
 #include "hf_internal.h"
 
+
 namespace hf {
 namespace chain {
 
@@ -91,7 +92,10 @@ __device__ __forceinline__ void nb_sum(const float (&v)[MT], float (&s)[MT]) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     // the rotated (DPP) operand first: hipcc folds a row_ror mov into the add
-    // only as src0, and does not commute to get it there
+    // only as src0.  (It still canonicalises the row_ror:15 add with the mov as
+    // src1, where it does not fold: one extra VALU per seam value.  Writing the
+    // DPP add as inline asm is NOT safe: hipcc then may reuse a VGPR an
+    // in-flight MFMA still reads as the asm's destination.)
     if (mt == MT - 1 && MT > 1) s[mt] = __fadd_rn(r[mt], l[mt]);
     else s[mt] = __fadd_rn(l[mt], r[mt]);
   }
@@ -133,8 +137,9 @@ __device__ __forceinline__ Small stage_small(const ChainW &W, float *s) {
 template <int CF>
 struct Ring {
   static constexpr int kPerWave = CF / (kWaves * 256);  // 1 KiB DMA instructions per wave per chunk
-  const float *src;  // packed weight stream (global)
-  float *lds;        // 4 slots
+  __amdgpu_buffer_rsrc_t rsrc;  // packed weight stream (global)
+  int lane_off;                 // lane * 16 bytes (the only per-lane address term)
+  float *lds;                   // 4 slots
   int chunks;        // chunks per forward pass
   int wave, lane;
   int pos;           // stream position being consumed (slot = pos & 3)
@@ -144,19 +149,21 @@ struct Ring {
   // bookkeeping: with a visible LDS-DMA in the kernel hipcc gives every
   // ds_read an lgkmcnt(0) wait, which serialises the fragment prefetch.  The
   // ring's own counted vmcnt + barrier in next() order the DMA for readers.
+  // buffer_load ... lds: the chunk offset is an SGPR (soffset), the lane
+  // offset a fixed VGPR, so an issue costs no VALU address arithmetic.
   __device__ __forceinline__ void issue(int chunk, int slot) const {
-    const float *g = src + (size_t)chunk * CF + lane * 4;
     const unsigned d = (unsigned)(uintptr_t)(lds_void *)(lds + slot * CF);
 #pragma unroll
     for (int jj = 0; jj < kPerWave; ++jj) {
       const int j = kPerWave * wave + jj;  // this wave's quarter of the chunk
       const unsigned dst = __builtin_amdgcn_readfirstlane(d + j * 1024);
+      const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(chunk * CF + j * 256) * 4u);
       unsigned keep;
       asm volatile(
           "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-          "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+          "buffer_load_dwordx4 %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
           : "=&s"(keep)
-          : "v"(g + j * 256), "s"(dst)
+          : "v"(lane_off), "s"(dst), "s"(rsrc), "s"(soff)
           : "memory");
     }
   }
@@ -175,7 +182,9 @@ struct Ring {
     // sched_barrier(0) on both sides: the compiler may otherwise move register-only
     // MFMAs across the asm, which orders memory operations only.
     __builtin_amdgcn_sched_barrier(0);
-#ifdef HF_DIAG_NOBAR  // timing diagnostic only: results are wrong
+#if defined(HF_DIAG_NOSYNC)  // timing diagnostic only: results are wrong (no wait, no barrier, no DMA)
+    if (false) {
+#elif defined(HF_DIAG_NOBAR)  // timing diagnostic only: results are wrong
     asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
 #else
     if constexpr (kPerWave == 2)
@@ -183,8 +192,13 @@ struct Ring {
     else
       asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #endif
+#if defined(HF_DIAG_NOSYNC)
+    }
+#endif
     __builtin_amdgcn_sched_barrier(0);
+#if !defined(HF_DIAG_NODMA) && !defined(HF_DIAG_NOSYNC)  // timing diagnostics only
     issue(ahead, (pos + 2) & (kRingSlots - 1));
+#endif
     ahead = ahead + 1 == chunks ? 0 : ahead + 1;
     const float *slot = lds + (pos & (kRingSlots - 1)) * CF;
     ++pos;
@@ -196,9 +210,11 @@ struct Ring {
 template <class Core>
 __device__ __forceinline__ Ring<Core::kChunkFloats> make_ring(const ChainW &W, float *ring_lds) {
   Ring<Core::kChunkFloats> R;
-  R.src = static_cast<const float *>(W.stream);
-  R.lds = ring_lds;
   R.chunks = chain_chunks(W.layers, W.prec);
+  R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0,
+                                             R.chunks * Core::kChunkFloats * 4, 0x00020000);
+  R.lane_off = (threadIdx.x & 63) * 16;
+  R.lds = ring_lds;
   R.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   R.lane = threadIdx.x & 63;
   R.pos = 0;
@@ -220,7 +236,8 @@ __device__ __forceinline__ float *park_of(float *lds, int wave) {
 
 // Readout epilogue for one output tile ot: z_fwd(i) = P(i)+b + Q(i+1),
 // z_bwd(i) = P(i+1)+b + Q(i); flux partial += w2 . ReLU(z)     (src/flux_gnn.py:62-66)
-template <int MT>
+// BIASED: b_e is already in P (the C operand of P's first MFMA).
+template <int MT, bool BIASED = false>
 __device__ __forceinline__ void readout_epilogue(const f4 (&P)[MT], const f4 (&Q)[MT], const f4 be, const f4 w2,
                                                  float (&pf)[MT], float (&pb)[MT]) {
 #pragma unroll
@@ -228,7 +245,7 @@ __device__ __forceinline__ void readout_epilogue(const f4 (&P)[MT], const f4 (&Q
     float pv[MT], qv[MT], pr[MT], qr[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      pv[mt] = __fadd_rn(P[mt][r], be[r]);
+      pv[mt] = BIASED ? P[mt][r] : __fadd_rn(P[mt][r], be[r]);
       qv[mt] = Q[mt][r];
     }
     right_nb<MT>(pv, pr);

@@ -157,11 +157,15 @@ struct CoreF32 {
 
     // message passing: h = ReLU(W_l [h ; (h[i+1]+h[i-1])/2] + b_l)        (src/flux_gnn.py:53-60)
     for (int l = 0; l < W.layers; ++l) {
+      // b_l enters every chain as its initial accumulator (the C operand of
+      // its first MFMA): no bias add in the epilogue
       f4 acc[MT][kNT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int nt = 0; nt < kNT; ++nt) {
+        const f4 bias = ldf4(S.bl + l * kH + 16 * nt + g4);
 #pragma unroll
-        for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = bias;
+      }
       float b[MT];
       b_operand<MT, 0>(h, b);
       layer_chunk<MT, 0>(R, F, h, b, acc);
@@ -181,11 +185,9 @@ struct CoreF32 {
       layer_chunk<MT, 56>(R, F, h, b, acc);
       layer_chunk<MT, 60>(R, F, h, b, acc);
 #pragma unroll
-      for (int nt = 0; nt < kNT; ++nt) {
-        const f4 bias = ldf4(S.bl + l * kH + 16 * nt + g4);
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) h[mt][nt] = relu4(acc[mt][nt] + bias);
-      }
+        for (int nt = 0; nt < kNT; ++nt) h[mt][nt] = relu4(acc[mt][nt]);
     }
 
     // edge readout, P/Q split (src/flux_gnn.py:62-66).  The 128-feature dot
@@ -204,11 +206,15 @@ struct CoreF32 {
       for (int t = 0; t < 2; ++t) {
         const int ot = 2 * w + t;
         f4 P[MT], Q[MT];
+        const f4 be = ldf4(S.be + 16 * ot + g4);  // b_e enters P as the C operand of its first MFMA
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) P[mt] = Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int mt = 0; mt < MT; ++mt) {
+          P[mt] = be;
+          Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
+        }
         readout_chunk<MT, 0>(R, F, h, P, Q);
         readout_chunk<MT, 1>(R, F, h, P, Q);
-        readout_epilogue<MT>(P, Q, ldf4(S.be + 16 * ot + g4), ldf4(S.w2 + 16 * ot + g4), pf, pb);
+        readout_epilogue<MT, true>(P, Q, be, ldf4(S.w2 + 16 * ot + g4), pf, pb);
       }
       float ff[MT], fb[MT];
       readout_finish<MT>(pf, pb, 0.f, ff, fb);

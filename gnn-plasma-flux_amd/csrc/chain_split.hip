@@ -151,9 +151,15 @@ __device__ __forceinline__ void split_gnn(const ChainW &W, const Small &S, Split
   input_layer<MT>(S, lane, feat, h);
   // message passing: h = ReLU(W_l [h ; (h[i+1]+h[i-1])/2] + b_l)        (src/flux_gnn.py:53-60)
   for (int l = 0; l < W.layers; ++l) {
+    // b_l enters each chain as its initial accumulator (the C operand of its
+    // first MFMA), as in CoreF32
     f4 acc[MT][2];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt][0] = acc[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 2; ++t) {
+      const f4 bias = ldf4(S.bl + l * kH + 16 * (2 * wave + t) + g4);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt][t] = bias;
+    }
     split_layer<MT>(F, h, acc, std::make_integer_sequence<int, kKS>{});
     // double-buffered by layer parity: a wave may write layer l+1's tiles
     // while a slower one still reads layer l's
@@ -161,9 +167,8 @@ __device__ __forceinline__ void split_gnn(const ChainW &W, const Small &S, Split
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int nt = 2 * wave + t;
-      const f4 bias = ldf4(S.bl + l * kH + 16 * nt + g4);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) hx4[(nt * 4 + mt) * 64 + lane] = relu4(acc[mt][t] + bias);
+      for (int mt = 0; mt < MT; ++mt) hx4[(nt * 4 + mt) * 64 + lane] = relu4(acc[mt][t]);
     }
     lds_barrier();  // every wave's tiles in LDS
 #pragma unroll
@@ -175,9 +180,14 @@ __device__ __forceinline__ void split_gnn(const ChainW &W, const Small &S, Split
   // edge readout, P/Q split, tiles 2w, 2w+1 of this wave           (src/flux_gnn.py:62-66)
   f4 P[2][MT], Q[2][MT];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < 2; ++t) {
+    const f4 be = ldf4(S.be + 16 * (2 * wave + t) + g4);  // b_e as P's initial accumulator, as CoreF32
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) P[t][mt] = Q[t][mt] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt) {
+      P[t][mt] = be;
+      Q[t][mt] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   split_readout<MT>(F, h, P, Q, std::make_integer_sequence<int, kKS>{});
   float pf[MT], pb[MT], ff[MT], fb[MT];
 #pragma unroll
@@ -185,7 +195,7 @@ __device__ __forceinline__ void split_gnn(const ChainW &W, const Small &S, Split
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int ot = 2 * wave + t;
-    readout_epilogue<MT>(P[t], Q[t], ldf4(S.be + 16 * ot + g4), ldf4(S.w2 + 16 * ot + g4), pf, pb);
+    readout_epilogue<MT, true>(P[t], Q[t], ldf4(S.be + 16 * ot + g4), ldf4(S.w2 + 16 * ot + g4), pf, pb);
   }
   readout_finish<MT>(pf, pb, 0.f, ff, fb);
   if (lane < 16) {
