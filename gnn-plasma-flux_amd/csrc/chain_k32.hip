@@ -117,13 +117,13 @@ struct CoreK32 {
     }
   }
 
-  // h_new = ReLU(acc + (G[i+1] + G[i-1]) / 2 + b) for one half of the output tiles.
+  // h_new = ReLU(acc + (G[i+1] + G[i-1]) / 2) for one half of the output
+  // tiles; the bias is already in acc (the C operand of its first MFMA).
   template <int MT>
   static __device__ __forceinline__ void layer_epilogue(const f4 (&acc)[MT][4], const f4 (&gac)[MT][4],
-                                                        const float *bias, int g4, f4 (&out)[MT][4]) {
+                                                        f4 (&out)[MT][4]) {
 #pragma unroll
     for (int ntl = 0; ntl < 4; ++ntl) {
-      const f4 b = ldf4(bias + 16 * ntl + g4);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float gv[MT], gs[MT];
@@ -133,8 +133,7 @@ struct CoreK32 {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           // acc + 0.5*(G[i+1] + G[i-1]): one rounding either way, 0.5*x is exact
-          const float a = fmaf(gs[mt], 0.5f, acc[mt][ntl][r]);
-          out[mt][ntl][r] = relu(__fadd_rn(a, b[r]));
+          out[mt][ntl][r] = relu(fmaf(gs[mt], 0.5f, acc[mt][ntl][r]));
         }
       }
     }
@@ -145,14 +144,19 @@ struct CoreK32 {
                                                     f4 (&out)[MT][4]) {
     f4 acc[MT][4], gac[MT][4];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int n = 0; n < 4; ++n) {
+      const f4 b = ldf4(bias + 64 * NTH + 16 * n + g4);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[mt][n] = gac[mt][n] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MT; ++mt) {
+        acc[mt][n] = b;
+        gac[mt][n] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
     layer_chunk<MT, 0>(R, B, acc, gac);
     layer_chunk<MT, 1>(R, B, acc, gac);
     layer_chunk<MT, 2>(R, B, acc, gac);
     layer_chunk<MT, 3>(R, B, acc, gac);
-    layer_epilogue<MT>(acc, gac, bias + 64 * NTH, g4, out);
+    layer_epilogue<MT>(acc, gac, out);
   }
 
   // Readout chunk for output tile ot: fragment j = 2*kb + (0: P, 1: Q).
@@ -219,10 +223,14 @@ struct CoreK32 {
     for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
     for (int ot = 0; ot < kNT; ++ot) {
       f4 P[MT], Q[MT];
+      const f4 be = ldf4(S.be + 16 * ot + g4);  // b_e enters P as the C operand of its first MFMA
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) P[mt] = Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MT; ++mt) {
+        P[mt] = be;
+        Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
+      }
       readout_chunk<MT>(R, B, P, Q);
-      readout_epilogue<MT>(P, Q, ldf4(S.be + 16 * ot + g4), ldf4(S.w2 + 16 * ot + g4), pf, pb);
+      readout_epilogue<MT, true>(P, Q, be, ldf4(S.w2 + 16 * ot + g4), pf, pb);
     }
     readout_finish<MT>(pf, pb, W.b2, ffwd, fbwd);
   }
@@ -326,12 +334,17 @@ struct CoreK32A {
     __builtin_amdgcn_sched_group_barrier(0x008, 4 * MT * M::kMma, 0);
   }
 
+  // bias: this half's 64 biases; they enter every chain as its initial
+  // accumulator (the C operand of its first MFMA), so the epilogue adds none.
   template <int MT>
-  static __device__ __forceinline__ void half(R_t &R, Feed &F, const Acts<MT> &X, f4 (&acc)[MT][4]) {
+  static __device__ __forceinline__ void half(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
+                                              f4 (&acc)[MT][4]) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int n = 0; n < 4; ++n) {
+      const f4 b = ldf4(bias + 16 * n + g4);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[mt][n] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MT; ++mt) acc[mt][n] = b;
+    }
     layer_unit<MT, 0, 0>(R, F, X, acc);
     layer_unit<MT, 0, 1>(R, F, X, acc);
     layer_unit<MT, 1, 0>(R, F, X, acc);
@@ -342,17 +355,15 @@ struct CoreK32A {
     layer_unit<MT, 3, 1>(R, F, X, acc);
   }
 
-  // h = ReLU(acc + b) of output tiles (2*KBL, 2*KBL+1) of a half, as 8 values per m-tile.
+  // h = ReLU(acc) (bias already in acc) of output tiles (2*KBL, 2*KBL+1) of a half, as 8 values per m-tile.
   template <int MT, int KBL>
-  static __device__ __forceinline__ void activate(const f4 (&acc)[MT][4], const float *bias, int g4, f8 (&hv)[MT]) {
+  static __device__ __forceinline__ void activate(const f4 (&acc)[MT][4], f8 (&hv)[MT]) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const f4 b = ldf4(bias + 16 * (2 * KBL + t) + g4);
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hv[mt][4 * t + r] = relu(__fadd_rn(acc[mt][2 * KBL + t][r], b[r]));
-    }
+        for (int r = 0; r < 4; ++r) hv[mt][4 * t + r] = relu(acc[mt][2 * KBL + t][r]);
   }
 
   // Readout chunk for output tile ot: fragment j = 2*kb + (0: P, 1: Q), unit u = kb pair.
@@ -404,11 +415,11 @@ struct CoreK32A {
       const float *bias = S.bl + l * kH;
       {
         f4 acc[MT][4];
-        half<MT>(R, F, X, acc);  // output tiles 0..3
+        half<MT>(R, F, X, bias, g4, acc);  // output tiles 0..3
 #pragma unroll
         for (int kbl = 0; kbl < 2; ++kbl) {
           f8 hv[MT];
-          if (kbl == 0) activate<MT, 0>(acc, bias, g4, hv); else activate<MT, 1>(acc, bias, g4, hv);
+          if (kbl == 0) activate<MT, 0>(acc, hv); else activate<MT, 1>(acc, hv);
           Frag fh[MT], fa[MT];
           frags_of<MT>(hv, fh, fa);
 #pragma unroll
@@ -422,11 +433,11 @@ struct CoreK32A {
       }
       {
         f4 acc[MT][4];
-        half<MT>(R, F, X, acc);  // output tiles 4..7
+        half<MT>(R, F, X, bias + 64, g4, acc);  // output tiles 4..7
 #pragma unroll
         for (int kbl = 0; kbl < 2; ++kbl) {
           f8 hv[MT];
-          if (kbl == 0) activate<MT, 0>(acc, bias + 64, g4, hv); else activate<MT, 1>(acc, bias + 64, g4, hv);
+          if (kbl == 0) activate<MT, 0>(acc, hv); else activate<MT, 1>(acc, hv);
           Frag fh[MT], fa[MT];
           frags_of<MT>(hv, fh, fa);
 #pragma unroll
@@ -453,11 +464,15 @@ struct CoreK32A {
     for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
     for (int ot = 0; ot < kNT; ++ot) {
       f4 P[MT], Q[MT];
+      const f4 be = ldf4(S.be + 16 * ot + g4);  // b_e enters P as the C operand of its first MFMA
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) P[mt] = Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MT; ++mt) {
+        P[mt] = be;
+        Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
+      }
       readout_unit<MT, 0>(R, F, X, P, Q);
       readout_unit<MT, 1>(R, F, X, P, Q);
-      readout_epilogue<MT>(P, Q, ldf4(S.be + 16 * ot + g4), ldf4(S.w2 + 16 * ot + g4), pf, pb);
+      readout_epilogue<MT, true>(P, Q, be, ldf4(S.w2 + 16 * ot + g4), pf, pb);
     }
     readout_finish<MT>(pf, pb, W.b2, ffwd, fbwd);
   }
