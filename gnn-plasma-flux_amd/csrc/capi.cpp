@@ -69,9 +69,11 @@ int kperm(int s, int lane) { return 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3); }
 //    chunk (l, gi): k-step s = 4gi + (j>>1), output tile nt = 4(j&1) + c,
 //    k = (s < 32 ? 0 : 128) + kperm(s % 32, lane).  Readout chunk (ot, hh):
 //    k-step s = 16hh + 2j + (c>>1), c&1 selects P = W_e[:, :H] or Q = W_e[:, H:].
-//  k32 `stream`: per layer chunks (nth, kb) for nth = 0..1, kb = 0..3, each
+//  k32 `stream` (f16x3): per layer chunks (nth, kb) for nth = 0..1, kb = 0..3, each
 //    [j = 2*ntl + (W_a|W_b)][term][lane][e 0..7] 16-bit values with output tile
 //    nt = 4nth + ntl and k = (W_b ? 128 : 0) + 16(2kb + (e>>2)) + 4(lane>>4) + (e&3);
+//    bf16: per layer units (pair q = 0..3, kb = 0..3) of [i = 2t + (W_a|W_b)][lane][e],
+//    output tile nt = 2q + t, two units per chunk;
 //    then per readout tile ot one chunk [j = 2kb + (P|Q)][term][lane][e].
 //    f16x3: term 0 = fp16(w), term 1 = fp16(w - term0); bf16: one bf16(w) term.
 //  Row n = 16*tile + (lane&15) throughout.
@@ -148,7 +150,7 @@ void pack_chain(const float *p, int L, int prec, ChainPack &P) {
       for (int e = 0; e < 8; ++e) {
         const int k = kbase + 16 * (2 * kb + (e >> 2)) + 4 * (lane >> 4) + (e & 3);
         // bf16: the 1/deg = 1/2 of the mean aggregation is folded into W_b
-        // (CoreK32A, input-side aggregation); exact, bf16(w/2) == bf16(w)/2
+        // (chain_bf16.hip, input-side aggregation); exact, bf16(w/2) == bf16(w)/2
         const float w = W[(int64_t)row * ld + k] * (halve_b && kbase == kH ? 0.5f : 1.0f);
         if (prec == hf::kPrecBF16) {
           put(out, to_bf16(w));
@@ -159,15 +161,28 @@ void pack_chain(const float *p, int L, int prec, ChainPack &P) {
         }
       }
     };
-    for (int l = 0; l < L; ++l)
-      for (int nth = 0; nth < 2; ++nth)
-        for (int kb = 0; kb < 4; ++kb)
-          for (int j = 0; j < 8; ++j)
-            for (int t = 0; t < terms; ++t)
+    if (prec == hf::kPrecBF16) {
+      // chain_bf16.hip walks a layer by output pair q (tiles 2q, 2q+1), k-block
+      // kb within it: unit (q, kb) = fragments i = 2t + (W_a | W_b), tile 2q + t
+      for (int l = 0; l < L; ++l)
+        for (int qp = 0; qp < 4; ++qp)
+          for (int kb = 0; kb < 4; ++kb)
+            for (int i = 0; i < 4; ++i)
               for (int lane = 0; lane < 64; ++lane) {
-                const int nt = 4 * nth + (j >> 1), ab = j & 1;
-                frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, t, prec == hf::kPrecBF16);
+                const int nt = 2 * qp + (i >> 1), ab = i & 1;
+                frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, 0, true);
               }
+    } else {
+      for (int l = 0; l < L; ++l)
+        for (int nth = 0; nth < 2; ++nth)
+          for (int kb = 0; kb < 4; ++kb)
+            for (int j = 0; j < 8; ++j)
+              for (int t = 0; t < terms; ++t)
+                for (int lane = 0; lane < 64; ++lane) {
+                  const int nt = 4 * nth + (j >> 1), ab = j & 1;
+                  frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, t, false);
+                }
+    }
     for (int ot = 0; ot < kNT; ++ot)
       for (int j = 0; j < 8; ++j)
         for (int t = 0; t < terms; ++t)

@@ -50,17 +50,6 @@ struct ModeF16x3 {
   }
 };
 
-struct ModeBF16 {
-  static constexpr int kNS = 1;
-  static constexpr int kMma = 1;
-  static constexpr int kChunkFloats = 2048;  // 8 KiB
-  using T = b8;
-  static __device__ __forceinline__ void split(const f8 &v, T (&o)[kNS]) { o[0] = __builtin_convertvector(v, b8); }
-  static __device__ __forceinline__ f4 mma(const T (&a)[kNS], const T (&b)[kNS], f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
-  }
-};
-
 template <class M>
 struct CoreK32 {
   static constexpr int kChunkFloats = M::kChunkFloats;
@@ -236,255 +225,13 @@ struct CoreK32 {
   }
 };
 
-// bf16 core with the aggregation on the input side, as the reference forms
-// it: the neighbour sum h[i+1] + h[i-1] is taken in float32 (one VALU per value
-// on the interleaved cell layout) and rounded into its own B fragments; the
-// 1/deg is folded into the packed W_b (bf16(w/2) = bf16(w)/2 exactly).  One
-// accumulator set per output half, so per activated value the epilogue spends
-// ~4.5 VALU (accumulator read, bias, ReLU, neighbour sum, conversions) instead
-// of the linearity form's ~6.5; the issue-bound bf16 rollout is that much
-// shorter.  The new fragments of output half 0 are parked in LDS while half 1
-// still multiplies the old ones.
-template <class M>
-struct CoreK32A {
-  static constexpr int kChunkFloats = M::kChunkFloats;
-  static constexpr int kNS = M::kNS;
-  static constexpr int kKB = kH / 32;
-  // parked fragments of k-blocks 0, 1: [kb 2][h|agg 2][mt 4][term][lane 64][4] floats per wave
-  static constexpr int kParkFloats = 2 * 2 * 4 * kNS * 64 * 4;
-  using T = typename M::T;
-  using R_t = Ring<kChunkFloats>;
-  struct Frag {
-    T v[kNS];
-  };
-  template <int MT>
-  struct Acts {
-    Frag h[MT][kKB], a[MT][kKB];
-  };
-  static __device__ __forceinline__ Frag lds_frag(const float *slot, int j, int lane) {
-    Frag f;
-#pragma unroll
-    for (int s = 0; s < kNS; ++s)
-      f.v[s] = __builtin_bit_cast(T, ldf4(slot + ((j * kNS + s) * 64 + lane) * 4));
-    return f;
-  }
-
-  // Register-prefetched weight feed (as CoreF32's): a chunk is 2 units of 4
-  // fragments (16 MFMAs at MT=4); the next unit's ds_reads issue before this
-  // unit's MFMAs, and the ring's wait + barrier for chunk p+1 precede the
-  // last unit of chunk p.
-  struct Feed {
-    const float *slot;
-    Frag cur[4];
-  };
-  static __device__ __forceinline__ void load_unit(Feed &F, int u, int lane) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) F.cur[i] = lds_frag(F.slot, 4 * u + i, lane);
-  }
-  static __device__ __forceinline__ void begin(R_t &R, Feed &F) {
-    F.slot = R.next();
-    load_unit(F, 0, R.lane);
-  }
-  template <int U>
-  static __device__ __forceinline__ void take(R_t &R, Feed &F, Frag (&a)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = F.cur[i];
-    if constexpr (U == 1) F.slot = R.next();
-    load_unit(F, (U + 1) & 1, R.lane);
-  }
-  static __device__ __forceinline__ float *park_at(float *park, int kb, int ha, int mt, int s, int lane) {
-    return park + ((((kb * 2 + ha) * 4 + mt) * kNS + s) * 64 + lane) * 4;
-  }
-
-  // Fragments of k-block KB (h and its neighbour sums) from 8 activated values per m-tile.
-  template <int MT>
-  static __device__ __forceinline__ void frags_of(const f8 (&hv)[MT], Frag (&fh)[MT], Frag (&fa)[MT]) {
-    f8 av[MT];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float v[MT], s2[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) v[mt] = hv[mt][e];
-      nb_sum<MT>(v, s2);  // index_add_ of h[i+1], h[i-1] (src/flux_gnn.py:55-59); / deg in W_b
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) av[mt][e] = s2[mt];
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      M::split(hv[mt], fh[mt].v);
-      M::split(av[mt], fa[mt].v);
-    }
-  }
-
-  // Update-layer chunk (half, k-block KB): fragment j = 2*ntl + (0: W_a on h, 1: W_b/2 on the sums).
-  template <int MT, int KB, int U>
-  static __device__ __forceinline__ void layer_unit(R_t &R, Feed &F, const Acts<MT> &X, f4 (&acc)[MT][4]) {
-    Frag w[4];
-    take<U>(R, F, w);
-#pragma unroll
-    for (int ab = 0; ab < 2; ++ab)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int ntl = 2 * U + t;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-          acc[mt][ntl] = M::mma(w[2 * t + ab].v, ab ? X.a[mt][KB].v : X.h[mt][KB].v, acc[mt][ntl]);
-      }
-    __builtin_amdgcn_sched_group_barrier(0x100, 4 * kNS, 0);  // next unit's ds_reads first
-    __builtin_amdgcn_sched_group_barrier(0x008, 4 * MT * M::kMma, 0);
-  }
-
-  // bias: this half's 64 biases; they enter every chain as its initial
-  // accumulator (the C operand of its first MFMA), so the epilogue adds none.
-  template <int MT>
-  static __device__ __forceinline__ void half(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
-                                              f4 (&acc)[MT][4]) {
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const f4 b = ldf4(bias + 16 * n + g4);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt][n] = b;
-    }
-    layer_unit<MT, 0, 0>(R, F, X, acc);
-    layer_unit<MT, 0, 1>(R, F, X, acc);
-    layer_unit<MT, 1, 0>(R, F, X, acc);
-    layer_unit<MT, 1, 1>(R, F, X, acc);
-    layer_unit<MT, 2, 0>(R, F, X, acc);
-    layer_unit<MT, 2, 1>(R, F, X, acc);
-    layer_unit<MT, 3, 0>(R, F, X, acc);
-    layer_unit<MT, 3, 1>(R, F, X, acc);
-  }
-
-  // h = ReLU(acc) (bias already in acc) of output tiles (2*KBL, 2*KBL+1) of a half, as 8 values per m-tile.
-  template <int MT, int KBL>
-  static __device__ __forceinline__ void activate(const f4 (&acc)[MT][4], f8 (&hv)[MT]) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hv[mt][4 * t + r] = relu(acc[mt][2 * KBL + t][r]);
-  }
-
-  // Readout chunk for output tile ot: fragment j = 2*kb + (0: P, 1: Q), unit u = kb pair.
-  template <int MT, int U>
-  static __device__ __forceinline__ void readout_unit(R_t &R, Feed &F, const Acts<MT> &X, f4 (&P)[MT], f4 (&Q)[MT]) {
-    Frag w[4];
-    take<U>(R, F, w);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kb = 2 * U + (i >> 1);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        if (i & 1) Q[mt] = M::mma(w[i].v, X.h[mt][kb].v, Q[mt]);
-        else P[mt] = M::mma(w[i].v, X.h[mt][kb].v, P[mt]);
-      }
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 4 * kNS, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 4 * MT * M::kMma, 0);
-  }
-
-  template <int MT>
-  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &F, float *park,
-                                             const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
-    const int lane = R.lane;
-    const int g4 = 4 * (lane >> 4);
-    Acts<MT> X;
-    {
-      f4 h[MT][kNT];
-      input_layer<MT>(S, lane, feat, h);
-#pragma unroll
-      for (int kb = 0; kb < kKB; ++kb) {
-        f8 hv[MT];
-        Frag fh[MT], fa[MT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const f4 x0 = h[mt][2 * kb], x1 = h[mt][2 * kb + 1];
-          hv[mt] = f8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        }
-        frags_of<MT>(hv, fh, fa);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          X.h[mt][kb] = fh[mt];
-          X.a[mt][kb] = fa[mt];
-        }
-      }
-    }
-    // message passing (src/flux_gnn.py:53-60)
-    for (int l = 0; l < W.layers; ++l) {
-      const float *bias = S.bl + l * kH;
-      {
-        f4 acc[MT][4];
-        half<MT>(R, F, X, bias, g4, acc);  // output tiles 0..3
-#pragma unroll
-        for (int kbl = 0; kbl < 2; ++kbl) {
-          f8 hv[MT];
-          if (kbl == 0) activate<MT, 0>(acc, hv); else activate<MT, 1>(acc, hv);
-          Frag fh[MT], fa[MT];
-          frags_of<MT>(hv, fh, fa);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int s = 0; s < kNS; ++s) {
-              *reinterpret_cast<f4 *>(park_at(park, kbl, 0, mt, s, lane)) = __builtin_bit_cast(f4, fh[mt].v[s]);
-              *reinterpret_cast<f4 *>(park_at(park, kbl, 1, mt, s, lane)) = __builtin_bit_cast(f4, fa[mt].v[s]);
-            }
-        }
-      }
-      {
-        f4 acc[MT][4];
-        half<MT>(R, F, X, bias + 64, g4, acc);  // output tiles 4..7
-#pragma unroll
-        for (int kbl = 0; kbl < 2; ++kbl) {
-          f8 hv[MT];
-          if (kbl == 0) activate<MT, 0>(acc, hv); else activate<MT, 1>(acc, hv);
-          Frag fh[MT], fa[MT];
-          frags_of<MT>(hv, fh, fa);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            X.h[mt][2 + kbl] = fh[mt];
-            X.a[mt][2 + kbl] = fa[mt];
-          }
-        }
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int s = 0; s < kNS; ++s) {
-            X.h[mt][kb].v[s] = __builtin_bit_cast(T, ldf4(park_at(park, kb, 0, mt, s, lane)));
-            X.a[mt][kb].v[s] = __builtin_bit_cast(T, ldf4(park_at(park, kb, 1, mt, s, lane)));
-          }
-    }
-    // edge readout, P/Q split (src/flux_gnn.py:62-66)
-    float pf[MT], pb[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
-    for (int ot = 0; ot < kNT; ++ot) {
-      f4 P[MT], Q[MT];
-      const f4 be = ldf4(S.be + 16 * ot + g4);  // b_e enters P as the C operand of its first MFMA
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        P[mt] = be;
-        Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
-      }
-      readout_unit<MT, 0>(R, F, X, P, Q);
-      readout_unit<MT, 1>(R, F, X, P, Q);
-      readout_epilogue<MT, true>(P, Q, be, ldf4(S.w2 + 16 * ot + g4), pf, pb);
-    }
-    readout_finish<MT>(pf, pb, W.b2, ffwd, fbwd);
-  }
-};
-
 }  // namespace
 
 hipError_t launch_chain_flux_k32(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                  const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
   if (w.prec == kPrecF16x3)
     return chain::launch_flux_core<CoreK32<ModeF16x3>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
-  return chain::launch_flux_core<CoreK32A<ModeBF16>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  return launch_chain_flux_bf16(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float *state_final, const float *x,
@@ -493,8 +240,8 @@ hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float 
   if (w.prec == kPrecF16x3)
     return chain::launch_rollout_core<CoreK32<ModeF16x3>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
                                                           flux_traj, metrics, ex, s);
-  return chain::launch_rollout_core<CoreK32A<ModeBF16>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
-                                                       flux_traj, metrics, ex, s);
+  return launch_chain_rollout_bf16(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, ex,
+                                   s);
 }
 
 }  // namespace hf

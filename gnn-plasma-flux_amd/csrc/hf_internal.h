@@ -28,9 +28,10 @@ constexpr int kWinFaces = kWinCells - 2 * kWinHalo - 1;  // 55
 // consumed in order through an LDS ring (chain_common.h):
 //  f32   (v_mfma_f32_16x16x4_f32): 8 KiB chunks, 16 per update layer (4 k-steps
 //        each, [h ; agg] input order) + 2 per readout output tile.
-//  k32   (v_mfma_f32_16x16x32_{f16,bf16}): per update layer 8 chunks, (k-block
-//        kb = 0..3) x (W_a | W_b), then one chunk per readout output tile.
-//        f16x3: 16 KiB chunks of (hi, lo) fp16 fragment pairs; bf16: 8 KiB.
+//  k32   (v_mfma_f32_16x16x32_{f16,bf16}): per update layer 8 chunks, then one
+//        chunk per readout output tile.  f16x3: 16 KiB chunks (output half,
+//        k-block) of (hi, lo) fp16 fragment pairs; bf16: 8 KiB chunks (output
+//        pair, k-block pair), the order chain_bf16.hip walks a layer in.
 // Each chunk is [fragment j][lane 64][16 B], so one wave instruction moves 1 KiB.
 enum ChainPrec { kPrecF32 = HF_WDTYPE_F32, kPrecBF16 = HF_WDTYPE_BF16, kPrecF16x3 = HF_WDTYPE_F16X3 };
 constexpr int kMaxChainLayers = 8;
@@ -104,12 +105,14 @@ hipError_t launch_pinn_run(const float *params, int D, int H, int L, const float
 // order of hf_model_create): update layers interleave weight and bias.
 GraphW graph_view_state_dict(const float *p, int in_dim, int hidden, int layers);
 
-// Per-precision launchers (chain_f32.hip, chain_k32.hip); the generic entry
+// Per-precision launchers (chain_f32.hip, chain_k32.hip = f16x3, chain_bf16.hip); the generic entry
 // points below dispatch on ChainW::prec.
 hipError_t launch_chain_flux_f32(const ChainW &, const float *, const float *, int64_t, const float *, int, int,
                                  float *, float *, hipStream_t);
 hipError_t launch_chain_flux_k32(const ChainW &, const float *, const float *, int64_t, const float *, int, int,
                                  float *, float *, hipStream_t);
+hipError_t launch_chain_flux_bf16(const ChainW &, const float *, const float *, int64_t, const float *, int, int,
+                                  float *, float *, hipStream_t);
 // Extra outputs of the persistent rollout: a classical twin of every IC
 // stepped in the same wave (hf_run_compare), all optional.
 struct RolloutExtras {
@@ -127,6 +130,9 @@ hipError_t launch_chain_rollout_split(const ChainW &, const float *, float *, co
 hipError_t launch_chain_rollout_k32(const ChainW &, const float *, float *, const float *, const double *, int, int,
                                     int, float, float, float *, float *, float *, const RolloutExtras &,
                                     hipStream_t);
+hipError_t launch_chain_rollout_bf16(const ChainW &, const float *, float *, const float *, const double *, int, int,
+                                     int, float, float, float *, float *, float *, const RolloutExtras &,
+                                     hipStream_t);
 
 // Chain flux.  Feature source: AoS node features [B*nx][4] (nf != nullptr)
 // or SoA state [B][3][nx] with IC stride ld_state floats + x[nx].

@@ -104,3 +104,37 @@ def test_bf16_vs_bf16_weight_oracle(hf, nx):
     err_f = close(fe, fe_want[:, 0], 2e-2)
     err_s = close(solver.run_batch(ics, 10)["traj"].cpu().numpy(), want, 2e-2)
     print(f"bf16 nx={nx}: max flux err {err_f:.2e}, 10-step state err {err_s:.2e}")
+
+
+def rand_sd(layers, seed):
+    """Random FluxGNN(4, 128, layers) state dict (reference keys, src/flux_gnn.py:17-38)."""
+    g = np.random.default_rng(seed)
+    sd = {"input_mlp.0.weight": g.normal(0, 0.5, (128, 4)), "input_mlp.0.bias": g.normal(0, 0.1, 128)}
+    for l in range(layers):
+        sd[f"update_mlps.{l}.0.weight"] = g.normal(0, 1 / 16, (128, 256))
+        sd[f"update_mlps.{l}.0.bias"] = g.normal(0, 0.1, 128)
+    sd["edge_mlp.0.weight"] = g.normal(0, 1 / 16, (128, 256))
+    sd["edge_mlp.0.bias"] = g.normal(0, 0.1, 128)
+    sd["edge_mlp.2.weight"] = g.normal(0, 1 / 11, (1, 128))
+    sd["edge_mlp.2.bias"] = g.normal(0, 0.1, 1)
+    return {k: np.asarray(v, np.float32) for k, v in sd.items()}
+
+
+@pytest.mark.parametrize("layers", [0, 1, 3])
+@pytest.mark.parametrize("nx", [16, 48, 64, 100])
+def test_bf16_flux_layers_and_nx(hf, layers, nx):
+    """The pair-pipelined bf16 core at every layer count it special-cases
+    (none, one, several) and every chain-kernel shape: MT = 1, 3, 4 exact and
+    the windowed kernel (nx=100); vs the float32 oracle on bf16-rounded weights."""
+    sd = rand_sd(layers, 40 + layers)
+    G = O.Grid(nx, dt=5e-3)
+    ics = np.stack([O.initial_condition(G, s) for s in (11, 12, 13, 14, 15)])
+    want = O.hybrid_flux_edge(O.params_from(O.bf16_weights(sd)), G, ics)
+    m = hf.FluxGNN(4, 128, layers, precision="bf16")
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to(DEV)
+    nf, ei = hf.build_chain_graph_batch(ics, G.x, DEV)
+    with torch.no_grad():
+        fe = m(nf, ei).cpu().numpy().reshape(5, 2 * nx)
+    err = close(fe, want, 2e-2)
+    print(f"bf16 L={layers} nx={nx}: max flux err {err:.2e}")

@@ -84,6 +84,10 @@ def main():
     out["layer_frac_of_f32_peak"] = FLOP_LAYER * cells / (slope * 1e-3) / 157.3e12
     out["fixed_ms"] = per_l[0]
     out["fixed_frac_of_f32_peak"] = FLOP_FIXED * cells / (per_l[0] * 1e-3) / 157.3e12
+    peak = 157.3e12 if prec == "f32" else 2.5e15  # fp32 MFMA; dense bf16/f16 MFMA (f16x3: 3 products each)
+    mult = 3 if prec == "f16x3" else 1
+    out["layer_frac_of_prec_peak"] = mult * FLOP_LAYER * cells / (slope * 1e-3) / peak
+    out["fixed_frac_of_prec_peak"] = mult * FLOP_FIXED * cells / (per_l[0] * 1e-3) / peak
     out["precision"] = prec
     print(json.dumps(out))
 
