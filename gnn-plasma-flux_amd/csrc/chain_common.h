@@ -234,28 +234,34 @@ __device__ __forceinline__ float *park_of(float *lds, int wave) {
          wave * Core::kParkFloats;
 }
 
-// Readout epilogue for one output tile ot: z_fwd(i) = P(i)+b + Q(i+1),
+// Row R of the readout epilogue for one output tile ot: z_fwd(i) = P(i)+b + Q(i+1),
 // z_bwd(i) = P(i+1)+b + Q(i); flux partial += w2 . ReLU(z)     (src/flux_gnn.py:62-66)
 // BIASED: b_e is already in P (the C operand of P's first MFMA).
+template <int MT, int R, bool BIASED = false>
+__device__ __forceinline__ void readout_row(const f4 (&P)[MT], const f4 (&Q)[MT], const f4 be, const f4 w2,
+                                            float (&pf)[MT], float (&pb)[MT]) {
+  float pv[MT], qv[MT], pr[MT], qr[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    pv[mt] = BIASED ? P[mt][R] : __fadd_rn(P[mt][R], be[R]);
+    qv[mt] = Q[mt][R];
+  }
+  right_nb<MT>(pv, pr);
+  right_nb<MT>(qv, qr);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    pf[mt] = fmaf(w2[R], relu(__fadd_rn(pv[mt], qr[mt])), pf[mt]);
+    pb[mt] = fmaf(w2[R], relu(__fadd_rn(pr[mt], qv[mt])), pb[mt]);
+  }
+}
+// The whole epilogue of one tile: rows 0..3 in order.
 template <int MT, bool BIASED = false>
 __device__ __forceinline__ void readout_epilogue(const f4 (&P)[MT], const f4 (&Q)[MT], const f4 be, const f4 w2,
                                                  float (&pf)[MT], float (&pb)[MT]) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float pv[MT], qv[MT], pr[MT], qr[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      pv[mt] = BIASED ? P[mt][r] : __fadd_rn(P[mt][r], be[r]);
-      qv[mt] = Q[mt][r];
-    }
-    right_nb<MT>(pv, pr);
-    right_nb<MT>(qv, qr);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      pf[mt] = fmaf(w2[r], relu(__fadd_rn(pv[mt], qr[mt])), pf[mt]);
-      pb[mt] = fmaf(w2[r], relu(__fadd_rn(pr[mt], qv[mt])), pb[mt]);
-    }
-  }
+  readout_row<MT, 0, BIASED>(P, Q, be, w2, pf, pb);
+  readout_row<MT, 1, BIASED>(P, Q, be, w2, pf, pb);
+  readout_row<MT, 2, BIASED>(P, Q, be, w2, pf, pb);
+  readout_row<MT, 3, BIASED>(P, Q, be, w2, pf, pb);
 }
 
 // The 128-feature dot product is split over the 4 lane groups of a column.

@@ -133,6 +133,9 @@ struct CoreF32 {
     }
     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // next unit's ds_reads first
     __builtin_amdgcn_sched_group_barrier(0x008, 8 * MT, 0);
+    // close the unit's region: otherwise the DS group above may be filled with
+    // a LATER unit's reads and this unit's prefetch lands just before its use
+    __builtin_amdgcn_sched_barrier(0);
   }
   template <int MT, int HH>
   static __device__ __forceinline__ void readout_chunk(R_t &R, Feed &F, const f4 (&h)[MT][kNT], f4 (&P)[MT],
@@ -224,7 +227,6 @@ struct CoreF32 {
         sb[mt] = __fadd_rn(sb[mt], fb[mt]);
       }
     }
-#pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       ffwd[mt] = __fadd_rn(sf[mt], W.b2);
       fbwd[mt] = __fadd_rn(sb[mt], W.b2);
