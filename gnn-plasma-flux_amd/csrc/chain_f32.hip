@@ -227,6 +227,7 @@ struct CoreF32 {
         sb[mt] = __fadd_rn(sb[mt], fb[mt]);
       }
     }
+#pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       ffwd[mt] = __fadd_rn(sf[mt], W.b2);
       fbwd[mt] = __fadd_rn(sb[mt], W.b2);
