@@ -258,6 +258,11 @@ __device__ __forceinline__ void readout_row(const f4 (&P)[MT], const f4 (&Q)[MT]
 template <int MT, bool BIASED = false>
 __device__ __forceinline__ void readout_epilogue(const f4 (&P)[MT], const f4 (&Q)[MT], const f4 be, const f4 w2,
                                                  float (&pf)[MT], float (&pb)[MT]) {
+#ifdef HF_DIAG_NOEPI  // timing diagnostic only: results are wrong (one add per value instead of the epilogue)
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) pf[mt] += P[mt][0] + P[mt][1] + P[mt][2] + P[mt][3], pb[mt] += Q[mt][0] + Q[mt][1] + Q[mt][2] + Q[mt][3];
+  return;
+#endif
   readout_row<MT, 0, BIASED>(P, Q, be, w2, pf, pb);
   readout_row<MT, 1, BIASED>(P, Q, be, w2, pf, pb);
   readout_row<MT, 2, BIASED>(P, Q, be, w2, pf, pb);
@@ -268,6 +273,11 @@ __device__ __forceinline__ void readout_epilogue(const f4 (&P)[MT], const f4 (&Q
 template <int MT>
 __device__ __forceinline__ void readout_finish(float (&pf)[MT], float (&pb)[MT], float b2, float (&ffwd)[MT],
                                                float (&fbwd)[MT]) {
+#ifdef HF_DIAG_NOFINISH  // timing diagnostic only: results are wrong (no cross-lane sums)
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) ffwd[mt] = pf[mt] + b2, fbwd[mt] = pb[mt] + b2;
+  return;
+#endif
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     pf[mt] += __shfl_xor(pf[mt], 16, 64);
