@@ -101,7 +101,6 @@ uint16_t f16_bits(_Float16 h) {
 
 struct ChainPack {
   std::vector<unsigned char> stream;
-  std::vector<float> split;  // f32: chain_split.hip per-wave streams
   std::vector<float> small;
   int64_t o_win = 0, o_bin = 0, o_bl = 0, o_be = 0, o_w2 = 0;
   float b2 = 0.f;
@@ -211,38 +210,6 @@ void pack_chain(const float *p, int L, int prec, ChainPack &P) {
   P.b2 = p[lay.b_2];
 }
 
-// Feature-split f32 streams (chain_split.hip): for wave w = 0..3, a private
-// stream of (L + 1) * 32 units of [lane 64][4] floats.  Update-layer unit
-// (l, kp): k-steps s = 2kp, 2kp+1, tiles nt = 2w, 2w+1, in the order
-// (s, 2w), (s, 2w+1), (s+1, 2w), (s+1, 2w+1); W_b halved as in `stream`.
-// Readout unit s: (P, 2w), (Q, 2w), (P, 2w+1), (Q, 2w+1) at k-step s.
-void pack_chain_split(const float *p, int L, std::vector<float> &out) {
-  using hf::kH;
-  using hf::kKS;
-  const Layout lay(hf::kIn, kH, L);
-  auto layer_w = [&](int l) { return p + lay.w_l + (int64_t)l * ((int64_t)kH * 2 * kH + kH); };
-  auto A = [&](int l, int s, int nt, int lane) {
-    const int k = (s < kKS ? 0 : kH) + kperm(s % kKS, lane);
-    const float v = layer_w(l)[(int64_t)(16 * nt + (lane & 15)) * 2 * kH + k];
-    return s >= kKS ? v * 0.5f : v;
-  };
-  auto E = [&](int s, int ot, int pq, int lane) {
-    return p[lay.w_e + (int64_t)(16 * ot + (lane & 15)) * 2 * kH + pq * kH + kperm(s, lane)];
-  };
-  out.clear();
-  for (int w = 0; w < 4; ++w) {
-    for (int l = 0; l < L; ++l)
-      for (int kp = 0; kp < kKS; ++kp)
-        for (int lane = 0; lane < 64; ++lane)
-          for (int q = 0; q < 2; ++q)
-            for (int t = 0; t < 2; ++t) out.push_back(A(l, 2 * kp + q, 2 * w + t, lane));
-    for (int s = 0; s < kKS; ++s)
-      for (int lane = 0; lane < 64; ++lane)
-        for (int t = 0; t < 2; ++t)
-          for (int pq = 0; pq < 2; ++pq) out.push_back(E(s, 2 * w + t, pq, lane));
-  }
-}
-
 hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 bool fused_nx(int nx) { return nx == 16 || nx == 32 || nx == 48 || nx == 64; }
@@ -306,7 +273,6 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
   // natural copy (graph path) followed by the packed copy (chain path)
   ChainPack pk;
   if (m->chain_ok) pack_chain(host_params, layers, wdtype, pk);
-  if (m->chain_ok && wdtype == hf::kPrecF32) pack_chain_split(host_params, layers, pk.split);
   // natural layer weights are split into contiguous [L][H][2H] and [L][H]
   std::vector<float> nat((size_t)lay.total);
   {
@@ -330,7 +296,7 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
   const size_t nat_bytes = (sizeof(float) * nat.size() + 255) & ~size_t(255);
   const size_t stream_bytes = (pk.stream.size() + 255) & ~size_t(255);
   const size_t small_bytes = (sizeof(float) * pk.small.size() + 255) & ~size_t(255);
-  const size_t bytes = nat_bytes + stream_bytes + small_bytes + sizeof(float) * pk.split.size();
+  const size_t bytes = nat_bytes + stream_bytes + small_bytes;
   hipError_t e = hipMalloc(&m->dev, bytes);
   if (e != hipSuccess) {
     delete m;
@@ -342,9 +308,6 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
     e = hipMemcpy(base + nat_bytes, pk.stream.data(), pk.stream.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && !pk.small.empty())
     e = hipMemcpy(base + nat_bytes + stream_bytes, pk.small.data(), sizeof(float) * pk.small.size(),
-                  hipMemcpyHostToDevice);
-  if (e == hipSuccess && !pk.split.empty())
-    e = hipMemcpy(base + nat_bytes + stream_bytes + small_bytes, pk.split.data(), sizeof(float) * pk.split.size(),
                   hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     (void)hipFree(m->dev);
@@ -373,7 +336,6 @@ int hf_model_create(const float *host_params, int in_dim, int hidden, int layers
     const float *d = reinterpret_cast<const float *>(base + nat_bytes + stream_bytes);
     hf::ChainW &c = m->chain;
     c.stream = base + nat_bytes;
-    c.split = pk.split.empty() ? nullptr : base + nat_bytes + stream_bytes + small_bytes;
     c.prec = wdtype;
     c.win = d + pk.o_win;
     c.bin = d + pk.o_bin;

@@ -101,6 +101,13 @@ __device__ __forceinline__ void nb_sum(const float (&v)[MT], float (&s)[MT]) {
   }
 }
 
+// Workgroup barrier that also orders this wave's LDS traffic.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ f4 relu4(f4 v) { return f4{relu(v.x), relu(v.y), relu(v.z), relu(v.w)}; }
 
 __device__ __forceinline__ f4 ldf4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
@@ -112,6 +119,47 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 // ------------------------------------------------------------------ LDS plan
 constexpr int kWaves = 4;  // one IC (item) per wave
 constexpr int kRingSlots = 4;
+
+// --------------------------------------------------------- cell-split waves
+// An IC of 16*W cells spread over W waves, 16 consecutive cells per wave
+// (MT = 1, lane column j = cell 16*pos + j).  The chain neighbours that fall
+// off a wave's 16 lanes come from the adjacent waves' boundary columns,
+// exchanged through LDS once per layer (chain_rollout_cells_kernel, chain_f32.hip).
+struct NoHalo {
+  static constexpr bool kOn = false;
+};
+struct CellHalo {
+  static constexpr bool kOn = true;
+  f4 l[kNT], r[kNT];  // the lane's 32 features at cell 16*pos - 1 (lanes j=0) / 16*pos + 16 (lanes j=15)
+  f4 *xh;             // [parity 2][wave 4][side 2][g 4][nt 8]: boundary columns of h
+  f4 *xq;             // [wave 4][ot 8][P|Q 2][g 4]: column j=0 of the readout accumulators
+  int wave, lw, rw, lane, par;
+  // Publish this wave's boundary columns of h (j = 0: side 0, j = 15: side 1),
+  // then read the left wave's side 1 and the right wave's side 0.
+  __device__ __forceinline__ void exchange(const f4 (&h)[1][kNT]) {
+    f4 *b = xh + par * (kWaves * 2 * 4 * kNT);
+    const int j = lane & 15, g = lane >> 4;
+    if (j == 0 || j == 15) {
+      const int side = j == 15;
+#pragma unroll
+      for (int nt = 0; nt < kNT; ++nt) b[((wave * 2 + side) * 4 + g) * kNT + nt] = h[0][nt];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int nt = 0; nt < kNT; ++nt) {
+      l[nt] = b[((lw * 2 + 1) * 4 + g) * kNT + nt];
+      r[nt] = b[((rw * 2 + 0) * 4 + g) * kNT + nt];
+    }
+    par ^= 1;
+  }
+};
+
+// v[i-1] + v[i+1] for a cell-split wave: row shifts, with the lane that falls
+// off the row taking the halo value.  The same single fp32 add as nb_sum.
+__device__ __forceinline__ float nb_sum_halo(float v, float hl, float hr) {
+  return __fadd_rn(dpp_over<kRowShr1>(hl, v), dpp_over<kRowShl1>(hr, v));
+}
+
 constexpr int kSmallFloats = 512 + kH * (3 + kMaxChainLayers);  // win, bin, be, w2, bl[L]
 // per wave: n,u,E,x,F,rho | 64 doubles (Poisson column) | classical twin n,u,E,F,rho
 constexpr int kWaveScratchFloats = 6 * 64 + 2 * 64 + 5 * 64;
@@ -253,6 +301,16 @@ __device__ __forceinline__ void readout_row(const f4 (&P)[MT], const f4 (&Q)[MT]
     pf[mt] = fmaf(w2[R], relu(__fadd_rn(pv[mt], qr[mt])), pf[mt]);
     pb[mt] = fmaf(w2[R], relu(__fadd_rn(pr[mt], qv[mt])), pb[mt]);
   }
+}
+// Row R of the readout epilogue on a cell-split wave (MT = 1, b_e in P):
+// P(i+1) and Q(i+1) of lane j = 15 come from the right wave (prh, qrh).
+template <int R>
+__device__ __forceinline__ void readout_row_halo(const f4 &P, const f4 &Q, const f4 &prh, const f4 &qrh, const f4 w2,
+                                                 float &pf, float &pb) {
+  const float pv = P[R], qv = Q[R];
+  const float pr = dpp_over<kRowShl1>(prh[R], pv), qr = dpp_over<kRowShl1>(qrh[R], qv);
+  pf = fmaf(w2[R], relu(__fadd_rn(pv, qr)), pf);
+  pb = fmaf(w2[R], relu(__fadd_rn(pr, qv)), pb);
 }
 // The whole epilogue of one tile: rows 0..3 in order.
 template <int MT, bool BIASED = false>

@@ -55,9 +55,10 @@ struct CoreF32 {
 #endif
   }
   // B operand of flat k-step KS (0..63) of an update layer: k-steps 0..31 read
-  // h itself, 32..63 the neighbour mean (h[i+1] + h[i-1]) / 2.
-  template <int MT, int KS>
-  static __device__ __forceinline__ void b_operand(const f4 (&h)[MT][kNT], float (&b)[MT]) {
+  // h itself, 32..63 the neighbour mean (h[i+1] + h[i-1]) / 2.  H = CellHalo:
+  // a cell-split wave (MT = 1), its boundary neighbours from X's halos.
+  template <int MT, int KS, class H>
+  static __device__ __forceinline__ void b_operand(const f4 (&h)[MT][kNT], float (&b)[MT], const H &X) {
     constexpr int s = KS % kKS;  // k-step within its 128-wide half
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) b[mt] = h[mt][s >> 2][s & 3];
@@ -66,10 +67,15 @@ struct CoreF32 {
 #else
     if constexpr (KS >= kKS) {
 #endif
-      float sum[MT];
-      nb_sum<MT>(b, sum);  // index_add_ of h[i+1], h[i-1]; the / deg 2 is folded into W_b
+      if constexpr (H::kOn) {
+        static_assert(MT == 1, "cell-split waves hold 16 cells");
+        b[0] = nb_sum_halo(b[0], X.l[s >> 2][s & 3], X.r[s >> 2][s & 3]);
+      } else {
+        float sum[MT];
+        nb_sum<MT>(b, sum);  // index_add_ of h[i+1], h[i-1]; the / deg 2 is folded into W_b
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) b[mt] = sum[mt];
+        for (int mt = 0; mt < MT; ++mt) b[mt] = sum[mt];
+      }
     }
   }
 
@@ -77,13 +83,13 @@ struct CoreF32 {
   // B operand on entry and the next k-step's on exit: the next operand's lane
   // shifts are interleaved with this k-step's MFMAs instead of stalling the
   // matrix pipe between m-tiles.
-  template <int MT, int KS>
+  template <int MT, int KS, class H>
   static __device__ __forceinline__ void layer_step(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
-                                                    f4 (&acc)[MT][kNT]) {
+                                                    f4 (&acc)[MT][kNT], const H &X) {
     f4 a[2];
     take<KS & 3>(R, F, a);
     float bn[MT];
-    if constexpr (KS + 1 < 2 * kKS) b_operand<MT, KS + 1>(h, bn);
+    if constexpr (KS + 1 < 2 * kKS) b_operand<MT, KS + 1>(h, bn, X);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -105,13 +111,13 @@ struct CoreF32 {
       for (int mt = 0; mt < MT; ++mt) b[mt] = bn[mt];
     }
   }
-  template <int MT, int KS0>
+  template <int MT, int KS0, class H>
   static __device__ __forceinline__ void layer_chunk(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
-                                                     f4 (&acc)[MT][kNT]) {
-    layer_step<MT, KS0 + 0>(R, F, h, b, acc);
-    layer_step<MT, KS0 + 1>(R, F, h, b, acc);
-    layer_step<MT, KS0 + 2>(R, F, h, b, acc);
-    layer_step<MT, KS0 + 3>(R, F, h, b, acc);
+                                                     f4 (&acc)[MT][kNT], const H &X) {
+    layer_step<MT, KS0 + 0>(R, F, h, b, acc, X);
+    layer_step<MT, KS0 + 1>(R, F, h, b, acc, X);
+    layer_step<MT, KS0 + 2>(R, F, h, b, acc, X);
+    layer_step<MT, KS0 + 3>(R, F, h, b, acc, X);
   }
 
   // One readout unit: k-steps s = 16*HH + 4*U + i for P (W_e[:, :H]) and Q (W_e[:, H:]).
@@ -146,6 +152,51 @@ struct CoreF32 {
     readout_unit<MT, HH, 3>(R, F, h, P, Q);
   }
 
+  // Edge readout of a cell-split wave (MT = 1): all 8 output tiles' P and Q
+  // first, then column j = 0 of each through LDS (P(i+1), Q(i+1) of lane 15
+  // live on the right wave), then the epilogues and partial dots in the same
+  // order as gnn_impl's readout, so the fluxes are bit-identical to it.
+  static __device__ __forceinline__ void readout_cells(const ChainW &W, const Small &S, R_t &R, Feed &F,
+                                                       const f4 (&h)[1][kNT], float (&ffwd)[1], float (&fbwd)[1],
+                                                       CellHalo &X) {
+    const int lane = R.lane, j = lane & 15, g = lane >> 4, g4 = 4 * g;
+    f4 P[kNT][1], Q[kNT][1];
+#pragma unroll
+    for (int ot = 0; ot < kNT; ++ot) {
+      P[ot][0] = ldf4(S.be + 16 * ot + g4);  // b_e as P's initial accumulator
+      Q[ot][0] = f4{0.f, 0.f, 0.f, 0.f};
+      readout_chunk<1, 0>(R, F, h, P[ot], Q[ot]);
+      readout_chunk<1, 1>(R, F, h, P[ot], Q[ot]);
+      if (j == 0) {
+        X.xq[((X.wave * kNT + ot) * 2 + 0) * 4 + g] = P[ot][0];
+        X.xq[((X.wave * kNT + ot) * 2 + 1) * 4 + g] = Q[ot][0];
+      }
+    }
+    lds_barrier();
+    float sf = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < kNT / 2; ++w) {
+      float pf = 0.f, pb = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ot = 2 * w + t;
+        const f4 prh = X.xq[((X.rw * kNT + ot) * 2 + 0) * 4 + g];
+        const f4 qrh = X.xq[((X.rw * kNT + ot) * 2 + 1) * 4 + g];
+        const f4 w2 = ldf4(S.w2 + 16 * ot + g4);
+        readout_row_halo<0>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
+        readout_row_halo<1>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
+        readout_row_halo<2>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
+        readout_row_halo<3>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
+      }
+      float pf1[1] = {pf}, pb1[1] = {pb}, ff[1], fb[1];
+      readout_finish<1>(pf1, pb1, 0.f, ff, fb);
+      sf = __fadd_rn(sf, ff[0]);
+      sb = __fadd_rn(sb, fb[0]);
+    }
+    ffwd[0] = __fadd_rn(sf, W.b2);
+    fbwd[0] = __fadd_rn(sb, W.b2);
+  }
+
   // FluxGNN forward for the MT*16 cells of this wave.  feat[mt] is the lane's
   // input feature (index l>>4 of [n,u,E,x]) of cell cell_of<MT>(mt, l&15).  Returns
   // the edge fluxes of (i -> i+1) in ffwd and of (i+1 -> i) in fbwd for cell
@@ -153,10 +204,26 @@ struct CoreF32 {
   template <int MT>
   static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &F, float * /*park*/,
                                              const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
+    NoHalo X;
+    gnn_impl<MT, NoHalo>(W, S, R, F, feat, ffwd, fbwd, X);
+  }
+  // A cell-split wave: 16 consecutive cells of an IC spread over several
+  // waves (chain_rollout_cells_kernel below), boundary columns exchanged through X.
+  static __device__ __forceinline__ void gnn_cells(const ChainW &W, const Small &S, R_t &R, Feed &F,
+                                                   const float (&feat)[1], float (&ffwd)[1], float (&fbwd)[1],
+                                                   CellHalo &X) {
+    gnn_impl<1, CellHalo>(W, S, R, F, feat, ffwd, fbwd, X);
+  }
+
+  template <int MT, class H>
+  static __device__ __forceinline__ void gnn_impl(const ChainW &W, const Small &S, R_t &R, Feed &F,
+                                                  const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT],
+                                                  H &X) {
     const int lane = R.lane;
     const int g4 = 4 * (lane >> 4);
     f4 h[MT][kNT];
     input_layer<MT>(S, lane, feat, h);
+    if constexpr (H::kOn) X.exchange(h);
 
     // message passing: h = ReLU(W_l [h ; (h[i+1]+h[i-1])/2] + b_l)        (src/flux_gnn.py:53-60)
     for (int l = 0; l < W.layers; ++l) {
@@ -170,34 +237,41 @@ struct CoreF32 {
         for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = bias;
       }
       float b[MT];
-      b_operand<MT, 0>(h, b);
-      layer_chunk<MT, 0>(R, F, h, b, acc);
-      layer_chunk<MT, 4>(R, F, h, b, acc);
-      layer_chunk<MT, 8>(R, F, h, b, acc);
-      layer_chunk<MT, 12>(R, F, h, b, acc);
-      layer_chunk<MT, 16>(R, F, h, b, acc);
-      layer_chunk<MT, 20>(R, F, h, b, acc);
-      layer_chunk<MT, 24>(R, F, h, b, acc);
-      layer_chunk<MT, 28>(R, F, h, b, acc);
-      layer_chunk<MT, 32>(R, F, h, b, acc);
-      layer_chunk<MT, 36>(R, F, h, b, acc);
-      layer_chunk<MT, 40>(R, F, h, b, acc);
-      layer_chunk<MT, 44>(R, F, h, b, acc);
-      layer_chunk<MT, 48>(R, F, h, b, acc);
-      layer_chunk<MT, 52>(R, F, h, b, acc);
-      layer_chunk<MT, 56>(R, F, h, b, acc);
-      layer_chunk<MT, 60>(R, F, h, b, acc);
+      b_operand<MT, 0>(h, b, X);
+      layer_chunk<MT, 0>(R, F, h, b, acc, X);
+      layer_chunk<MT, 4>(R, F, h, b, acc, X);
+      layer_chunk<MT, 8>(R, F, h, b, acc, X);
+      layer_chunk<MT, 12>(R, F, h, b, acc, X);
+      layer_chunk<MT, 16>(R, F, h, b, acc, X);
+      layer_chunk<MT, 20>(R, F, h, b, acc, X);
+      layer_chunk<MT, 24>(R, F, h, b, acc, X);
+      layer_chunk<MT, 28>(R, F, h, b, acc, X);
+      layer_chunk<MT, 32>(R, F, h, b, acc, X);
+      layer_chunk<MT, 36>(R, F, h, b, acc, X);
+      layer_chunk<MT, 40>(R, F, h, b, acc, X);
+      layer_chunk<MT, 44>(R, F, h, b, acc, X);
+      layer_chunk<MT, 48>(R, F, h, b, acc, X);
+      layer_chunk<MT, 52>(R, F, h, b, acc, X);
+      layer_chunk<MT, 56>(R, F, h, b, acc, X);
+      layer_chunk<MT, 60>(R, F, h, b, acc, X);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) h[mt][nt] = relu4(acc[mt][nt]);
+      if constexpr (H::kOn) {
+        if (l + 1 < W.layers) X.exchange(h);
+      }
+    }
+    if constexpr (H::kOn) {
+      readout_cells(W, S, R, F, h, ffwd, fbwd, X);
+      return;
     }
 
     // edge readout, P/Q split (src/flux_gnn.py:62-66).  The 128-feature dot
     // w2 . ReLU(z) is summed as four partial dots over tile pairs (2w, 2w+1),
-    // then added in w order: the order of chain_split.hip, so both rollout
-    // kernels give bit-identical results and a batch is invariant to which
-    // of them its size selects.
+    // then added in w order; readout_cells keeps the same order, so both
+    // rollout kernels give bit-identical results and a batch is invariant to
+    // which of them its size selects.
     float sf[MT], sb[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) sf[mt] = sb[mt] = 0.f;
@@ -235,7 +309,153 @@ struct CoreF32 {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Cell-split persistent rollout for small batches: an IC of NX = 16*WPI cells
+// on WPI waves (16 consecutive cells each, CoreF32 at MT = 1), 4/WPI ICs per
+// workgroup (WPI = 3: one IC and a shadow wave that keeps the weight ring's
+// lockstep and writes nothing).  B ICs occupy B*WPI/4 CUs' worth of waves
+// instead of B/4, for the same per-cell arithmetic as chain_rollout_kernel:
+// every MFMA chain, neighbour sum, readout partial dot and FV/Poisson
+// expression is evaluated in the same order, so the results are bit-identical
+// to it.  The four waves share the LDS weight ring as in chain_rollout_kernel;
+// per layer they swap boundary columns of h (CellHalo), per step column 0 of
+// the readout accumulators.  The IC's first wave does FV + Poisson + outputs
+// for all its cells, one per lane (src/hybrid_solver.py:45-63).
+constexpr int kXhF4 = 2 * kWaves * 2 * 4 * kNT;  // CellHalo::xh
+constexpr int kXqF4 = kWaves * kNT * 2 * 4;      // CellHalo::xq
+constexpr int kCellsLds =
+    kRingSlots * CoreF32::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats + 4 * (kXhF4 + kXqF4);
+
+template <int WPI>
+__global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
+    ChainW W, const float *__restrict__ state0, float *__restrict__ state_final, const float *__restrict__ x,
+    const double *__restrict__ pc, int B, int T, float c, float dt, float *__restrict__ traj,
+    float *__restrict__ flux_traj, float *__restrict__ metrics) {
+  constexpr int NX = 16 * WPI;
+  constexpr int IPW = kWaves / WPI;  // ICs per workgroup
+  constexpr int kRingFloats = kRingSlots * CoreF32::kChunkFloats;
+  __shared__ f4 lds4[kCellsLds / 4];
+  float *lds = reinterpret_cast<float *>(lds4);
+  const Small S = stage_small(W, lds + kRingFloats);
+  auto R = make_ring<CoreF32>(W, lds);
+  const int wave = R.wave, lane = R.lane, j = lane & 15, g = lane >> 4;
+  const bool shadow = wave >= IPW * WPI;
+  const int slot = shadow ? 0 : wave / WPI;  // IC of this wave within the workgroup
+  const int pos = shadow ? 0 : wave % WPI;   // cells 16*pos .. 16*pos + 15 of it
+  const bool lead = !shadow && pos == 0;
+  CellHalo X;
+  X.xh = reinterpret_cast<f4 *>(lds + kRingFloats + kSmallFloats + kWaves * kWaveScratchFloats);
+  X.xq = X.xh + kXhF4;
+  X.wave = wave;
+  X.lane = lane;
+  X.par = 0;
+  X.lw = shadow ? wave : slot * WPI + (pos + WPI - 1) % WPI;  // periodic chain
+  X.rw = shadow ? wave : slot * WPI + (pos + 1) % WPI;
+  float *scratch = lds + kRingFloats + kSmallFloats + slot * kWaveScratchFloats;
+  float *s_st = scratch;  // n | u | E | x   (4 x 64)
+  float *s_F = scratch + 4 * 64;
+  float *s_rho = scratch + 5 * 64;
+  double *s_c = reinterpret_cast<double *>(scratch + 6 * 64);
+  const int b_raw = blockIdx.x * IPW + slot;
+  const bool live = b_raw < B;
+  const int64_t b = live ? b_raw : B - 1;  // a missing IC mirrors the last one and writes nothing
+  if (lead) {
+    const float *st0 = state0 + b * 3 * NX;
+    for (int i = lane; i < 3 * NX; i += 64) s_st[(i / NX) * 64 + i % NX] = st0[i];
+    if (lane < NX) {
+      s_st[3 * 64 + lane] = x[lane];
+      s_c[lane] = pc[lane];
+    }
+  }
+  __syncthreads();  // small weights + IC state visible (no DMA in flight yet)
+  const bool out = lead && live;
+  float *tj = (traj && out) ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
+  float *mt_out = (metrics && out) ? metrics + b * (int64_t)(T + 1) * HF_NUM_METRICS : nullptr;
+  float *ftj = (flux_traj && out) ? flux_traj + b * (int64_t)T * NX : nullptr;
+  auto emit = [&](int t) {  // lead wave
+    if (tj)
+      for (int i = lane; i < 3 * NX; i += 64) tj[(int64_t)t * 3 * NX + i] = s_st[(i / NX) * 64 + i % NX];
+    if (mt_out) {
+      MetricAcc m;
+      m.init();
+      if (lane < NX) m.add(s_st[lane], s_st[64 + lane], s_st[128 + lane]);
+      m.wave_reduce();
+      if (lane == 0) m.store(mt_out + t * HF_NUM_METRICS, NX);
+    }
+  };
+  if (lead) emit(0);
+  R.prime();
+  CoreF32::Feed F;
+  CoreF32::begin(R, F);
+  for (int t = 0; t < T; ++t) {
+    const float feat[1] = {s_st[g * 64 + 16 * pos + j]};
+    float ff[1], fb[1];
+    CoreF32::gnn_cells(W, S, R, F, feat, ff, fb, X);
+    if (!shadow && g == 0) s_F[16 * pos + j] = face_flux(ff[0], fb[0]);
+    lds_barrier();  // every wave's face fluxes in s_F
+    if (lead) {     // src/hybrid_solver.py:45-63, one cell per lane
+      float n_new = 0.f, u_new = 0.f;
+      if (lane < NX) {
+        const int im = lane == 0 ? NX - 1 : lane - 1;
+        const float Fv = s_F[lane];
+        n_new = continuity(s_st[lane], Fv, s_F[im], c);
+        u_new = velocity_hybrid(s_st[64 + lane], s_st[64 + im], s_st[128 + lane], c, dt);
+        s_rho[lane] = __fsub_rn(n_new, 1.0f);
+        if (ftj) ftj[(int64_t)t * NX + lane] = Fv;
+      }
+      wave_lds_sync();
+      if (lane < NX) {
+        const float E_new = poisson_cell(s_rho, s_c, lane, NX);
+        s_st[lane] = n_new;
+        s_st[64 + lane] = u_new;
+        s_st[128 + lane] = E_new;
+      }
+      wave_lds_sync();
+      emit(t + 1);
+    }
+    lds_barrier();  // new state visible to every wave
+  }
+  R.drain();
+  if (!out) return;
+  float *dst = state_final + b * 3 * NX;
+  for (int i = lane; i < 3 * NX; i += 64) dst[i] = s_st[(i / NX) * 64 + i % NX];
+}
+
+template <int WPI>
+hipError_t cells_launch(const ChainW &w, const float *state0, float *state_final, const float *x, const double *pc,
+                        int B, int T, float c, float dt, float *traj, float *flux_traj, float *metrics,
+                        hipStream_t s) {
+  constexpr int IPW = kWaves / WPI;
+  hipLaunchKernelGGL((chain_rollout_cells_kernel<WPI>), dim3((B + IPW - 1) / IPW), dim3(64 * kWaves), 0, s, w,
+                     state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// Whether the cell-split kernel beats the IC-per-wave kernel for B ICs of nx
+// cells: its workgroups carry 4/WPI ICs at about 1/WPI of the IC-per-wave
+// kernel's time per step (plus the exchanges), against 4 ICs per workgroup.
+bool chain_rollout_prefers_cells(const ChainW &w, int B, int nx) {
+  if (w.prec != kPrecF32 || B <= 0 || (nx != 32 && nx != 48 && nx != 64)) return false;
+  const int wpi = nx / 16, ipw = kWaves / wpi;
+  const int64_t cus = chain::resident_groups();
+  const int64_t wave_rounds = ((int64_t)B + 4 * cus - 1) / (4 * cus);
+  const int64_t cell_rounds = ((int64_t)B + ipw * cus - 1) / (ipw * cus);
+  return cell_rounds * (100 + 15 * wpi) < wave_rounds * 100 * wpi;
+}
+
+hipError_t launch_chain_rollout_cells(const ChainW &w, const float *state0, float *state_final, const float *x,
+                                      const double *pc, int B, int nx, int T, float c, float dt, float *traj,
+                                      float *flux_traj, float *metrics, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  switch (nx) {
+    case 32: return cells_launch<2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 48: return cells_launch<3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 64: return cells_launch<4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t launch_chain_flux_f32(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                  const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
@@ -245,9 +465,9 @@ hipError_t launch_chain_flux_f32(const ChainW &w, const float *nf, const float *
 hipError_t launch_chain_rollout_f32(const ChainW &w, const float *state0, float *state_final, const float *x,
                                     const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                     float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
-  // small batches: one IC per workgroup, output features split over its waves
-  if (ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_split(w, B))
-    return launch_chain_rollout_split(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, s);
+  // small batches: each IC spread over nx/16 waves (cell-split kernel)
+  if (ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx))
+    return launch_chain_rollout_cells(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, s);
   return chain::launch_rollout_core<CoreF32>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj,
                                              metrics, ex, s);
 }

@@ -51,7 +51,6 @@ __host__ __device__ inline int chain_chunk_bytes(int prec) { return prec == kPre
 
 struct ChainW {
   const void *stream;   // [chain_chunks][chunk]
-  const void *split;    // f32 only: per-wave streams of chain_split.hip (pack_chain_split), else null
   const float *win;     // [2][64][4]   input layer A fragments (f32; bf16-rounded in bf16 mode)
   const float *bin;     // [kH]
   const float *bl;      // [L][kH]
@@ -123,9 +122,9 @@ struct RolloutExtras {
 hipError_t launch_chain_rollout_f32(const ChainW &, const float *, float *, const float *, const double *, int, int,
                                     int, float, float, float *, float *, float *, const RolloutExtras &,
                                     hipStream_t);
-// Feature-split rollout for small batches (chain_split.hip; f32, nx in {16,32,48,64}, no classical twin).
-bool chain_rollout_prefers_split(const ChainW &, int B);
-hipError_t launch_chain_rollout_split(const ChainW &, const float *, float *, const float *, const double *, int,
+// Cell-split rollout for small batches (chain_f32.hip; f32, nx in {32,48,64}, no classical twin).
+bool chain_rollout_prefers_cells(const ChainW &, int B, int nx);
+hipError_t launch_chain_rollout_cells(const ChainW &, const float *, float *, const float *, const double *, int,
                                       int, int, float, float, float *, float *, float *, hipStream_t);
 hipError_t launch_chain_rollout_k32(const ChainW &, const float *, float *, const float *, const double *, int, int,
                                     int, float, float, float *, float *, float *, const RolloutExtras &,

@@ -281,8 +281,8 @@ def test_full_batch_properties(hf):
     sub = [0, 1, 777, 2048, 4095]
     alone = solver.run_batch(ics[sub], 30, traj=False)["final"]
     assert torch.equal(alone, a["final"][sub])                       # batch invariant
-    # BASELINE config 2 size: 256 ICs take the feature-split kernel
-    # (chain_split.hip), 4096 the IC-per-wave kernel; results are bit-identical
+    # BASELINE config 2 size: 256 ICs take the cell-split kernel
+    # (chain_f32.hip), 4096 the IC-per-wave kernel; results are bit-identical
     cfg2 = solver.run_batch(ics[:256], 30, traj=False, metrics=True)
     assert torch.equal(cfg2["final"], a["final"][:256])
     assert torch.equal(cfg2["metrics"], a["metrics"][:256])
@@ -293,6 +293,26 @@ def test_full_batch_properties(hf):
     pick = np.random.RandomState(0).choice(4096, 24, replace=False)
     want, _ = O.hybrid_run(O.params_from(w), O.Grid(64), ics[pick].cpu().numpy(), 30)
     close(a["final"][pick].cpu().numpy(), want[:, -1], ROLL_ATOL, ROLL_RTOL)
+
+
+@pytest.mark.parametrize("nx", [32, 48, 64])
+def test_cell_split_kernel_bitwise(hf, nx):
+    """Small batches run on the cell-split kernel (an IC over nx/16 waves,
+    boundary columns exchanged through LDS), large ones on the IC-per-wave
+    kernel: every output, every step, bit-identical.  B=5 also leaves a
+    workgroup half empty at nx=32 (2 ICs per workgroup) and runs the shadow
+    wave at nx=48."""
+    w = weights("W1_r1")
+    G = O.Grid(nx, dt=5e-3 * min(1.0, nx / 64.0))
+    solver = hf.HybridSolver(w, radius=1, nx=nx, dt=G.dt, device=DEV)
+    big = solver.baseline.initial_conditions(list(range(2000, 2000 + 3072)), as_tensor=True)
+    ref = solver.run_batch(big, 12, traj=True, flux=True, metrics=True)
+    for sub in ([0, 1, 2, 3, 4], list(range(100, 356))):
+        got = solver.run_batch(big[sub], 12, traj=True, flux=True, metrics=True)
+        for k in ("final", "traj", "flux", "metrics"):
+            assert torch.equal(got[k], ref[k][sub]), (nx, len(sub), k)
+    want, _ = O.hybrid_run(O.params_from(w), G, big[:5].cpu().numpy(), 12)
+    close(solver.run_batch(big[:5], 12)["traj"].cpu().numpy(), want, ROLL_ATOL, ROLL_RTOL)
 
 
 # ------------------------------------------------- fused classical comparison
