@@ -421,6 +421,59 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
   for (int i = lane; i < 3 * NX; i += 64) dst[i] = s_st[(i / NX) * 64 + i % NX];
 }
 
+// FluxGNN.forward on B chains of 16*WPI cells, cell-split as above (the
+// small-batch counterpart of chain_flux_kernel<CoreF32, MT, true>, bit-identical to it).
+template <int WPI>
+__global__ __launch_bounds__(256, 1) void chain_flux_cells_kernel(ChainW W, const float *__restrict__ nf,
+                                                                  const float *__restrict__ state, int64_t ld_state,
+                                                                  const float *__restrict__ x, int B,
+                                                                  float *__restrict__ fe, float *__restrict__ ff) {
+  constexpr int NX = 16 * WPI;
+  constexpr int IPW = kWaves / WPI;
+  constexpr int kRingFloats = kRingSlots * CoreF32::kChunkFloats;
+  __shared__ f4 lds4[kCellsLds / 4];
+  float *lds = reinterpret_cast<float *>(lds4);
+  const Small S = stage_small(W, lds + kRingFloats);
+  auto R = make_ring<CoreF32>(W, lds);
+  const int wave = R.wave, lane = R.lane, j = lane & 15, g = lane >> 4;
+  const bool shadow = wave >= IPW * WPI;
+  const int slot = shadow ? 0 : wave / WPI, pos = shadow ? 0 : wave % WPI;
+  CellHalo X;
+  X.xh = reinterpret_cast<f4 *>(lds + kRingFloats + kSmallFloats + kWaves * kWaveScratchFloats);
+  X.xq = X.xh + kXhF4;
+  X.wave = wave;
+  X.lane = lane;
+  X.par = 0;
+  X.lw = shadow ? wave : slot * WPI + (pos + WPI - 1) % WPI;
+  X.rw = shadow ? wave : slot * WPI + (pos + 1) % WPI;
+  const int b_raw = blockIdx.x * IPW + slot;
+  const bool out = !shadow && b_raw < B;
+  const int64_t b = b_raw < B ? b_raw : B - 1;
+  const int cell = 16 * pos + j;
+  const float feat[1] = {nf ? nf[(b * NX + cell) * kIn + g]
+                            : (g < 3 ? state[b * ld_state + (int64_t)g * NX + cell] : x[cell])};
+  __syncthreads();  // small weights staged (no DMA in flight yet)
+  R.prime();
+  CoreF32::Feed F;
+  CoreF32::begin(R, F);
+  float f_fwd[1], f_bwd[1];
+  CoreF32::gnn_cells(W, S, R, F, feat, f_fwd, f_bwd, X);
+  R.drain();
+  if (!out) return;
+  if (fe && g == 0) fe[b * 2 * NX + cell] = f_fwd[0];
+  if (fe && g == 1) fe[b * 2 * NX + NX + cell] = f_bwd[0];
+  if (ff && g == 2) ff[b * NX + cell] = face_flux(f_fwd[0], f_bwd[0]);
+}
+
+template <int WPI>
+hipError_t flux_cells_launch(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
+                             int B, float *fe, float *ff, hipStream_t s) {
+  constexpr int IPW = kWaves / WPI;
+  hipLaunchKernelGGL((chain_flux_cells_kernel<WPI>), dim3((B + IPW - 1) / IPW), dim3(64 * kWaves), 0, s, w, nf,
+                     state, ld_state, x, B, fe, ff);
+  return hipGetLastError();
+}
+
 template <int WPI>
 hipError_t cells_launch(const ChainW &w, const float *state0, float *state_final, const float *x, const double *pc,
                         int B, int T, float c, float dt, float *traj, float *flux_traj, float *metrics,
@@ -459,6 +512,15 @@ hipError_t launch_chain_rollout_cells(const ChainW &w, const float *state0, floa
 
 hipError_t launch_chain_flux_f32(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                  const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
+  // small batches: each chain spread over nx/16 waves, as the rollout
+  if (chain_rollout_prefers_cells(w, B, nx)) {
+    switch (nx) {
+      case 32: return flux_cells_launch<2>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 48: return flux_cells_launch<3>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 64: return flux_cells_launch<4>(w, nf, state, ld_state, x, B, fe, ff, s);
+      default: break;
+    }
+  }
   return chain::launch_flux_core<CoreF32>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 

@@ -313,6 +313,15 @@ def test_cell_split_kernel_bitwise(hf, nx):
             assert torch.equal(got[k], ref[k][sub]), (nx, len(sub), k)
     want, _ = O.hybrid_run(O.params_from(w), G, big[:5].cpu().numpy(), 12)
     close(solver.run_batch(big[:5], 12)["traj"].cpu().numpy(), want, ROLL_ATOL, ROLL_RTOL)
+    # FluxGNN.forward on a batched chain graph takes the same split at small B
+    ics = big.cpu().numpy()
+    with torch.no_grad():
+        nf, ei = hf.build_chain_graph_batch(ics, G.x, DEV)
+        fe_big = solver.model(nf, ei).reshape(len(ics), 2 * nx)
+        nf, ei = hf.build_chain_graph_batch(ics[:5], G.x, DEV)
+        fe_small = solver.model(nf, ei).reshape(5, 2 * nx)
+    assert torch.equal(fe_small, fe_big[:5])
+    close(fe_small.cpu().numpy(), O.hybrid_flux_edge(O.params_from(w), G, ics[:5]), 2e-6)
 
 
 # ------------------------------------------------- fused classical comparison
