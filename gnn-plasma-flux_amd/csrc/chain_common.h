@@ -365,8 +365,9 @@ __device__ __forceinline__ void input_layer(const Small &S, int lane, const floa
 // FluxGNN.forward on B chains; items = (IC, window), one wave per item,
 // 4 items per workgroup.
 //  EXACT: nx == 16*MT, the wave owns the whole periodic IC, every face exact.
-//  else : MT == 4 window of 64 cells starting at w*55-4 (mod nx); faces
-//         [4,58] of the window (55 per window) are exact, the rest discarded.
+//  else : MT == 4 window of 64 cells starting at w*(63-2L)-L (mod nx); faces
+//         [L, 62-L] of the window (63 - 2L per window, L = update layers) are
+//         exact, the rest discarded.
 template <class Core, int MT, bool EXACT>
 __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const float *__restrict__ nf,
                                                             const float *__restrict__ state,
@@ -387,6 +388,10 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
   Core::begin(R, F);
   // Persistent over groups of 4 items: the weight stream keeps flowing from one
   // group's forward pass into the next, so the ring fill is paid once per workgroup.
+  // window halo: after L message-passing layers the L cells at each window
+  // edge (and the readout of the faces between them) have seen the window's
+  // artificial wrap; faces [L, 62 - L] of a 64-cell window are exact
+  const int halo = W.layers, win_faces = win_faces_of(W.layers);
   const int64_t groups = (items + kWaves - 1) / kWaves;
   for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
     const int64_t item_raw = grp * kWaves + R.wave;
@@ -394,7 +399,7 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
     const int64_t item = live ? item_raw : items - 1;  // idle waves mirror a real item, write nothing
     const int64_t b = item / nwin;
     const int w = (int)(item - b * nwin);
-    const int start = EXACT ? 0 : w * kWinFaces - kWinHalo;
+    const int start = EXACT ? 0 : w * win_faces - halo;
     float feat[MT];
     int cell[MT];
 #pragma unroll
@@ -414,8 +419,8 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
         int face = cell[mt];
         bool ok = true;
         if (!EXACT) {
-          face = w * kWinFaces + (wc - kWinHalo);
-          ok = wc >= kWinHalo && wc < kWinHalo + kWinFaces && face < nx;
+          face = w * win_faces + (wc - halo);
+          ok = wc >= halo && wc < halo + win_faces && face < nx;
         }
         if (!ok) continue;
         if (fe && g == 0) fe[b * 2 * nx + face] = f_fwd[mt];
@@ -592,7 +597,7 @@ hipError_t launch_flux_core(const ChainW &w, const float *nf, const float *state
     case 48: return flux_launch<Core, 3, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
     case 64: return flux_launch<Core, 4, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
     default: {
-      const int nwin = (nx + kWinFaces - 1) / kWinFaces;
+      const int nwin = (nx + win_faces_of(w.layers) - 1) / win_faces_of(w.layers);
       return flux_launch<Core, 4, false>(w, nf, state, ld_state, x, nx, nwin, (int64_t)B * nwin, fe, ff, s);
     }
   }

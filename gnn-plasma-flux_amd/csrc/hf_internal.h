@@ -17,11 +17,12 @@ constexpr int kNT = kH / 16;
 constexpr int kKS = kH / 4;
 
 // Window geometry of the halo-recompute chain kernel (any nx): a wave owns
-// 64 consecutive cells; L=4 layers + the 1-hop edge readout invalidate 4
-// cells at each window edge, so faces [4, 58] of the window are exact.
+// 64 consecutive cells; L update layers invalidate L cells at each window
+// edge and the readout needs both cells of a face, so faces [L, 62 - L] of
+// the window are exact.
 constexpr int kWinCells = 64;
-constexpr int kWinHalo = 4;
-constexpr int kWinFaces = kWinCells - 2 * kWinHalo - 1;  // 55
+// exact faces per window for L update layers: [L, 62 - L] (55 at L = 4, 47 at L = 8)
+__host__ __device__ inline int win_faces_of(int layers) { return kWinCells - 2 * layers - 1; }
 
 // Packed weights (device) for the chain kernels; see capi.cpp pack_chain_*
 // for the exact index maps.  The big matrices form ONE stream of chunks,

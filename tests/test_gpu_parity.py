@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import golden, rand_sd
 from oracle import hybrid_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -322,6 +322,26 @@ def test_cell_split_kernel_bitwise(hf, nx):
         fe_small = solver.model(nf, ei).reshape(5, 2 * nx)
     assert torch.equal(fe_small, fe_big[:5])
     close(fe_small.cpu().numpy(), O.hybrid_flux_edge(O.params_from(w), G, ics[:5]), 2e-6)
+
+
+@pytest.mark.parametrize("precision,atol", [("f32", 2e-6), ("f16x3", 2e-6), ("bf16", 2e-2)])
+@pytest.mark.parametrize("layers,nx", [(0, 100), (2, 100), (6, 100), (8, 200), (8, 64)])
+def test_flux_any_layer_count(hf, layers, nx, precision, atol):
+    """The windowed kernel's halo grows with the layer count (faces [L, 62-L]
+    of a 64-cell window are exact): FluxGNN(4, 128, L) for L up to the chain
+    kernels' limit of 8, at nx that take the windowed and the exact kernels."""
+    sd = rand_sd(layers, 70 + layers)
+    G = O.Grid(nx, dt=5e-3)
+    ics = np.stack([O.initial_condition(G, s) for s in (21, 22, 23)])
+    ref_sd = O.bf16_weights(sd) if precision == "bf16" else sd
+    want = O.hybrid_flux_edge(O.params_from(ref_sd), G, ics)
+    m = hf.FluxGNN(4, 128, layers, precision=precision)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to(DEV)
+    nf, ei = hf.build_chain_graph_batch(ics, G.x, DEV)
+    with torch.no_grad():
+        fe = m(nf, ei).cpu().numpy().reshape(3, 2 * nx)
+    close(fe, want, atol)
 
 
 # ------------------------------------------------- fused classical comparison

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import golden, rand_sd
 from oracle import hybrid_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -104,20 +104,6 @@ def test_bf16_vs_bf16_weight_oracle(hf, nx):
     err_f = close(fe, fe_want[:, 0], 2e-2)
     err_s = close(solver.run_batch(ics, 10)["traj"].cpu().numpy(), want, 2e-2)
     print(f"bf16 nx={nx}: max flux err {err_f:.2e}, 10-step state err {err_s:.2e}")
-
-
-def rand_sd(layers, seed):
-    """Random FluxGNN(4, 128, layers) state dict (reference keys, src/flux_gnn.py:17-38)."""
-    g = np.random.default_rng(seed)
-    sd = {"input_mlp.0.weight": g.normal(0, 0.5, (128, 4)), "input_mlp.0.bias": g.normal(0, 0.1, 128)}
-    for l in range(layers):
-        sd[f"update_mlps.{l}.0.weight"] = g.normal(0, 1 / 16, (128, 256))
-        sd[f"update_mlps.{l}.0.bias"] = g.normal(0, 0.1, 128)
-    sd["edge_mlp.0.weight"] = g.normal(0, 1 / 16, (128, 256))
-    sd["edge_mlp.0.bias"] = g.normal(0, 0.1, 128)
-    sd["edge_mlp.2.weight"] = g.normal(0, 1 / 11, (1, 128))
-    sd["edge_mlp.2.bias"] = g.normal(0, 0.1, 1)
-    return {k: np.asarray(v, np.float32) for k, v in sd.items()}
 
 
 @pytest.mark.parametrize("layers", [0, 1, 3])
