@@ -59,12 +59,21 @@ __device__ __forceinline__ void interleave() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-struct CoreBF16 {
+// NW = waves per workgroup sharing the weight ring; the kernels use NW = 4
+// (one wave per SIMD, up to 64 cells per wave).  NW = 8 (two waves per SIMD
+// at 191 registers, 32-cell windows) was measured for the windowed flux
+// kernel: per FLOP 7 % faster, but 32-cell windows recompute 41 % halo
+// against 19 % at 64 cells, so cfg4 ran at 2.18 M IC-steps/s against 2.41 M.
+template <int NW>
+struct CoreBF16T {
+  static constexpr int kNW = NW;
+  static constexpr int kWinMT = NW == 8 ? 2 : 4;  // m-tiles per wave in the windowed flux kernel
+  static constexpr int kParkMT = kWinMT;          // largest MT the park holds
   static constexpr int kChunkFloats = 2048;  // 8 KiB = 2 units of 4 fragments
   static constexpr int kKB = kH / 32;        // k-blocks per 128-wide operand
-  // parked fragments of k-blocks 0..2: [kb 3][h|agg 2][mt 4][lane 64][4 dwords]
-  static constexpr int kParkFloats = 3 * 2 * 4 * 64 * 4;
-  using R_t = Ring<kChunkFloats>;
+  // parked fragments of k-blocks 0..2: [kb 3][h|agg 2][mt kParkMT][lane 64][4 dwords]
+  static constexpr int kParkFloats = 3 * 2 * kParkMT * 64 * 4;
+  using R_t = Ring<kChunkFloats, NW>;
 
   template <int MT>
   struct Acts {
@@ -97,7 +106,7 @@ struct CoreBF16 {
   }
 
   static __device__ __forceinline__ float *park_at(float *park, int kb, int ha, int mt, int lane) {
-    return park + (((kb * 2 + ha) * 4 + mt) * 64 + lane) * 4;
+    return park + (((kb * 2 + ha) * kParkMT + mt) * 64 + lane) * 4;
   }
 
   // Dword K (tile t = K>>1, rows 2(K&1), 2(K&1)+1) of the k-block fragments
@@ -407,13 +416,13 @@ struct CoreBF16 {
 
 hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                   const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
-  return chain::launch_flux_core<CoreBF16>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  return chain::launch_flux_core<CoreBF16T<4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float *state_final, const float *x,
                                      const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                      float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
-  return chain::launch_rollout_core<CoreBF16>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj,
+  return chain::launch_rollout_core<CoreBF16T<4>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj,
                                               metrics, ex, s);
 }
 

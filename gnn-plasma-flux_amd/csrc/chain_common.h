@@ -181,10 +181,11 @@ __device__ __forceinline__ Small stage_small(const ChainW &W, float *s) {
 }
 
 // ----------------------------------------------------------------- the ring
-// CF = chunk size in floats (2048 = 8 KiB or 4096 = 16 KiB).
-template <int CF>
+// CF = chunk size in floats (2048 = 8 KiB or 4096 = 16 KiB); NW = waves sharing the ring.
+template <int CF, int NW = kWaves>
 struct Ring {
-  static constexpr int kPerWave = CF / (kWaves * 256);  // 1 KiB DMA instructions per wave per chunk
+  static constexpr int kPerWave = CF / (NW * 256);  // 1 KiB DMA instructions per wave per chunk
+  static_assert(kPerWave == 1 || kPerWave == 2 || kPerWave == 4, "ring chunk split over the waves");
   __amdgpu_buffer_rsrc_t rsrc;  // packed weight stream (global)
   int lane_off;                 // lane * 16 bytes (the only per-lane address term)
   float *lds;                   // 4 slots
@@ -235,7 +236,9 @@ struct Ring {
 #elif defined(HF_DIAG_NOBAR)  // timing diagnostic only: results are wrong
     asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
 #else
-    if constexpr (kPerWave == 2)
+    if constexpr (kPerWave == 1)
+      asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kPerWave == 2)
       asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -256,8 +259,8 @@ struct Ring {
 };
 
 template <class Core>
-__device__ __forceinline__ Ring<Core::kChunkFloats> make_ring(const ChainW &W, float *ring_lds) {
-  Ring<Core::kChunkFloats> R;
+__device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW> make_ring(const ChainW &W, float *ring_lds) {
+  Ring<Core::kChunkFloats, Core::kNW> R;
   R.chunks = chain_chunks(W.layers, W.prec);
   R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0,
                                              R.chunks * Core::kChunkFloats * 4, 0x00020000);
@@ -270,15 +273,16 @@ __device__ __forceinline__ Ring<Core::kChunkFloats> make_ring(const ChainW &W, f
   return R;
 }
 
-// LDS per workgroup: ring | small weights | per-wave scratch | per-wave park
-// (Core::kParkFloats: activations a core spills to LDS instead of VGPRs).
-template <class Core>
+// LDS per workgroup: ring | small weights | per-wave scratch (rollouts only) |
+// per-wave park (Core::kParkFloats: activations a core spills to LDS instead of VGPRs).
+template <class Core, bool SCRATCH = true>
 constexpr int lds_floats() {
-  return kRingSlots * Core::kChunkFloats + kSmallFloats + kWaves * (kWaveScratchFloats + Core::kParkFloats);
+  return kRingSlots * Core::kChunkFloats + kSmallFloats +
+         Core::kNW * ((SCRATCH ? kWaveScratchFloats : 0) + Core::kParkFloats);
 }
-template <class Core>
+template <class Core, bool SCRATCH = true>
 __device__ __forceinline__ float *park_of(float *lds, int wave) {
-  return lds + kRingSlots * Core::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats +
+  return lds + kRingSlots * Core::kChunkFloats + kSmallFloats + (SCRATCH ? Core::kNW * kWaveScratchFloats : 0) +
          wave * Core::kParkFloats;
 }
 
@@ -363,13 +367,13 @@ __device__ __forceinline__ void input_layer(const Small &S, int lane, const floa
 
 // ---------------------------------------------------------------------------
 // FluxGNN.forward on B chains; items = (IC, window), one wave per item,
-// 4 items per workgroup.
+// Core::kNW items per workgroup.
 //  EXACT: nx == 16*MT, the wave owns the whole periodic IC, every face exact.
-//  else : MT == 4 window of 64 cells starting at w*(63-2L)-L (mod nx); faces
-//         [L, 62-L] of the window (63 - 2L per window, L = update layers) are
-//         exact, the rest discarded.
+//  else : window of 16*MT cells starting at w*(16MT-1-2L)-L (mod nx); faces
+//         [L, 16MT-2-L] of the window (16MT - 1 - 2L per window, L = update
+//         layers) are exact, the rest discarded.
 template <class Core, int MT, bool EXACT>
-__global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const float *__restrict__ nf,
+__global__ __launch_bounds__(64 * Core::kNW, 1) void chain_flux_kernel(ChainW W, const float *__restrict__ nf,
                                                             const float *__restrict__ state,
                                                             int64_t ld_state,
                                                             const float *__restrict__ x, int nx,
@@ -377,7 +381,7 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
                                                             float *__restrict__ fe,
                                                             float *__restrict__ ff) {
   constexpr int kRingFloats = kRingSlots * Core::kChunkFloats;
-  __shared__ f4 lds4[lds_floats<Core>() / 4];
+  __shared__ f4 lds4[lds_floats<Core, false>() / 4];
   float *lds = reinterpret_cast<float *>(lds4);
   const Small S = stage_small(W, lds + kRingFloats);
   auto R = make_ring<Core>(W, lds);
@@ -391,10 +395,10 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
   // window halo: after L message-passing layers the L cells at each window
   // edge (and the readout of the faces between them) have seen the window's
   // artificial wrap; faces [L, 62 - L] of a 64-cell window are exact
-  const int halo = W.layers, win_faces = win_faces_of(W.layers);
-  const int64_t groups = (items + kWaves - 1) / kWaves;
+  const int halo = W.layers, win_faces = win_faces_of(W.layers, 16 * MT);
+  const int64_t groups = (items + Core::kNW - 1) / Core::kNW;
   for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
-    const int64_t item_raw = grp * kWaves + R.wave;
+    const int64_t item_raw = grp * Core::kNW + R.wave;
     const bool live = item_raw < items;
     const int64_t item = live ? item_raw : items - 1;  // idle waves mirror a real item, write nothing
     const int64_t b = item / nwin;
@@ -411,7 +415,7 @@ __global__ __launch_bounds__(256, 1) void chain_flux_kernel(ChainW W, const floa
                     : (g < 3 ? state[b * ld_state + (int64_t)g * nx + cidx] : x[cidx]);
     }
     float f_fwd[MT], f_bwd[MT];
-    Core::template gnn<MT>(W, S, R, F, park_of<Core>(lds, R.wave), feat, f_fwd, f_bwd);
+    Core::template gnn<MT>(W, S, R, F, park_of<Core, false>(lds, R.wave), feat, f_fwd, f_bwd);
     if (live) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -459,6 +463,7 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
   float *s_rhoc = scratch + 12 * 64;
   float *park = park_of<Core>(lds, R.wave);
   const bool twin = ex.mse != nullptr;
+  static_assert(Core::kNW == kWaves, "rollout: 4 waves, one IC each");
   const int b_raw = blockIdx.x * kWaves + R.wave;
   const bool live = b_raw < B;
   const int64_t b = live ? b_raw : B - 1;
@@ -580,11 +585,22 @@ inline int resident_groups() {
 template <class Core, int MT, bool EXACT>
 hipError_t flux_launch(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
                        int nx, int nwin, int64_t items, float *fe, float *ff, hipStream_t s) {
-  const int64_t groups = (items + kWaves - 1) / kWaves;
+  const int64_t groups = (items + Core::kNW - 1) / Core::kNW;
   const int64_t blocks = groups < resident_groups() ? groups : resident_groups();  // persistent: 1 per CU
-  hipLaunchKernelGGL((chain_flux_kernel<Core, MT, EXACT>), dim3((unsigned)blocks), dim3(64 * kWaves), 0, s, w,
-                     nf, state, ld_state, x, nx, nwin, items, fe, ff);
+  hipLaunchKernelGGL((chain_flux_kernel<Core, MT, EXACT>), dim3((unsigned)blocks), dim3(64 * Core::kNW), 0, s,
+                     w, nf, state, ld_state, x, nx, nwin, items, fe, ff);
   return hipGetLastError();
+}
+
+// Windowed flux for any nx: windows of 16*Core::kWinMT cells.
+template <class Core>
+hipError_t launch_flux_windowed(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
+                                const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  constexpr int WMT = Core::kWinMT;
+  const int faces = win_faces_of(w.layers, 16 * WMT);
+  const int nwin = (nx + faces - 1) / faces;
+  return flux_launch<Core, WMT, false>(w, nf, state, ld_state, x, nx, nwin, (int64_t)B * nwin, fe, ff, s);
 }
 
 template <class Core>
@@ -596,10 +612,7 @@ hipError_t launch_flux_core(const ChainW &w, const float *nf, const float *state
     case 32: return flux_launch<Core, 2, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
     case 48: return flux_launch<Core, 3, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
     case 64: return flux_launch<Core, 4, true>(w, nf, state, ld_state, x, nx, 1, B, fe, ff, s);
-    default: {
-      const int nwin = (nx + win_faces_of(w.layers) - 1) / win_faces_of(w.layers);
-      return flux_launch<Core, 4, false>(w, nf, state, ld_state, x, nx, nwin, (int64_t)B * nwin, fe, ff, s);
-    }
+    default: return launch_flux_windowed<Core>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
   }
 }
 

@@ -22,6 +22,8 @@ namespace {
 using namespace chain;
 
 struct CoreF32 {
+  static constexpr int kNW = kWaves;   // waves sharing the weight ring
+  static constexpr int kWinMT = 4;     // m-tiles per wave in the windowed flux kernel
   static constexpr int kChunkFloats = 2048;  // 8 KiB: 4 units of 2 KiB (2 ds_read_b128 per lane)
   static constexpr int kParkFloats = 0;
   using R_t = Ring<kChunkFloats>;

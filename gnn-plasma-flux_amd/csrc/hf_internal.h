@@ -21,8 +21,9 @@ constexpr int kKS = kH / 4;
 // edge and the readout needs both cells of a face, so faces [L, 62 - L] of
 // the window are exact.
 constexpr int kWinCells = 64;
-// exact faces per window for L update layers: [L, 62 - L] (55 at L = 4, 47 at L = 8)
-__host__ __device__ inline int win_faces_of(int layers) { return kWinCells - 2 * layers - 1; }
+// exact faces per window of `cells` cells for L update layers: [L, cells - 2 - L]
+// (55 at 64 cells and L = 4, 47 at L = 8)
+__host__ __device__ inline int win_faces_of(int layers, int cells = kWinCells) { return cells - 2 * layers - 1; }
 
 // Packed weights (device) for the chain kernels; see capi.cpp pack_chain_*
 // for the exact index maps.  The big matrices form ONE stream of chunks,
