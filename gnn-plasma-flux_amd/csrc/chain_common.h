@@ -261,7 +261,8 @@ struct Ring {
 template <class Core>
 __device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW> make_ring(const ChainW &W, float *ring_lds) {
   Ring<Core::kChunkFloats, Core::kNW> R;
-  R.chunks = chain_chunks(W.layers, W.prec);
+  // the packed stream is chain_chunks() chunks of chain_chunk_bytes(); a core may move it in larger chunks
+  R.chunks = chain_chunks(W.layers, W.prec) * chain_chunk_bytes(W.prec) / (Core::kChunkFloats * 4);
   R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0,
                                              R.chunks * Core::kChunkFloats * 4, 0x00020000);
   R.lane_off = (threadIdx.x & 63) * 16;

@@ -24,9 +24,12 @@ using namespace chain;
 struct CoreF32 {
   static constexpr int kNW = kWaves;   // waves sharing the weight ring
   static constexpr int kWinMT = 4;     // m-tiles per wave in the windowed flux kernel
-  static constexpr int kChunkFloats = 2048;  // 8 KiB: 4 units of 2 KiB (2 ds_read_b128 per lane)
+  // units per ring chunk: 4 (8 KiB chunks); 8 (16 KiB, half the barriers)
+  // measured no faster, for the IC-per-wave and the cell-split kernels alike
+  static constexpr int kUPC = 4;
+  static constexpr int kChunkFloats = 512 * kUPC;  // 4 units of 2 KiB (2 ds_read_b128 per lane)
   static constexpr int kParkFloats = 0;
-  using R_t = Ring<kChunkFloats>;
+  using R_t = Ring<kChunkFloats, kNW>;
 
   // Register-prefetched weight feed.  A chunk is 4 units; unit u is the lane's
   // fragments 2u, 2u+1 and feeds 32 MFMAs (one update k-step, or four readout
@@ -51,9 +54,9 @@ struct CoreF32 {
   static __device__ __forceinline__ void take(R_t &R, Feed &F, f4 (&a)[2]) {
     a[0] = F.cur[0];
     a[1] = F.cur[1];
-    if constexpr (U == 3) F.slot = R.next();
+    if constexpr (U == kUPC - 1) F.slot = R.next();
 #ifndef HF_DIAG_NODS  // timing diagnostic only: results are wrong
-    load_unit(F, (U + 1) & 3, R.lane);
+    load_unit(F, (U + 1) % kUPC, R.lane);
 #endif
   }
   // B operand of flat k-step KS (0..63) of an update layer: k-steps 0..31 read
@@ -89,7 +92,7 @@ struct CoreF32 {
   static __device__ __forceinline__ void layer_step(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
                                                     f4 (&acc)[MT][kNT], const H &X) {
     f4 a[2];
-    take<KS & 3>(R, F, a);
+    take<KS % kUPC>(R, F, a);
     float bn[MT];
     if constexpr (KS + 1 < 2 * kKS) b_operand<MT, KS + 1>(h, bn, X);
 #pragma unroll
@@ -127,7 +130,7 @@ struct CoreF32 {
   static __device__ __forceinline__ void readout_unit(R_t &R, Feed &F, const f4 (&h)[MT][kNT], f4 (&P)[MT],
                                                       f4 (&Q)[MT]) {
     f4 a[2];
-    take<U>(R, F, a);
+    take<(4 * HH + U) % kUPC>(R, F, a);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s = 16 * HH + 4 * U + i;
