@@ -64,16 +64,21 @@ __device__ __forceinline__ void interleave() {
 // at 191 registers, 32-cell windows) was measured for the windowed flux
 // kernel: per FLOP 7 % faster, but 32-cell windows recompute 41 % halo
 // against 19 % at 64 cells, so cfg4 ran at 2.18 M IC-steps/s against 2.41 M.
-template <int NW>
+// UPC = units (4 fragments, 4 KiB) per ring chunk: 2 (8 KiB chunks, 4 slots)
+// or 4 (16 KiB chunks, 3 slots: half the ring barriers, +16 KiB of LDS, which
+// the windowed flux kernel has and the rollout, with its per-IC scratch, has not).
+template <int NW, int UPC = 2>
 struct CoreBF16T {
   static constexpr int kNW = NW;
+  static constexpr int kUPC = UPC;
+  static constexpr int kSlots = UPC == 4 ? 3 : 4;
   static constexpr int kWinMT = NW == 8 ? 2 : 4;  // m-tiles per wave in the windowed flux kernel
   static constexpr int kParkMT = kWinMT;          // largest MT the park holds
-  static constexpr int kChunkFloats = 2048;  // 8 KiB = 2 units of 4 fragments
+  static constexpr int kChunkFloats = 1024 * UPC;
   static constexpr int kKB = kH / 32;        // k-blocks per 128-wide operand
   // parked fragments of k-blocks 0..2: [kb 3][h|agg 2][mt kParkMT][lane 64][4 dwords]
   static constexpr int kParkFloats = 3 * 2 * kParkMT * 64 * 4;
-  using R_t = Ring<kChunkFloats, NW>;
+  using R_t = Ring<kChunkFloats, NW, kSlots>;
 
   template <int MT>
   struct Acts {
@@ -99,9 +104,9 @@ struct CoreBF16T {
   static __device__ __forceinline__ void take(R_t &R, Feed &F, u4 (&w)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = F.cur[i];
-    if constexpr (U == 1) F.slot = R.next();
+    if constexpr (U == UPC - 1) F.slot = R.next();
 #ifndef HF_DIAG_NODS  // timing diagnostic only: results are wrong
-    load_unit(F, (U + 1) & 1, R.lane);
+    load_unit(F, (U + 1) % UPC, R.lane);
 #endif
   }
 
@@ -171,16 +176,16 @@ struct CoreBF16T {
                                                         float *park, int lane) {
     init_pair<MT>(bias, q, g4, acc);
     u4 nh[MT], na[MT];
-    unit<MT, 0, 0>(R, F, X, acc);
+    unit<MT, 0, 0 % UPC>(R, F, X, acc);
     piece<MT, 0, true>(prev, nh, na);
     interleave<4 * MT, 2>();
-    unit<MT, 1, 1>(R, F, X, acc);
+    unit<MT, 1, 1 % UPC>(R, F, X, acc);
     piece<MT, 1, true>(prev, nh, na);
     interleave<4 * MT, 2>();
-    unit<MT, 2, 0>(R, F, X, acc);
+    unit<MT, 2, 2 % UPC>(R, F, X, acc);
     piece<MT, 2, true>(prev, nh, na);
     interleave<4 * MT, 2>();
-    unit<MT, 3, 1>(R, F, X, acc);
+    unit<MT, 3, 3 % UPC>(R, F, X, acc);
     piece<MT, 3, true>(prev, nh, na);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -207,14 +212,14 @@ struct CoreBF16T {
       }
     init_pair<MT>(bias, 0, g4, acc);
     u4 nh[MT], na[MT];
-    unit<MT, 0, 0>(R, F, X, acc);
+    unit<MT, 0, 0 % UPC>(R, F, X, acc);
     piece<MT, 0, true>(pend, nh, na);
     piece<MT, 1, true>(pend, nh, na);
     interleave<4 * MT, 4>();
-    unit<MT, 1, 1>(R, F, X, acc);
+    unit<MT, 1, 1 % UPC>(R, F, X, acc);
     piece<MT, 2, true>(pend, nh, na);
     interleave<4 * MT, 2>();
-    unit<MT, 2, 0>(R, F, X, acc);
+    unit<MT, 2, 2 % UPC>(R, F, X, acc);
     piece<MT, 3, true>(pend, nh, na);
     interleave<4 * MT, 2>();
 #pragma unroll
@@ -222,7 +227,7 @@ struct CoreBF16T {
       X.h[mt][3] = nh[mt];
       X.a[mt][3] = na[mt];
     }
-    unit<MT, 3, 1>(R, F, X, acc);
+    unit<MT, 3, 3 % UPC>(R, F, X, acc);
     interleave<4 * MT, 0>();
   }
 
@@ -231,13 +236,13 @@ struct CoreBF16T {
   static __device__ __forceinline__ void pair0_first(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
                                                      f4 (&acc)[MT][2]) {
     init_pair<MT>(bias, 0, g4, acc);
-    unit<MT, 0, 0>(R, F, X, acc);
+    unit<MT, 0, 0 % UPC>(R, F, X, acc);
     interleave<4 * MT, 0>();
-    unit<MT, 1, 1>(R, F, X, acc);
+    unit<MT, 1, 1 % UPC>(R, F, X, acc);
     interleave<4 * MT, 0>();
-    unit<MT, 2, 0>(R, F, X, acc);
+    unit<MT, 2, 2 % UPC>(R, F, X, acc);
     interleave<4 * MT, 0>();
-    unit<MT, 3, 1>(R, F, X, acc);
+    unit<MT, 3, 3 % UPC>(R, F, X, acc);
     interleave<4 * MT, 0>();
   }
 
@@ -251,11 +256,12 @@ struct CoreBF16T {
     pair_with_prev<MT>(R, F, X, bias, 3, g4, pend, acc2, park, lane);
   }
 
-  // Readout unit U of output tile ot: fragment i = 2*(kb - 2U) + (P|Q), kb = 2U, 2U+1.
-  template <int MT, int U>
+  // Readout unit U of output tile ot: fragment i = 2*(kb - 2U) + (P|Q), kb = 2U, 2U+1;
+  // T = its index in the ring chunk.
+  template <int MT, int U, int T>
   static __device__ __forceinline__ void ro_unit(R_t &R, Feed &F, const Acts<MT> &X, f4 (&P)[MT], f4 (&Q)[MT]) {
     u4 w[4];
-    take<U>(R, F, w);
+    take<T>(R, F, w);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kb = 2 * U + (i >> 1);
@@ -301,6 +307,28 @@ struct CoreBF16T {
     }
   }
 
+  // Readout tile ot >= 1 (ring indices T0, T0+1), with the epilogue of tile
+  // ot-1 (P, Q on entry; tile ot's on exit) spread over its two units.
+  template <int MT, int T0>
+  static __device__ __forceinline__ void ro_tile(R_t &R, Feed &F, const Acts<MT> &X, const Small &S, int ot,
+                                                 int g4, f4 (&P)[MT], f4 (&Q)[MT], float (&pf)[MT],
+                                                 float (&pb)[MT]) {
+    f4 Pn[MT], Qn[MT];
+    init_ro<MT>(S, ot, g4, Pn, Qn);
+    const f4 w2 = ldf4(S.w2 + 16 * (ot - 1) + g4);
+    ro_unit<MT, 0, T0>(R, F, X, Pn, Qn);
+    ro_piece<MT, 0>(P, Q, w2, pf, pb);
+    interleave<4 * MT, 3>();
+    ro_unit<MT, 1, T0 + 1>(R, F, X, Pn, Qn);
+    ro_piece<MT, 1>(P, Q, w2, pf, pb);
+    interleave<4 * MT, 3>();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      P[mt] = Pn[mt];
+      Q[mt] = Qn[mt];
+    }
+  }
+
   // Edge readout, P/Q split (src/flux_gnn.py:62-66), pipelined tile by tile.
   // The last layer's pair 3 (pend) is still to be activated: h of k-blocks
   // 0..2 comes from the park, k-block 3 is finished under the first readout unit.
@@ -320,7 +348,7 @@ struct CoreBF16T {
     init_ro<MT>(S, 0, g4, P, Q);
     {
       u4 nh[MT], na[MT];
-      ro_unit<MT, 0>(R, F, X, P, Q);
+      ro_unit<MT, 0, 0>(R, F, X, P, Q);
       piece<MT, 0, false>(pend, nh, na);
       piece<MT, 1, false>(pend, nh, na);
       piece<MT, 2, false>(pend, nh, na);
@@ -328,25 +356,16 @@ struct CoreBF16T {
       interleave<4 * MT, 3>();
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
-      ro_unit<MT, 1>(R, F, X, P, Q);
+      ro_unit<MT, 1, 1>(R, F, X, P, Q);
       interleave<4 * MT, 0>();
     }
-    for (int ot = 1; ot < kNT; ++ot) {
-      f4 Pn[MT], Qn[MT];
-      init_ro<MT>(S, ot, g4, Pn, Qn);
-      const f4 w2 = ldf4(S.w2 + 16 * (ot - 1) + g4);
-      ro_unit<MT, 0>(R, F, X, Pn, Qn);
-      ro_piece<MT, 0>(P, Q, w2, pf, pb);
-      interleave<4 * MT, 3>();
-      ro_unit<MT, 1>(R, F, X, Pn, Qn);
-      ro_piece<MT, 1>(P, Q, w2, pf, pb);
-      interleave<4 * MT, 3>();
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        P[mt] = Pn[mt];
-        Q[mt] = Qn[mt];
-      }
+    // tiles 1..7; an odd tile starts mid-chunk when a chunk holds two tiles
+    constexpr int kOdd = UPC == 4 ? 2 : 0;
+    for (int ot = 1; ot < kNT - 1; ot += 2) {
+      ro_tile<MT, kOdd>(R, F, X, S, ot, g4, P, Q, pf, pb);
+      ro_tile<MT, 0>(R, F, X, S, ot + 1, g4, P, Q, pf, pb);
     }
+    ro_tile<MT, kOdd>(R, F, X, S, kNT - 1, g4, P, Q, pf, pb);
     {
       const f4 w2 = ldf4(S.w2 + 16 * (kNT - 1) + g4);
       ro_piece<MT, 0>(P, Q, w2, pf, pb);
@@ -416,7 +435,10 @@ struct CoreBF16T {
 
 hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                   const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
-  return chain::launch_flux_core<CoreBF16T<4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
+    return chain::launch_flux_core<CoreBF16T<4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  // windowed (e.g. cfg4's 1024 cells): 16 KiB chunks in 3 slots
+  return chain::launch_flux_windowed<CoreBF16T<4, 4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float *state_final, const float *x,

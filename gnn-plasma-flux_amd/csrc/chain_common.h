@@ -181,9 +181,13 @@ __device__ __forceinline__ Small stage_small(const ChainW &W, float *s) {
 }
 
 // ----------------------------------------------------------------- the ring
-// CF = chunk size in floats (2048 = 8 KiB or 4096 = 16 KiB); NW = waves sharing the ring.
-template <int CF, int NW = kWaves>
+// CF = chunk size in floats (2048 = 8 KiB or 4096 = 16 KiB); NW = waves sharing
+// the ring; SLOTS = LDS slots (3 suffice: at next() every wave has passed the
+// barrier with its reads of chunk pos-1 retired, so pos+2 may take that slot;
+// 4 keep the slot arithmetic a mask).
+template <int CF, int NW = kWaves, int SLOTS = kRingSlots>
 struct Ring {
+  static_assert(SLOTS == 3 || SLOTS == 4, "ring slots");
   static constexpr int kPerWave = CF / (NW * 256);  // 1 KiB DMA instructions per wave per chunk
   static_assert(kPerWave == 1 || kPerWave == 2 || kPerWave == 4, "ring chunk split over the waves");
   __amdgpu_buffer_rsrc_t rsrc;  // packed weight stream (global)
@@ -191,7 +195,8 @@ struct Ring {
   float *lds;                   // 4 slots
   int chunks;        // chunks per forward pass
   int wave, lane;
-  int pos;           // stream position being consumed (slot = pos & 3)
+  int pos;           // stream position being consumed
+  int rd;            // its slot (pos % SLOTS)
   int ahead;         // chunk id of stream position pos + 2
 
   // The DMA is issued from inline asm, hidden from hipcc's s_waitcnt
@@ -219,6 +224,7 @@ struct Ring {
   // Start the stream at chunk 0 (positions 0 and 1 in flight).
   __device__ __forceinline__ void prime() {
     pos = 0;
+    rd = 0;
     issue(0, 0);
     issue(1 % chunks, 1);
     ahead = 2 % chunks;
@@ -248,10 +254,11 @@ struct Ring {
 #endif
     __builtin_amdgcn_sched_barrier(0);
 #if !defined(HF_DIAG_NODMA) && !defined(HF_DIAG_NOSYNC)  // timing diagnostics only
-    issue(ahead, (pos + 2) & (kRingSlots - 1));
+    issue(ahead, rd + 2 >= SLOTS ? rd + 2 - SLOTS : rd + 2);
 #endif
     ahead = ahead + 1 == chunks ? 0 : ahead + 1;
-    const float *slot = lds + (pos & (kRingSlots - 1)) * CF;
+    const float *slot = lds + rd * CF;
+    rd = rd + 1 == SLOTS ? 0 : rd + 1;
     ++pos;
     return slot;
   }
@@ -259,8 +266,9 @@ struct Ring {
 };
 
 template <class Core>
-__device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW> make_ring(const ChainW &W, float *ring_lds) {
-  Ring<Core::kChunkFloats, Core::kNW> R;
+__device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW, Core::kSlots> make_ring(const ChainW &W,
+                                                                                    float *ring_lds) {
+  Ring<Core::kChunkFloats, Core::kNW, Core::kSlots> R;
   // the packed stream is chain_chunks() chunks of chain_chunk_bytes(); a core may move it in larger chunks
   R.chunks = chain_chunks(W.layers, W.prec) * chain_chunk_bytes(W.prec) / (Core::kChunkFloats * 4);
   R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0,
@@ -270,6 +278,7 @@ __device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW> make_ring(const C
   R.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   R.lane = threadIdx.x & 63;
   R.pos = 0;
+  R.rd = 0;
   R.ahead = 0;
   return R;
 }
@@ -278,12 +287,12 @@ __device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW> make_ring(const C
 // per-wave park (Core::kParkFloats: activations a core spills to LDS instead of VGPRs).
 template <class Core, bool SCRATCH = true>
 constexpr int lds_floats() {
-  return kRingSlots * Core::kChunkFloats + kSmallFloats +
+  return Core::kSlots * Core::kChunkFloats + kSmallFloats +
          Core::kNW * ((SCRATCH ? kWaveScratchFloats : 0) + Core::kParkFloats);
 }
 template <class Core, bool SCRATCH = true>
 __device__ __forceinline__ float *park_of(float *lds, int wave) {
-  return lds + kRingSlots * Core::kChunkFloats + kSmallFloats + (SCRATCH ? Core::kNW * kWaveScratchFloats : 0) +
+  return lds + Core::kSlots * Core::kChunkFloats + kSmallFloats + (SCRATCH ? Core::kNW * kWaveScratchFloats : 0) +
          wave * Core::kParkFloats;
 }
 
@@ -381,7 +390,7 @@ __global__ __launch_bounds__(64 * Core::kNW, 1) void chain_flux_kernel(ChainW W,
                                                             int nwin, int64_t items,
                                                             float *__restrict__ fe,
                                                             float *__restrict__ ff) {
-  constexpr int kRingFloats = kRingSlots * Core::kChunkFloats;
+  constexpr int kRingFloats = Core::kSlots * Core::kChunkFloats;
   __shared__ f4 lds4[lds_floats<Core, false>() / 4];
   float *lds = reinterpret_cast<float *>(lds4);
   const Small S = stage_small(W, lds + kRingFloats);
@@ -448,7 +457,7 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
     const float *__restrict__ x, const double *__restrict__ pc, int B, int T, float c, float dt,
     float *__restrict__ traj, float *__restrict__ flux_traj, float *__restrict__ metrics, RolloutExtras ex) {
   constexpr int NX = 16 * MT;
-  constexpr int kRingFloats = kRingSlots * Core::kChunkFloats;
+  constexpr int kRingFloats = Core::kSlots * Core::kChunkFloats;
   __shared__ f4 lds4[lds_floats<Core>() / 4];
   float *lds = reinterpret_cast<float *>(lds4);
   const Small S = stage_small(W, lds + kRingFloats);

@@ -23,6 +23,7 @@ using namespace chain;
 
 struct CoreF32 {
   static constexpr int kNW = kWaves;   // waves sharing the weight ring
+  static constexpr int kSlots = kRingSlots;
   static constexpr int kWinMT = 4;     // m-tiles per wave in the windowed flux kernel
   // units per ring chunk: 4 (8 KiB chunks); 8 (16 KiB, half the barriers)
   // measured no faster, for the IC-per-wave and the cell-split kernels alike

@@ -53,6 +53,7 @@ struct ModeF16x3 {
 template <class M>
 struct CoreK32 {
   static constexpr int kNW = kWaves;   // waves sharing the weight ring
+  static constexpr int kSlots = kRingSlots;
   static constexpr int kWinMT = 4;     // m-tiles per wave in the windowed flux kernel
   static constexpr int kChunkFloats = M::kChunkFloats;
   // first output half of a layer parked in LDS while the second half runs:
