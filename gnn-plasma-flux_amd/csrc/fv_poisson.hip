@@ -126,6 +126,85 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
   if (metrics) block_metrics(m, metrics + b * ld_metrics, nx);
 }
 
+// FFT sizes: two ICs per workgroup share one complex transform pair.  The
+// spectral operator T = i/k (k = 0 zeroed) maps the FFT of a real signal to
+// the FFT of a real signal, so with z = rho_a + i rho_b,
+//   ifft(T fft(z)) = ifft(T fft(rho_a)) + i ifft(T fft(rho_b)) = E_a + i E_b:
+// the real part is IC a's field and the imaginary part IC b's, for half the
+// transform work per IC (src/baseline_solver.py:59-68 evaluates each
+// separately; the two agree to float64 rounding, far below the float32 result).
+// LDS: n, u, E, F [2][nx] (float; every global read issued up front, one HBM
+// round trip) | FFT buffers 2 x nx double2 | twiddles nx/2 double2.
+__host__ __device__ inline size_t fv_pair_offset(int nx) { return ((size_t)nx * 8 * sizeof(float) + 15) & ~size_t(15); }
+inline size_t fv_pair_lds_bytes(int nx) { return fv_pair_offset(nx) + (2 * (size_t)nx + nx / 2) * sizeof(double2); }
+
+template <bool HYBRID>
+__global__ __launch_bounds__(kFvThreads) void fv_step_pair_kernel(
+    const float *__restrict__ in, int64_t ld_in, float *__restrict__ out, int64_t ld_out,
+    const float *__restrict__ face_flux, const double *__restrict__ pc, int nx, float c, float dt,
+    float nu, float dx2, float *__restrict__ flux_out, int64_t ld_flux, float *__restrict__ metrics,
+    int64_t ld_metrics, int B) {
+  extern __shared__ double s_dyn[];
+  float *s_u = reinterpret_cast<float *>(s_dyn);  // [2][nx]
+  float *s_F = s_u + 2 * nx;                      // [2][nx]
+  float *s_n = s_F + 2 * nx;                      // [2][nx]
+  float *s_E = s_n + 2 * nx;                      // [2][nx]
+  double2 *fa = reinterpret_cast<double2 *>(reinterpret_cast<char *>(s_dyn) + fv_pair_offset(nx));
+  double2 *fb = fa + nx, *tw = fb + nx;
+  const int64_t b0 = 2 * (int64_t)blockIdx.x;
+  const int nic = b0 + 1 < B ? 2 : 1;
+  for (int q = 0; q < nic; ++q) {
+    const float *st = in + (b0 + q) * ld_in;
+    for (int i = threadIdx.x; i < nx; i += kFvThreads) {
+      const float n = st[i], u = st[nx + i];
+      s_n[q * nx + i] = n;
+      s_u[q * nx + i] = u;
+      s_E[q * nx + i] = st[2 * nx + i];
+      s_F[q * nx + i] = HYBRID ? face_flux[(b0 + q) * nx + i] : __fmul_rn(n, u);  // F_n = n*u (:70-71)
+    }
+  }
+  stage_twiddles(pc, tw, nx);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nx; i += kFvThreads) {
+    const int im = i == 0 ? nx - 1 : i - 1;
+    const int ip = i == nx - 1 ? 0 : i + 1;
+    double rho[2] = {0.0, 0.0};
+    for (int q = 0; q < nic; ++q) {
+      float *so = out + (b0 + q) * ld_out;
+      const float *u = s_u + q * nx, *Fq = s_F + q * nx;
+      const float F = Fq[i];
+      const float n_new = continuity(s_n[q * nx + i], F, Fq[im], c);
+      const float E = s_E[q * nx + i];
+      const float u_new = HYBRID ? velocity_hybrid(u[i], u[im], E, c, dt)
+                                 : velocity_classical(u[i], u[im], u[ip], E, c, dt, nu, dx2);
+      rho[q] = (double)__fsub_rn(n_new, 1.0f);
+      so[i] = n_new;
+      so[nx + i] = u_new;
+      if (flux_out) flux_out[(b0 + q) * ld_flux + i] = F;
+    }
+    fa[i] = make_double2(rho[0], rho[1]);
+  }
+  const double2 *X = poisson_fft(fa, fb, tw, pc + 2 * nx, nx);
+  MetricAcc m[2];
+  m[0].init();
+  m[1].init();
+  for (int i = threadIdx.x; i < nx; i += kFvThreads) {
+    for (int q = 0; q < nic; ++q) {
+      float *so = out + (b0 + q) * ld_out;
+      const float E_new = (float)((q == 0 ? X[i].x : X[i].y) / nx);
+      so[2 * nx + i] = E_new;
+      if (metrics) m[q].add(so[i], so[nx + i], E_new);
+    }
+  }
+  if (metrics) {
+    block_metrics(m[0], metrics + b0 * ld_metrics, nx);
+    if (nic == 2) {
+      __syncthreads();  // block_metrics' shared partials are reused
+      block_metrics(m[1], metrics + (b0 + 1) * ld_metrics, nx);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kFvThreads) void state_metrics_kernel(const float *__restrict__ st,
                                                                    int64_t ld, int nx,
                                                                    float *__restrict__ metrics,
@@ -205,6 +284,17 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
                           float dt, float nu, float dx2, float *flux_out, int64_t ld_flux,
                           float *metrics, int64_t ld_metrics, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  if (poisson_uses_fft(nx)) {  // two ICs per workgroup, one transform pair
+    const size_t lds = fv_pair_lds_bytes(nx);
+    const unsigned grid = (unsigned)((B + 1) / 2);
+    if (face_flux)
+      hipLaunchKernelGGL(fv_step_pair_kernel<true>, dim3(grid), dim3(kFvThreads), lds, s, in, ld_in, out, ld_out,
+                         face_flux, pc, nx, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
+    else
+      hipLaunchKernelGGL(fv_step_pair_kernel<false>, dim3(grid), dim3(kFvThreads), lds, s, in, ld_in, out, ld_out,
+                         face_flux, pc, nx, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
+    return hipGetLastError();
+  }
   const size_t lds = fv_lds_bytes(nx);
   if (face_flux)
     hipLaunchKernelGGL(fv_step_kernel<true>, dim3(B), dim3(kFvThreads), lds, s, in, ld_in, out,
