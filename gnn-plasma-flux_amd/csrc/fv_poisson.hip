@@ -39,11 +39,10 @@ __device__ __forceinline__ void block_metrics(MetricAcc &m, float *dst, int nx) 
 }
 
 // LDS, circulant nx: c[nx] (double) | u, F, rho, E (float).
-// LDS, FFT nx: u, F (float) | FFT buffers 2 x nx double2 | twiddles nx/2 double2
-// (48 KiB at nx = 1024: three workgroups per CU).
+// LDS, FFT nx: u, F (float) | FFT buffers 2 x nx double2 | twiddles nx/4 double2.
 __host__ __device__ inline size_t fv_fft_offset(int nx) { return ((size_t)nx * 2 * sizeof(float) + 15) & ~size_t(15); }
 inline size_t fv_lds_bytes(int nx) {
-  return poisson_uses_fft(nx) ? fv_fft_offset(nx) + (2 * (size_t)nx + nx / 2) * sizeof(double2)
+  return poisson_uses_fft(nx) ? fv_fft_offset(nx) + (2 * (size_t)nx + nx / 4) * sizeof(double2)
                               : (size_t)nx * (sizeof(double) + 4 * sizeof(float));
 }
 
@@ -72,10 +71,10 @@ struct FvLds {
   }
 };
 
-// Stage the plan's twiddles (after the circulant column c[nx]) into LDS.
+// Stage the first quarter of the plan's twiddles (after the circulant column c[nx]) into LDS.
 __device__ __forceinline__ void stage_twiddles(const double *pc, double2 *s_tw, int nx) {
   const double2 *tw = reinterpret_cast<const double2 *>(pc + nx);
-  for (int q = threadIdx.x; q < nx / 2; q += blockDim.x) s_tw[q] = tw[q];
+  for (int q = threadIdx.x; q < nx / 4; q += blockDim.x) s_tw[q] = tw[q];
 }
 
 template <bool HYBRID>
@@ -133,10 +132,13 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
 // the real part is IC a's field and the imaginary part IC b's, for half the
 // transform work per IC (src/baseline_solver.py:59-68 evaluates each
 // separately; the two agree to float64 rounding, far below the float32 result).
-// LDS: n, u, E, F [2][nx] (float; every global read issued up front, one HBM
-// round trip) | FFT buffers 2 x nx double2 | twiddles nx/2 double2.
-__host__ __device__ inline size_t fv_pair_offset(int nx) { return ((size_t)nx * 8 * sizeof(float) + 15) & ~size_t(15); }
-inline size_t fv_pair_lds_bytes(int nx) { return fv_pair_offset(nx) + (2 * (size_t)nx + nx / 2) * sizeof(double2); }
+// Every global read is issued up front (one HBM round trip): n and E into
+// registers, u and F (read at i-1, i+1) into LDS, where they share the second
+// FFT buffer (first written by the transform, after its opening barrier).
+// LDS: FFT buffer a [nx] double2 | buffer b [nx] double2 = u, F [2][nx] float |
+// twiddles nx/4 double2: 36 KiB at nx = 1024, four workgroups per CU.
+constexpr int kFvPer = kFftMaxNx / kFvThreads;  // cells per thread, at most
+inline size_t fv_pair_lds_bytes(int nx) { return (2 * (size_t)nx + nx / 4) * sizeof(double2); }
 
 template <bool HYBRID>
 __global__ __launch_bounds__(kFvThreads) void fv_step_pair_kernel(
@@ -145,36 +147,47 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_pair_kernel(
     float nu, float dx2, float *__restrict__ flux_out, int64_t ld_flux, float *__restrict__ metrics,
     int64_t ld_metrics, int B) {
   extern __shared__ double s_dyn[];
-  float *s_u = reinterpret_cast<float *>(s_dyn);  // [2][nx]
-  float *s_F = s_u + 2 * nx;                      // [2][nx]
-  float *s_n = s_F + 2 * nx;                      // [2][nx]
-  float *s_E = s_n + 2 * nx;                      // [2][nx]
-  double2 *fa = reinterpret_cast<double2 *>(reinterpret_cast<char *>(s_dyn) + fv_pair_offset(nx));
+  double2 *fa = reinterpret_cast<double2 *>(s_dyn);
   double2 *fb = fa + nx, *tw = fb + nx;
+  float *s_u = reinterpret_cast<float *>(fb);  // [2][nx], then [2][nx] F: the 16*nx bytes of fb
+  float *s_F = s_u + 2 * nx;
   const int64_t b0 = 2 * (int64_t)blockIdx.x;
   const int nic = b0 + 1 < B ? 2 : 1;
-  for (int q = 0; q < nic; ++q) {
-    const float *st = in + (b0 + q) * ld_in;
-    for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-      const float n = st[i], u = st[nx + i];
-      s_n[q * nx + i] = n;
-      s_u[q * nx + i] = u;
-      s_E[q * nx + i] = st[2 * nx + i];
-      s_F[q * nx + i] = HYBRID ? face_flux[(b0 + q) * nx + i] : __fmul_rn(n, u);  // F_n = n*u (:70-71)
+  float n_r[2][kFvPer], E_r[2][kFvPer];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if (q < nic) {
+      const float *st = in + (b0 + q) * ld_in;
+#pragma unroll
+      for (int k = 0; k < kFvPer; ++k) {
+        const int i = threadIdx.x + k * kFvThreads;
+        if (i < nx) {
+          const float n = st[i], u = st[nx + i];
+          n_r[q][k] = n;
+          E_r[q][k] = st[2 * nx + i];
+          s_u[q * nx + i] = u;
+          s_F[q * nx + i] = HYBRID ? face_flux[(b0 + q) * nx + i] : __fmul_rn(n, u);  // F_n = n*u (:70-71)
+        }
+      }
     }
   }
   stage_twiddles(pc, tw, nx);
   __syncthreads();
-  for (int i = threadIdx.x; i < nx; i += kFvThreads) {
+#pragma unroll
+  for (int k = 0; k < kFvPer; ++k) {
+    const int i = threadIdx.x + k * kFvThreads;
+    if (i >= nx) break;
     const int im = i == 0 ? nx - 1 : i - 1;
     const int ip = i == nx - 1 ? 0 : i + 1;
     double rho[2] = {0.0, 0.0};
-    for (int q = 0; q < nic; ++q) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q >= nic) break;
       float *so = out + (b0 + q) * ld_out;
       const float *u = s_u + q * nx, *Fq = s_F + q * nx;
       const float F = Fq[i];
-      const float n_new = continuity(s_n[q * nx + i], F, Fq[im], c);
-      const float E = s_E[q * nx + i];
+      const float n_new = continuity(n_r[q][k], F, Fq[im], c);
+      const float E = E_r[q][k];
       const float u_new = HYBRID ? velocity_hybrid(u[i], u[im], E, c, dt)
                                  : velocity_classical(u[i], u[im], u[ip], E, c, dt, nu, dx2);
       rho[q] = (double)__fsub_rn(n_new, 1.0f);

@@ -74,9 +74,14 @@ __device__ __forceinline__ float poisson_cell(const float *s_rho, const double *
 __device__ __forceinline__ double2 cmul(double2 a, double2 w) {
   return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
 }
-// exp(-+2 pi i m / n) for 0 <= m < n from the half table tw[m < n/2]
+// exp(-+2 pi i m / n) for 0 <= m < n from the quarter table tw[m < n/4] (the
+// plan holds m < n/2; only the first quarter is staged): quadrant q multiplies
+// by (-i)^q, a swap and sign flips, so every twiddle is exactly the table's.
 __device__ __forceinline__ double2 twiddle(const double2 *__restrict__ tw, int m, int n, bool inverse) {
-  double2 w = m < n / 2 ? tw[m] : make_double2(-tw[m - n / 2].x, -tw[m - n / 2].y);
+  const int n4 = n / 4, q = m / n4;
+  const double2 t = tw[m - q * n4];
+  double2 w = q == 0 ? t : q == 1 ? make_double2(t.y, -t.x) : q == 2 ? make_double2(-t.x, -t.y)
+                                                                    : make_double2(-t.y, t.x);
   if (inverse) w.y = -w.y;
   return w;
 }
