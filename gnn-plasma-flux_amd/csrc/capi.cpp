@@ -69,11 +69,9 @@ int kperm(int s, int lane) { return 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3); }
 //    chunk (l, gi): k-step s = 4gi + (j>>1), output tile nt = 4(j&1) + c,
 //    k = (s < 32 ? 0 : 128) + kperm(s % 32, lane).  Readout chunk (ot, hh):
 //    k-step s = 16hh + 2j + (c>>1), c&1 selects P = W_e[:, :H] or Q = W_e[:, H:].
-//  k32 `stream` (f16x3): per layer chunks (nth, kb) for nth = 0..1, kb = 0..3, each
-//    [j = 2*ntl + (W_a|W_b)][term][lane][e 0..7] 16-bit values with output tile
-//    nt = 4nth + ntl and k = (W_b ? 128 : 0) + 16(2kb + (e>>2)) + 4(lane>>4) + (e&3);
-//    bf16: per layer units (pair q = 0..3, kb = 0..3) of [i = 2t + (W_a|W_b)][lane][e],
-//    output tile nt = 2q + t, two units per chunk;
+//  k32 `stream` (f16x3, bf16): per layer units (pair q = 0..3, kb = 0..3) of
+//    [i = 2t + (W_a|W_b)][term][lane][e 0..7] 16-bit values with output tile
+//    nt = 2q + t and k = (W_b ? 128 : 0) + 16(2kb + (e>>2)) + 4(lane>>4) + (e&3);
 //    then per readout tile ot one chunk [j = 2kb + (P|Q)][term][lane][e].
 //    f16x3: term 0 = fp16(w), term 1 = fp16(w - term0); bf16: one bf16(w) term.
 //  Row n = 16*tile + (lane&15) throughout.
@@ -160,28 +158,19 @@ void pack_chain(const float *p, int L, int prec, ChainPack &P) {
         }
       }
     };
-    if (prec == hf::kPrecBF16) {
-      // chain_bf16.hip walks a layer by output pair q (tiles 2q, 2q+1), k-block
-      // kb within it: unit (q, kb) = fragments i = 2t + (W_a | W_b), tile 2q + t
-      for (int l = 0; l < L; ++l)
-        for (int qp = 0; qp < 4; ++qp)
-          for (int kb = 0; kb < 4; ++kb)
-            for (int i = 0; i < 4; ++i)
+    // chain_bf16.hip and chain_k32.hip walk a layer by output pair q (tiles
+    // 2q, 2q+1), k-block kb within it: unit (q, kb) = fragments i = 2t +
+    // (W_a | W_b) of tile 2q + t, each [term][lane][e].  bf16 folds the 1/deg
+    // into W_b (input-side aggregation); f16x3 applies it to G in the epilogue.
+    for (int l = 0; l < L; ++l)
+      for (int qp = 0; qp < 4; ++qp)
+        for (int kb = 0; kb < 4; ++kb)
+          for (int i = 0; i < 4; ++i)
+            for (int t = 0; t < terms; ++t)
               for (int lane = 0; lane < 64; ++lane) {
                 const int nt = 2 * qp + (i >> 1), ab = i & 1;
-                frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, 0, true);
+                frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, t, prec == hf::kPrecBF16);
               }
-    } else {
-      for (int l = 0; l < L; ++l)
-        for (int nth = 0; nth < 2; ++nth)
-          for (int kb = 0; kb < 4; ++kb)
-            for (int j = 0; j < 8; ++j)
-              for (int t = 0; t < terms; ++t)
-                for (int lane = 0; lane < 64; ++lane) {
-                  const int nt = 4 * nth + (j >> 1), ab = j & 1;
-                  frag(layer_w(l), 2 * kH, 16 * nt + (lane & 15), ab * kH, kb, lane, t, false);
-                }
-    }
     for (int ot = 0; ot < kNT; ++ot)
       for (int j = 0; j < 8; ++j)
         for (int t = 0; t < terms; ++t)

@@ -1,16 +1,15 @@
-// Fused FluxGNN on the periodic chain on the K=32 matrix cores:
-// v_mfma_f32_16x16x32_f16 (mode F16x3) and v_mfma_f32_16x16x32_bf16 (BF16).
+// Fused FluxGNN on the periodic chain, fp32-accurate on the fp16 matrix
+// cores (precision "f16x3"): v_mfma_f32_16x16x32_f16.  bf16 is chain_bf16.hip.
 //
 // Reference: src/flux_gnn.py:40-67, src/hybrid_solver.py:34-73.
 //
 // F16x3 keeps float32-level accuracy at ~5x the f32 MFMA rate: every weight
 // and every activation is split into two fp16 terms, x = x_hi + x_lo with
 // x_hi = fp16(x), x_lo = fp16(x - x_hi) (22 significant bits), and each
-// product is accumulated in f32 as a_hi b_hi + a_hi b_lo + a_lo b_hi (the
+// product is accumulated in f32 as a_lo b_hi + a_hi b_lo + a_hi b_hi (the
 // dropped a_lo b_lo is 2^-22 relative).  Measured against an fp64 evaluation
 // the edge fluxes carry 5.4e-7 error, the same as the reference's own float32
-// CPU evaluation (4.7e-7).  BF16 (BASELINE config 4) is a single bf16 product
-// with bf16-rounded weights and activations.
+// CPU evaluation (4.7e-7).
 //
 // Fragments: for 16x16x32, lane l holds A[row l&15][k = 8(l>>4) + e] and
 // B[k = 8(l>>4) + e][col l&15], e = 0..7.  The B fragment of k-block kb is the
@@ -20,7 +19,17 @@
 //
 // Aggregation by linearity: W_b (h[i+1] + h[i-1]) / 2 = (G[i+1] + G[i-1]) / 2
 // with G = W_b h, so the split activations of a k-block feed both W_a and W_b
-// and the neighbour lane shifts run once per layer on the G accumulators.
+// (the split fragments are twice the size of bf16's, so no second set of
+// neighbour-sum fragments) and the neighbour lane shifts run on the G
+// accumulators.
+//
+// Schedule (as the bf16 core): a layer is walked in output-pair order (pair q
+// = tiles 2q, 2q+1 = the next layer's k-block q, 4 units of 48 MFMAs at MT=4),
+// the epilogue of pair q-1 (neighbour sums of G, ReLU, fp16 hi/lo split) is
+// spread over pair q's units, the new fragments of pairs 0..2 are parked in
+// LDS, and pair 3's epilogue runs under the next layer's first three k-blocks
+// (or the first readout tile).  Every value is formed by the same operations
+// in the same order as a whole-layer epilogue would.
 #include "chain_common.h"
 
 namespace hf {
@@ -29,202 +38,385 @@ namespace {
 using namespace chain;
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef __bf16 b8 __attribute__((ext_vector_type(8)));
-typedef float f8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
-struct ModeF16x3 {
-  static constexpr int kNS = 2;              // fp16 terms per operand
-  [[maybe_unused]] static constexpr int kMma = 3;  // MFMAs per product
-  static constexpr int kChunkFloats = 4096;  // 16 KiB
-  using T = h8;
-  static __device__ __forceinline__ void split(const f8 &v, T (&o)[kNS]) {
-    o[0] = __builtin_convertvector(v, h8);
-    const f8 r = v - __builtin_convertvector(o[0], f8);  // exact: v and hi share the leading bits
-    o[1] = __builtin_convertvector(r, h8);
-  }
-  // a_lo b_hi + a_hi b_lo + a_hi b_hi, small terms first
-  static __device__ __forceinline__ f4 mma(const T (&a)[kNS], const T (&b)[kNS], f4 c) {
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], c, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], c, 0, 0, 0);
-  }
+// the two fp16 terms of one value pair: hi = fp16(v), lo = fp16(v - hi) (exact difference)
+struct Split {
+  unsigned hi, lo;
 };
+__device__ __forceinline__ Split split_pair(float a, float b) {
+  const h2 h = __builtin_convertvector(f2{a, b}, h2);
+  const f2 back = __builtin_convertvector(h, f2);
+  return {__builtin_bit_cast(unsigned, h), __builtin_bit_cast(unsigned, __builtin_convertvector(f2{a, b} - back, h2))};
+}
 
-template <class M>
-struct CoreK32 {
-  static constexpr int kNW = kWaves;   // waves sharing the weight ring
-  static constexpr int kSlots = kRingSlots;
-  static constexpr int kWinMT = 4;     // m-tiles per wave in the windowed flux kernel
-  static constexpr int kChunkFloats = M::kChunkFloats;
-  // first output half of a layer parked in LDS while the second half runs:
-  // [mt 4][tile 4][lane 64][4] floats per wave
-  static constexpr int kParkFloats = 4 * 4 * 64 * 4;
-  static constexpr int kNS = M::kNS;
-  static constexpr int kKB = kH / 32;  // k-blocks per 128-wide operand
-  using T = typename M::T;
-  using R_t = Ring<kChunkFloats>;
+// A split fragment: [0] = hi terms, [1] = lo terms.
+struct Frag {
+  u4 v[2];
+};
+// a_lo b_hi + a_hi b_lo + a_hi b_hi, small terms first
+__device__ __forceinline__ f4 mma3(const Frag &a, const Frag &b, f4 c) {
+  const h8 ah = __builtin_bit_cast(h8, a.v[0]), al = __builtin_bit_cast(h8, a.v[1]);
+  const h8 bh = __builtin_bit_cast(h8, b.v[0]), bl = __builtin_bit_cast(h8, b.v[1]);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+}
 
-  struct Frag {
-    T v[kNS];
-  };
-  struct Feed {};  // fragments are read per chunk (no register prefetch)
-  static __device__ __forceinline__ void begin(R_t &, Feed &) {}
-
-  static __device__ __forceinline__ Frag lds_frag(const float *slot, int j, int lane) {
-    Frag f;
+// Closes one unit's scheduling region: the next unit's 8 ds_reads first, then
+// one MFMA and up to NV VALU at a time (see chain_bf16.hip).
+template <int NM, int NV>
+__device__ __forceinline__ void interleave() {
+  __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
-    for (int s = 0; s < kNS; ++s)
-      f.v[s] = __builtin_bit_cast(T, ldf4(slot + ((j * kNS + s) * 64 + lane) * 4));
-    return f;
+  for (int i = 0; i < NM; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// UPC = units (4 split fragments, 8 KiB) per ring chunk: 1 (8 KiB chunks,
+// 4 slots: fits beside the rollout's per-IC scratch) or 2 (16 KiB, 3 slots).
+template <int UPC>
+struct CoreF16x3T {
+  static constexpr int kNW = kWaves;
+  static constexpr int kUPC = UPC;
+  static constexpr int kSlots = UPC == 2 ? 3 : 4;
+  static constexpr int kWinMT = 4;
+  static constexpr int kChunkFloats = 2048 * UPC;
+  static constexpr int kKB = kH / 32;
+  // parked fragments of k-blocks 0..2: [kb 3][mt 4][term 2][lane 64][4 dwords]
+  static constexpr int kParkFloats = 3 * 4 * 2 * 64 * 4;
+  using R_t = Ring<kChunkFloats, kNW, kSlots>;
+
+  template <int MT>
+  struct Acts {
+    Frag h[MT][kKB];  // split B fragments of h
+  };
+  // One output pair's accumulators: W_a h (+ bias) and G = W_b h.
+  template <int MT>
+  struct PairAcc {
+    f4 a[MT][2], g[MT][2];
+  };
+
+  // Register-prefetched weight feed: the next unit's 8 ds_read_b128 issue
+  // before this unit's MFMAs; the ring's wait + barrier for chunk p+1 precede
+  // the last unit of chunk p.
+  struct Feed {
+    const float *slot;
+    Frag cur[4];
+  };
+  static __device__ __forceinline__ void load_unit(Feed &F, int u, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        F.cur[i].v[s] = __builtin_bit_cast(u4, ldf4(F.slot + (((4 * u + i) * 2 + s) * 64 + lane) * 4));
+  }
+  static __device__ __forceinline__ void begin(R_t &R, Feed &F) {
+    F.slot = R.next();
+    load_unit(F, 0, R.lane);
+  }
+  template <int U>
+  static __device__ __forceinline__ void take(R_t &R, Feed &F, Frag (&w)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = F.cur[i];
+    if constexpr (U == UPC - 1) F.slot = R.next();
+#ifndef HF_DIAG_NODS  // timing diagnostic only: results are wrong
+    load_unit(F, (U + 1) % UPC, R.lane);
+#endif
   }
 
-  // Activation tiles (2kb, 2kb+1) as the split B fragment of k-block kb.
-  static __device__ __forceinline__ void frag_of(const f4 &a, const f4 &b, Frag &o) {
-    const f8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    M::split(v, o.v);
+  static __device__ __forceinline__ float *park_at(float *park, int kb, int mt, int s, int lane) {
+    return park + (((kb * 4 + mt) * 2 + s) * 64 + lane) * 4;
   }
+
+  // Dword K (tile t = K>>1, rows 2(K&1), 2(K&1)+1) of the new k-block
+  // fragment from one output pair: h = ReLU(acc + 0.5*(G[i+1] + G[i-1]))
+  // (src/flux_gnn.py:55-60; 0.5*x is exact), split into fp16 hi/lo.
+  template <int MT, int K>
+  static __device__ __forceinline__ void piece(const PairAcc<MT> &p, Frag (&nh)[MT]) {
+    constexpr int t = K >> 1, r = 2 * (K & 1);
+#ifdef HF_DIAG_NOPIECE  // timing diagnostic only: results are wrong (no epilogue VALU)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      nh[mt].v[0][K] = __float_as_uint(p.a[mt][t][r]);
+      nh[mt].v[1][K] = __float_as_uint(p.g[mt][t][r]);
+    }
+    return;
+#endif
+    float v[2][MT];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float gv[MT], gs[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) gv[mt] = p.g[mt][t][r + e];
+      nb_sum<MT>(gv, gs);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) v[e][mt] = relu(fmaf(gs[mt], 0.5f, p.a[mt][t][r + e]));
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const Split sp = split_pair(v[0][mt], v[1][mt]);
+      nh[mt].v[0][K] = sp.hi;
+      nh[mt].v[1][K] = sp.lo;
+    }
+  }
+
+  // One unit of an update pair: k-block KB, fragments (t, W_a | W_b) = w[2t + ab].
+  template <int MT, int KB, int U>
+  static __device__ __forceinline__ void unit(R_t &R, Feed &F, const Acts<MT> &X, PairAcc<MT> &p) {
+    Frag w[4];
+    take<U>(R, F, w);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        if (i & 1) p.g[mt][i >> 1] = mma3(w[i], X.h[mt][KB], p.g[mt][i >> 1]);
+        else p.a[mt][i >> 1] = mma3(w[i], X.h[mt][KB], p.a[mt][i >> 1]);
+      }
+  }
+
   template <int MT>
-  static __device__ __forceinline__ void to_frags(const f4 (&h)[MT][kNT], Frag (&B)[MT][kKB]) {
+  static __device__ __forceinline__ void init_pair(const float *bias, int q, int g4, PairAcc<MT> &p) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const f4 b = ldf4(bias + 16 * (2 * q + t) + g4);  // b_l enters as the first MFMA's C operand
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        p.a[mt][t] = b;
+        p.g[mt][t] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+
+  // Output pair q >= 1, with the epilogue of pair q-1 (prev) spread over its
+  // 4 units and parked as k-block q-1.
+  template <int MT>
+  static __device__ __forceinline__ void pair_with_prev(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int q,
+                                                        int g4, PairAcc<MT> &p, const PairAcc<MT> &prev, float *park,
+                                                        int lane) {
+    init_pair<MT>(bias, q, g4, p);
+    Frag nh[MT];
+    unit<MT, 0, 0 % UPC>(R, F, X, p);
+    piece<MT, 0>(prev, nh);
+    interleave<12 * MT, 1>();
+    unit<MT, 1, 1 % UPC>(R, F, X, p);
+    piece<MT, 1>(prev, nh);
+    interleave<12 * MT, 1>();
+    unit<MT, 2, 2 % UPC>(R, F, X, p);
+    piece<MT, 2>(prev, nh);
+    interleave<12 * MT, 1>();
+    unit<MT, 3, 3 % UPC>(R, F, X, p);
+    piece<MT, 3>(prev, nh);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int kb = 0; kb < kKB; ++kb) frag_of(h[mt][2 * kb], h[mt][2 * kb + 1], B[mt][kb]);
+      for (int s = 0; s < 2; ++s) *reinterpret_cast<u4 *>(park_at(park, q - 1, mt, s, lane)) = nh[mt].v[s];
+    interleave<12 * MT, 1>();
   }
 
-  // Update-layer chunk (NTH, KB): W_a and W_b fragments of output tiles
-  // 4*NTH .. 4*NTH+3 over k-block KB.  Fragment j = 2*ntl + (0: W_a, 1: W_b).
-  template <int MT, int KB>
-  static __device__ __forceinline__ void layer_chunk(R_t &R, const Frag (&B)[MT][kKB], f4 (&acc)[MT][4],
-                                                     f4 (&gac)[MT][4]) {
-    const float *slot = R.next();
-#pragma unroll
-    for (int ntl = 0; ntl < 4; ++ntl) {
-      const Frag wa = lds_frag(slot, 2 * ntl, R.lane);
-      const Frag wb = lds_frag(slot, 2 * ntl + 1, R.lane);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        acc[mt][ntl] = M::mma(wa.v, B[mt][KB].v, acc[mt][ntl]);
-        gac[mt][ntl] = M::mma(wb.v, B[mt][KB].v, gac[mt][ntl]);
-      }
-    }
-  }
-
-  // h_new = ReLU(acc + (G[i+1] + G[i-1]) / 2) for one half of the output
-  // tiles; the bias is already in acc (the C operand of its first MFMA).
+  // Pair 0 of a layer after another: k-blocks 0..2 from the park, k-block 3
+  // from the previous layer's pair 3 (pend), finished under the first units.
   template <int MT>
-  static __device__ __forceinline__ void layer_epilogue(const f4 (&acc)[MT][4], const f4 (&gac)[MT][4],
-                                                        f4 (&out)[MT][4]) {
+  static __device__ __forceinline__ void pair0_after(R_t &R, Feed &F, Acts<MT> &X, const float *bias, int g4,
+                                                     PairAcc<MT> &p, const PairAcc<MT> &pend, float *park,
+                                                     int lane) {
+    wave_lds_sync();  // this wave's park writes of the previous layer have landed
 #pragma unroll
-    for (int ntl = 0; ntl < 4; ++ntl) {
+    for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float gv[MT], gs[MT];
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) gv[mt] = gac[mt][ntl][r];
-        nb_sum<MT>(gv, gs);
+        for (int s = 0; s < 2; ++s) X.h[mt][kb].v[s] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, mt, s, lane)));
+    init_pair<MT>(bias, 0, g4, p);
+    Frag nh[MT];
+    unit<MT, 0, 0 % UPC>(R, F, X, p);
+    piece<MT, 0>(pend, nh);
+    piece<MT, 1>(pend, nh);
+    interleave<12 * MT, 1>();
+    unit<MT, 1, 1 % UPC>(R, F, X, p);
+    piece<MT, 2>(pend, nh);
+    interleave<12 * MT, 1>();
+    unit<MT, 2, 2 % UPC>(R, F, X, p);
+    piece<MT, 3>(pend, nh);
+    interleave<12 * MT, 1>();
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          // acc + 0.5*(G[i+1] + G[i-1]): one rounding either way, 0.5*x is exact
-          out[mt][ntl][r] = relu(fmaf(gs[mt], 0.5f, acc[mt][ntl][r]));
-        }
-      }
-    }
+    for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
+    unit<MT, 3, 3 % UPC>(R, F, X, p);
+    interleave<12 * MT, 0>();
   }
 
-  template <int MT, int NTH>
-  static __device__ __forceinline__ void layer_half(R_t &R, const Frag (&B)[MT][kKB], const float *bias, int g4,
-                                                    f4 (&out)[MT][4]) {
-    f4 acc[MT][4], gac[MT][4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const f4 b = ldf4(bias + 64 * NTH + 16 * n + g4);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        acc[mt][n] = b;
-        gac[mt][n] = f4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-    layer_chunk<MT, 0>(R, B, acc, gac);
-    layer_chunk<MT, 1>(R, B, acc, gac);
-    layer_chunk<MT, 2>(R, B, acc, gac);
-    layer_chunk<MT, 3>(R, B, acc, gac);
-    layer_epilogue<MT>(acc, gac, out);
-  }
-
-  // Readout chunk for output tile ot: fragment j = 2*kb + (0: P, 1: Q).
   template <int MT>
-  static __device__ __forceinline__ void readout_chunk(R_t &R, const Frag (&B)[MT][kKB], f4 (&P)[MT], f4 (&Q)[MT]) {
-    const float *slot = R.next();
+  static __device__ __forceinline__ void pair0_first(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
+                                                     PairAcc<MT> &p) {
+    init_pair<MT>(bias, 0, g4, p);
+    unit<MT, 0, 0 % UPC>(R, F, X, p);
+    interleave<12 * MT, 0>();
+    unit<MT, 1, 1 % UPC>(R, F, X, p);
+    interleave<12 * MT, 0>();
+    unit<MT, 2, 2 % UPC>(R, F, X, p);
+    interleave<12 * MT, 0>();
+    unit<MT, 3, 3 % UPC>(R, F, X, p);
+    interleave<12 * MT, 0>();
+  }
+
+  template <int MT>
+  static __device__ __forceinline__ void pairs_rest(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
+                                                    PairAcc<MT> &p0, PairAcc<MT> &pend, float *park, int lane) {
+    PairAcc<MT> p1, p2;
+    pair_with_prev<MT>(R, F, X, bias, 1, g4, p1, p0, park, lane);
+    pair_with_prev<MT>(R, F, X, bias, 2, g4, p2, p1, park, lane);
+    pair_with_prev<MT>(R, F, X, bias, 3, g4, pend, p2, park, lane);
+  }
+
+  // Readout unit U of output tile ot (fragment i = 2*(kb - 2U) + (P|Q)), ring index T.
+  template <int MT, int U, int T>
+  static __device__ __forceinline__ void ro_unit(R_t &R, Feed &F, const Acts<MT> &X, f4 (&P)[MT], f4 (&Q)[MT]) {
+    Frag w[4];
+    take<T>(R, F, w);
 #pragma unroll
-    for (int kb = 0; kb < kKB; ++kb) {
-      const Frag wp = lds_frag(slot, 2 * kb, R.lane);
-      const Frag wq = lds_frag(slot, 2 * kb + 1, R.lane);
+    for (int i = 0; i < 4; ++i) {
+      const int kb = 2 * U + (i >> 1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        P[mt] = M::mma(wp.v, B[mt][kb].v, P[mt]);
-        Q[mt] = M::mma(wq.v, B[mt][kb].v, Q[mt]);
+        if (i & 1) Q[mt] = mma3(w[i], X.h[mt][kb], Q[mt]);
+        else P[mt] = mma3(w[i], X.h[mt][kb], P[mt]);
       }
     }
   }
 
   template <int MT>
-  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &, float *park,
-                                             const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
-    const int lane = R.lane;
-    const int g4 = 4 * (lane >> 4);
-    Frag B[MT][kKB];
-    {
-      f4 h[MT][kNT];
-      input_layer<MT>(S, lane, feat, h);
-      to_frags<MT>(h, B);
+  static __device__ __forceinline__ void init_ro(const Small &S, int ot, int g4, f4 (&P)[MT], f4 (&Q)[MT]) {
+    const f4 be = ldf4(S.be + 16 * ot + g4);  // b_e enters P as the C operand of its first MFMA
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      P[mt] = be;
+      Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
     }
-    // message passing (src/flux_gnn.py:53-60)
-    for (int l = 0; l < W.layers; ++l) {
-      const float *bias = S.bl + l * kH;
-      {
-        f4 lo[MT][4];
-        layer_half<MT, 0>(R, B, bias, g4, lo);
+  }
+
+  // Readout tile ot >= 1 (ring indices 0, 1 % UPC), with the epilogue of tile
+  // ot-1 (rows in order, as readout_epilogue) spread over its two units.
+  template <int MT>
+  static __device__ __forceinline__ void ro_tile(R_t &R, Feed &F, const Acts<MT> &X, const Small &S, int ot,
+                                                 int g4, f4 (&P)[MT], f4 (&Q)[MT], float (&pf)[MT],
+                                                 float (&pb)[MT]) {
+    f4 Pn[MT], Qn[MT];
+    init_ro<MT>(S, ot, g4, Pn, Qn);
+    const f4 w2 = ldf4(S.w2 + 16 * (ot - 1) + g4);
+    ro_unit<MT, 0, 0>(R, F, X, Pn, Qn);
+    readout_row<MT, 0, true>(P, Q, w2, w2, pf, pb);
+    readout_row<MT, 1, true>(P, Q, w2, w2, pf, pb);
+    interleave<12 * MT, 1>();
+    ro_unit<MT, 1, 1 % UPC>(R, F, X, Pn, Qn);
+    readout_row<MT, 2, true>(P, Q, w2, w2, pf, pb);
+    readout_row<MT, 3, true>(P, Q, w2, w2, pf, pb);
+    interleave<12 * MT, 1>();
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) *reinterpret_cast<f4 *>(park + ((mt * 4 + n) * 64 + lane) * 4) = lo[mt][n];
-      }
-      {
-        f4 hi[MT][4];
-        layer_half<MT, 1>(R, B, bias, g4, hi);
-        // new B fragments one k-block at a time (the old ones are dead now):
-        // k-blocks 2, 3 from registers, then 0, 1 from the park, so f32
-        // activations and fragments are never all live at once
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          frag_of(hi[mt][0], hi[mt][1], B[mt][2]);
-          frag_of(hi[mt][2], hi[mt][3], B[mt][3]);
-        }
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-          frag_of(ldf4(park + ((mt * 4 + 2 * kb) * 64 + lane) * 4),
-                  ldf4(park + ((mt * 4 + 2 * kb + 1) * 64 + lane) * 4), B[mt][kb]);
+    for (int mt = 0; mt < MT; ++mt) {
+      P[mt] = Pn[mt];
+      Q[mt] = Qn[mt];
     }
-    // edge readout, P/Q split (src/flux_gnn.py:62-66)
+  }
+
+  // Edge readout, P/Q split (src/flux_gnn.py:62-66), pipelined tile by tile;
+  // the last layer's pair 3 (pend) is activated under the first readout unit.
+  template <int MT>
+  static __device__ __forceinline__ void readout(const ChainW &W, const Small &S, R_t &R, Feed &F, Acts<MT> &X,
+                                                 const PairAcc<MT> &pend, float *park, int lane, int g4,
+                                                 float (&ffwd)[MT], float (&fbwd)[MT]) {
+    wave_lds_sync();
+#pragma unroll
+    for (int kb = 0; kb < 3; ++kb)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) X.h[mt][kb].v[s] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, mt, s, lane)));
     float pf[MT], pb[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
-    for (int ot = 0; ot < kNT; ++ot) {
-      f4 P[MT], Q[MT];
-      const f4 be = ldf4(S.be + 16 * ot + g4);  // b_e enters P as the C operand of its first MFMA
+    f4 P[MT], Q[MT];
+    init_ro<MT>(S, 0, g4, P, Q);
+    {
+      Frag nh[MT];
+      ro_unit<MT, 0, 0>(R, F, X, P, Q);
+      piece<MT, 0>(pend, nh);
+      piece<MT, 1>(pend, nh);
+      piece<MT, 2>(pend, nh);
+      piece<MT, 3>(pend, nh);
+      interleave<12 * MT, 1>();
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        P[mt] = be;
-        Q[mt] = f4{0.f, 0.f, 0.f, 0.f};
-      }
-      readout_chunk<MT>(R, B, P, Q);
-      readout_epilogue<MT, true>(P, Q, be, ldf4(S.w2 + 16 * ot + g4), pf, pb);
+      for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
+      ro_unit<MT, 1, 1 % UPC>(R, F, X, P, Q);
+      interleave<12 * MT, 0>();
+    }
+    // tiles 1..7 (two units each, so every tile starts a ring chunk)
+    for (int ot = 1; ot < kNT; ++ot) ro_tile<MT>(R, F, X, S, ot, g4, P, Q, pf, pb);
+    {
+      const f4 w2 = ldf4(S.w2 + 16 * (kNT - 1) + g4);
+      readout_epilogue<MT, true>(P, Q, w2, w2, pf, pb);
     }
     readout_finish<MT>(pf, pb, W.b2, ffwd, fbwd);
+  }
+
+  template <int MT>
+  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &F, float *park,
+                                             const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
+    const int lane = R.lane;
+    const int g4 = 4 * (lane >> 4);
+    Acts<MT> X;
+    PairAcc<MT> pend;
+    {
+      f4 h[MT][kNT];
+      input_layer<MT>(S, lane, feat, h);  // f32 MFMA, ReLU applied
+#pragma unroll
+      for (int kb = 0; kb < kKB; ++kb)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int t = k >> 1, r = 2 * (k & 1);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const Split sp = split_pair(h[mt][2 * kb + t][r], h[mt][2 * kb + t][r + 1]);
+            X.h[mt][kb].v[0][k] = sp.hi;
+            X.h[mt][kb].v[1][k] = sp.lo;
+          }
+        }
+      if (W.layers == 0) {
+        // no update layer: hand the readout the input layer's output the way
+        // a last layer would (k-blocks 0..2 parked, tiles 6, 7 pending with
+        // G = 0, so the epilogue returns ReLU(h) = h)
+#pragma unroll
+        for (int kb = 0; kb < 3; ++kb)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) *reinterpret_cast<u4 *>(park_at(park, kb, mt, s, lane)) = X.h[mt][kb].v[s];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            pend.a[mt][t] = h[mt][6 + t];
+            pend.g[mt][t] = f4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+    }
+    // message passing (src/flux_gnn.py:53-60), pair-pipelined
+    if (W.layers > 0) {
+      PairAcc<MT> p0;
+      pair0_first<MT>(R, F, X, S.bl, g4, p0);
+      pairs_rest<MT>(R, F, X, S.bl, g4, p0, pend, park, lane);
+    }
+    for (int l = 1; l < W.layers; ++l) {
+      const float *bias = S.bl + l * kH;
+      PairAcc<MT> p0;
+      pair0_after<MT>(R, F, X, bias, g4, p0, pend, park, lane);
+      pairs_rest<MT>(R, F, X, bias, g4, p0, pend, park, lane);
+    }
+    readout<MT>(W, S, R, F, X, pend, park, lane, g4, ffwd, fbwd);
   }
 };
 
@@ -232,17 +424,18 @@ struct CoreK32 {
 
 hipError_t launch_chain_flux_k32(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                  const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
-  if (w.prec == kPrecF16x3)
-    return chain::launch_flux_core<CoreK32<ModeF16x3>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
-  return launch_chain_flux_bf16(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  if (w.prec != kPrecF16x3) return launch_chain_flux_bf16(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
+    return chain::launch_flux_core<CoreF16x3T<1>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  return chain::launch_flux_windowed<CoreF16x3T<2>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float *state_final, const float *x,
                                     const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                     float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
   if (w.prec == kPrecF16x3)
-    return chain::launch_rollout_core<CoreK32<ModeF16x3>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
-                                                          flux_traj, metrics, ex, s);
+    return chain::launch_rollout_core<CoreF16x3T<1>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
+                                                     flux_traj, metrics, ex, s);
   return launch_chain_rollout_bf16(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, ex,
                                    s);
 }

@@ -31,9 +31,9 @@ __host__ __device__ inline int win_faces_of(int layers, int cells = kWinCells) {
 //  f32   (v_mfma_f32_16x16x4_f32): 8 KiB chunks, 16 per update layer (4 k-steps
 //        each, [h ; agg] input order) + 2 per readout output tile.
 //  k32   (v_mfma_f32_16x16x32_{f16,bf16}): per update layer 8 chunks, then one
-//        chunk per readout output tile.  f16x3: 16 KiB chunks (output half,
-//        k-block) of (hi, lo) fp16 fragment pairs; bf16: 8 KiB chunks (output
-//        pair, k-block pair), the order chain_bf16.hip walks a layer in.
+//        chunk per readout output tile, in the order the cores walk a layer:
+//        output pair, then k-block.  f16x3: 16 KiB of (hi, lo) fp16 fragment
+//        pairs; bf16: 8 KiB.  (A core may move two chunks at once.)
 // Each chunk is [fragment j][lane 64][16 B], so one wave instruction moves 1 KiB.
 enum ChainPrec { kPrecF32 = HF_WDTYPE_F32, kPrecBF16 = HF_WDTYPE_BF16, kPrecF16x3 = HF_WDTYPE_F16X3 };
 constexpr int kMaxChainLayers = 8;
