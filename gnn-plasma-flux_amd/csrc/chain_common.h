@@ -341,6 +341,23 @@ __device__ __forceinline__ void readout_epilogue(const f4 (&P)[MT], const f4 (&Q
   readout_row<MT, 3, BIASED>(P, Q, be, w2, pf, pb);
 }
 
+// v[l] + v[l ^ 16] on every lane, by a VALU row swap (v_permlane16_swap:
+// rows 1, 3 of the first operand trade places with rows 0, 2 of the second)
+// instead of an LDS ds_bpermute; fp addition commutes, so the sum is the same
+// bits as v + __shfl_xor(v, 16).
+__device__ __forceinline__ float add_xor16(float v) {
+  const unsigned u = __float_as_uint(v);
+  const auto s = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+// v[l] + v[l ^ 32] (v_permlane32_swap: upper half of the first operand
+// against the lower half of the second).
+__device__ __forceinline__ float add_xor32(float v) {
+  const unsigned u = __float_as_uint(v);
+  const auto s = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+
 // The 128-feature dot product is split over the 4 lane groups of a column.
 template <int MT>
 __device__ __forceinline__ void readout_finish(float (&pf)[MT], float (&pb)[MT], float b2, float (&ffwd)[MT],
@@ -352,10 +369,8 @@ __device__ __forceinline__ void readout_finish(float (&pf)[MT], float (&pb)[MT],
 #endif
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    pf[mt] += __shfl_xor(pf[mt], 16, 64);
-    pf[mt] += __shfl_xor(pf[mt], 32, 64);
-    pb[mt] += __shfl_xor(pb[mt], 16, 64);
-    pb[mt] += __shfl_xor(pb[mt], 32, 64);
+    pf[mt] = add_xor32(add_xor16(pf[mt]));
+    pb[mt] = add_xor32(add_xor16(pb[mt]));
     ffwd[mt] = pf[mt] + b2;
     fbwd[mt] = pb[mt] + b2;
   }
