@@ -52,6 +52,9 @@ __device__ __forceinline__ float velocity_classical(float u, float ul, float ur,
 // Circulant spectral Poisson for one cell: E[i] = f32(sum_j c[(i-j) mod nx] * rho[j]),
 // accumulated in float64 (src/baseline_solver.py:59-68; see hf_poisson_coeffs).
 __device__ __forceinline__ float poisson_cell(const float *s_rho, const double *s_c, int i, int nx) {
+#ifdef HF_DIAG_NOPOISSON  // timing diagnostic only: results are wrong
+  return s_rho[i] * (float)s_c[i];
+#endif
   double a0 = 0.0, a1 = 0.0;
   int d = i;  // (i - j) mod nx, walking j upward
   int j = 0;

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Timing-diagnostic builds of libhybridflux (wrong results by construction; never used by tests or bench):
 #   nobar: no s_barrier in the weight ring; nonb: no neighbour sums; nods: no fragment ds_reads;
-#   nopiece: no bf16 layer epilogue; nosync: no ring waits, barriers or DMA; a+b combines;
+#   nopiece: no bf16/f16x3 layer epilogue; nosync: no ring waits, barriers or DMA;
+#   noepi / nofinish: no readout epilogue / cross-lane sums; nopoisson: no Poisson sum; a+b combines;
 #   DIAG_VARIANTS="nonb nods" selects a subset.
 set -e
 cd "$(dirname "$0")/../gnn-plasma-flux_amd/csrc"
