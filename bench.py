@@ -250,6 +250,8 @@ def main():
                                                  / (PEAK_HBM_GBS * 1e9), 6)},
             "cpu_baseline": cpu,
             "finite_fraction": finite,
+            # SURVEY.md 8(d) secondary rates: batch-steps/s = T / wall, cell-steps/s = IC-steps/s * nx
+            "also": {"batch_steps_per_s": round(K / wall_max, 1), "cell_steps_per_s": round(value * nx, 1)},
             "alt": alt or None,
             "other_configs": others,
         }
