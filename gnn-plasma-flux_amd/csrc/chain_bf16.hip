@@ -64,15 +64,18 @@ __device__ __forceinline__ void interleave() {
 // at 191 registers, 32-cell windows) was measured for the windowed flux
 // kernel: per FLOP 7 % faster, but 32-cell windows recompute 41 % halo
 // against 19 % at 64 cells, so cfg4 ran at 2.18 M IC-steps/s against 2.41 M.
+// WMT = m-tiles per wave of the windowed flux kernel: 80-cell windows (WMT = 5,
+// 389 registers, 8 KiB chunks, the only ring that fits beside a 5-tile park)
+// recompute 13 % halo instead of 16 % but ran 2.7 % slower at cfg4.
 // UPC = units (4 fragments, 4 KiB) per ring chunk: 2 (8 KiB chunks, 4 slots)
 // or 4 (16 KiB chunks, 3 slots: half the ring barriers, +16 KiB of LDS, which
 // the windowed flux kernel has and the rollout, with its per-IC scratch, has not).
-template <int NW, int UPC = 2>
+template <int NW, int UPC = 2, int WMT = (NW == 8 ? 2 : 4)>
 struct CoreBF16T {
   static constexpr int kNW = NW;
   static constexpr int kUPC = UPC;
   static constexpr int kSlots = UPC == 4 ? 3 : 4;
-  static constexpr int kWinMT = NW == 8 ? 2 : 4;  // m-tiles per wave in the windowed flux kernel
+  static constexpr int kWinMT = WMT;  // m-tiles per wave in the windowed flux kernel
   static constexpr int kParkMT = kWinMT;          // largest MT the park holds
   static constexpr int kChunkFloats = 1024 * UPC;
   static constexpr int kKB = kH / 32;        // k-blocks per 128-wide operand
