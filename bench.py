@@ -38,7 +38,8 @@ METRIC = "hybrid rollout timesteps/sec (batched ICs) at 1/2/4/8 MI355X"
 def cpu_baseline(weights, nx, T, n_ics, threads):
     """Reference-faithful CPU hybrid solver (oracle port: one IC at a time,
     torch-CPU FluxGNN + numpy FV/FFT, src/hybrid_solver.py:34-73) on a bounded
-    sample; plus the batched torch-CPU form for context."""
+    sample; plus the batched torch-CPU form for context.  The process is pinned
+    to `threads` host cores for the leg (as taskset would), then unpinned."""
     from oracle import hybrid_oracle as O
     torch.set_num_threads(threads)
     p = O.params_from(weights)
@@ -54,15 +55,26 @@ def cpu_baseline(weights, nx, T, n_ics, threads):
     return alpha, beta
 
 
-def other_config(weights, dev, name, B, nx, precision, K, W):
+def pinned(n):
+    """The first n CPUs this process may run on (taskset -c equivalent), as a set."""
+    avail = sorted(os.sched_getaffinity(0))
+    return set(avail[:n])
+
+
+def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=None):
     """Time one more BASELINE.json single-GPU config the same way as the
-    headline (preallocated outputs, HIP events on the launch stream, wall
-    clock around the launches).  Reported next to the headline, never as it."""
-    from hybridflux import HybridSolver
+    headline (preallocated outputs and workspace, HIP events on the launch
+    stream, wall clock around the launches).  Reported next to the headline,
+    never as it.  fixture: {label: states [n, K+1, 3, nx]} of the batch's first
+    n ICs (committed test vectors); the final states' max |error| against each
+    is reported."""
+    from hybridflux import HybridSolver, engine
+    from hybridflux._lib import HF_OP_RUN
     dt = 5e-3 * 64.0 / nx
-    solver = HybridSolver(weights, radius=2, nx=nx, dt=dt, device=dev, precision=precision)
+    solver = HybridSolver(weights, radius=radius, nx=nx, dt=dt, device=dev, precision=precision)
     ics = solver.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True)
-    solver.run_batch(ics, max(W, 1), traj=False)
+    ws, _ = engine.workspace(HF_OP_RUN, B, nx, K, dev)
+    solver.run_batch(ics, max(W, 1), traj=False, ws=ws)
     final = torch.empty_like(ics)
     met = torch.empty(B, K + 1, 4, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -70,31 +82,41 @@ def other_config(weights, dev, name, B, nx, precision, K, W):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    solver.run_batch(ics, K, traj=False, metrics=met, out=final)
+    solver.run_batch(ics, K, traj=False, metrics=met, out=final, ws=ws)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     kms = e0.elapsed_time(e1)
     flop = GNN_FLOP_PER_CELL_STEP * B * nx * K
     peak = PEAK_F32_MFMA_TFLOPS if precision == "f32" else PEAK_F16_MFMA_TFLOPS
-    return {"workload": name, "ics": B, "nx": nx, "dt": dt, "precision": precision, "steps": K,
-            "value": round(B * K / wall, 1), "unit": "IC-steps/s", "ms_per_step": round(wall / K * 1e3, 4),
-            "kernel_ms": round(kms, 3), "mfma_frac": round(flop / (kms * 1e-3) / 1e12 / peak, 4),
-            "finite_fraction": float(met[:, -1, 2].float().mean().item())}
+    out = {"workload": name, "ics": B, "nx": nx, "dt": dt, "precision": precision, "steps": K,
+           "weights": f"W1_r{radius}",
+           "value": round(B * K / wall, 1), "unit": "IC-steps/s", "ms_per_step": round(wall / K * 1e3, 4),
+           "kernel_ms": round(kms, 3), "mfma_frac": round(flop / (kms * 1e-3) / 1e12 / peak, 4),
+           "finite_fraction": float(met[:, -1, 2].float().mean().item())}
+    for label, want in (fixture or {}).items():
+        n = want.shape[0]
+        if want.shape[1] == K + 1:
+            got = final[:n].cpu().numpy()
+            out[f"max_err_vs_{label}"] = float(np.abs(got.astype(np.float64) - want[:, -1]).max())
+    return out
 
 
 def pmc_traffic(K, B, nx, traj):
-    """HBM bytes per launch from the committed PMC passes of this same bench
-    command (tools/gpu_pmc.sh + tools/pmc_traffic.py), if they match."""
+    """HBM bytes per launch of the headline kernel from the committed PMC passes
+    (tools/gpu_pmc.sh + tools/pmc_traffic.py): FETCH_SIZE / WRITE_SIZE at two
+    step counts give a fixed part and a per-step part, so the figure applies to
+    any --steps of the same workload."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if (t.get("steps"), t.get("ics_per_gpu"), t.get("nx"), t.get("traj")) != (K, B, nx, traj):
+    if (t.get("ics_per_gpu"), t.get("nx"), t.get("traj")) != (B, nx, traj) or "per_step_bytes" not in t:
         return None
-    return t
+    return {"traffic_bytes": t["fixed_bytes"] + t["per_step_bytes"] * K, "source": t["source"],
+            "fixed_bytes": t["fixed_bytes"], "per_step_bytes": t["per_step_bytes"]}
 
 
 def main():
@@ -139,8 +161,9 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    from hybridflux import HybridSolver
-    from hybridflux.rollout import gather_ic_rows, shard_seeds
+    from hybridflux import HybridSolver, engine
+    from hybridflux._lib import HF_OP_RUN, version
+    from hybridflux.rollout import gather_rollout, max_over_ranks, shard_seeds
 
     weights = dict(np.load(args.weights, allow_pickle=False))
     B, nx, K, W = args.ics_per_gpu, args.nx, args.steps, args.warmup
@@ -149,12 +172,13 @@ def main():
     solver = HybridSolver(weights, radius=3, nx=nx, dt=dt, device=dev, precision=args.precision)
     ics = solver.baseline.initial_conditions(shard_seeds(1000, n_total, world, rank), as_tensor=True)
     stream = torch.cuda.current_stream(dev)
+    ws, _ = engine.workspace(HF_OP_RUN, B, nx, K, dev)
 
     # warmup: one rollout of W steps (compiles nothing; faults the code objects in)
-    solver.run_batch(ics, max(W, 1), traj=not args.no_traj, metrics=True)
+    solver.run_batch(ics, max(W, 1), traj=not args.no_traj, metrics=True, ws=ws)
     torch.cuda.synchronize(dev)
 
-    # preallocate outputs so the timed region is launches only
+    # preallocate outputs so the timed region is launches + the metric exchange
     final = torch.empty_like(ics)
     traj_buf = None if args.no_traj else torch.empty(B, K + 1, 3, nx, device=dev)
     met_buf = torch.empty(B, K + 1, 4, device=dev)
@@ -164,14 +188,18 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
-    res = solver.run_batch(ics, K, traj=traj_buf if traj_buf is not None else False, metrics=met_buf, out=final)
+    res = solver.run_batch(ics, K, traj=traj_buf if traj_buf is not None else False, metrics=met_buf, out=final,
+                           ws=ws)
     ev1.record(stream)
-    gathered = gather_ic_rows(res["metrics"][:, -1], n_total)   # RCCL all_gather of final metrics
+    # per-IC summaries (first non-finite step, drifts) on the device,
+    # then ONE exchange of the full metric series [B_rank, T+1, K] + summaries
+    gathered = gather_rollout(res, n_total)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1)
+    gather_bytes = (gathered["metrics"].numel() + gathered["summary"].numel()) * 4
 
     # other precisions, same ICs / K / warmup, timed the same way (reported, not the headline)
     alt = {}
@@ -195,15 +223,22 @@ def main():
 
     others = None
     if world == 1 and not args.no_other_configs:
-        others = [other_config(weights, dev, "cfg2: 64-cell chain, 256-IC batch, f32", 256, 64, "f32", K, W),
-                  other_config(weights, dev, "cfg4: 1024-cell chain, 4096-IC batch, bf16 MLP weights, dt=3.125e-4",
-                               4096, 1024, "bf16", 30, 3)]
+        # cfg4's first ICs (seeds 1000..1003) against committed vectors: the bf16
+        # kernels' emulation and the f32 forward on bf16 weights (tests/golden/
+        # make_oracle_vectors.py), and the reference's own f32 rollout
+        g = np.load(os.path.join(ROOT, "tests", "golden", "bf16_nx1024.npz"))
+        ref = np.load(os.path.join(ROOT, "tests", "golden", "hybrid_W1_r2_nx1024.npz"))
+        fx = {"bf16_oracle": g["states_emul"], "bf16_weight_f32_oracle": g["states_wbf16"],
+              "reference_f32": ref["states"]}
+        w_r1 = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r1.npz"), allow_pickle=False))
+        w_r2 = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r2.npz"), allow_pickle=False))
+        others = [other_config(w_r1, dev, "cfg2: 64-cell chain, 256-IC batch, r=1, f32", 256, 64, "f32", K, W, 1),
+                  other_config(w_r2, dev, "cfg4: 1024-cell chain, 4096-IC batch, r=2, bf16 MLP weights, dt=3.125e-4",
+                               4096, 1024, "bf16", 30, 3, 2, fixture=fx)]
 
-    t_max = torch.tensor([wall], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    wall_max = float(t_max.item())
-    finite = float(gathered[:, 2].float().mean().item())
+    wall_max = max_over_ranks(wall, device=dev if args.dist_backend == "nccl" else "cpu")
+    finite = float(gathered["metrics"][:, -1, 2].float().mean().item())
+    exploded = int((gathered["summary"][:, 0] >= 0).sum().item())
 
     if rank == 0:
         traffic = pmc_traffic(K, B, nx, not args.no_traj)
@@ -216,11 +251,18 @@ def main():
                   f"chain_flux_kernel<{args.precision},window> + fv_step_kernel<hybrid> per step")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            threads = min(16, os.cpu_count() or 1)
-            alpha, beta = cpu_baseline(weights, nx, 30, args.cpu_sample_ics, threads)
-            cpu = {"value": round(alpha, 1), "unit": "IC-steps/s", "cores": threads, "kind": "port",
+            # the GPU box's CPU share is 16 cores (os.cpu_count() there shows the whole host)
+            cores = pinned(min(16, len(os.sched_getaffinity(0))))
+            keep = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, cores)
+            try:
+                alpha, beta = cpu_baseline(weights, nx, 30, args.cpu_sample_ics, len(cores))
+            finally:
+                os.sched_setaffinity(0, keep)
+            cpu = {"value": round(alpha, 1), "unit": "IC-steps/s", "cores": len(cores), "kind": "port",
                    "sample": f"{args.cpu_sample_ics} ICs x 30 steps, one IC at a time (reference-faithful "
                              f"HybridSolver loop: torch-CPU FluxGNN + numpy FV/FFT), nx={nx}",
+                   "pinned_cpus": f"{min(cores)}-{max(cores)} ({len(cores)} of host nproc {os.cpu_count()})",
                    "batched_torch_cpu_value": round(beta, 1)}
         line = {
             "metric": METRIC,
@@ -239,17 +281,24 @@ def main():
             "config": {"workload": f"{'cfg3' if (nx == 64 and B == 4096) else 'cfg2' if (nx == 64 and B == 256) else 'cfg4' if nx == 1024 else 'custom'}: {nx}-cell periodic chain, {B}-IC batch per GPU, FluxGNN(4,128,4) {args.precision}, "
                                    f"{K}-step persistent rollout{'' if args.no_traj else ' recording every state'}",
                        "nx": nx, "dt": dt, "ics_per_gpu": B, "global_ics": n_total, "parallelism": f"ic-shard x{world}",
-                       "collective": f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_gather of per-IC final metrics"},
+                       "collective": f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_gather of the per-IC "
+                                     f"metric series [B,T+1,4] + summaries [B,8] ({gather_bytes} B gathered)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "traffic": traffic["traffic_bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
+                         "traffic_model": ({"fixed_bytes": traffic["fixed_bytes"],
+                                            "per_step_bytes": traffic["per_step_bytes"]} if traffic else None),
+                         "algorithmic_bytes": (12 * B * nx * (K + 1) if not args.no_traj else 0)
+                                              + 24 * B * nx + 4 * B * (K + 1) * 4,
                          "kernel": kernel, "kernel_ms": round(kernel_ms, 3),
                          "flop_per_launch": flop,
                          "hbm_state_frac": round(STATE_BYTES_PER_CELL_STEP * B * nx * K / (kernel_ms * 1e-3)
                                                  / (PEAK_HBM_GBS * 1e9), 6)},
             "cpu_baseline": cpu,
             "finite_fraction": finite,
+            "exploded_ics": exploded,
+            "build": version(),
             # SURVEY.md 8(d) secondary rates: batch-steps/s = T / wall, cell-steps/s = IC-steps/s * nx
             "also": {"batch_steps_per_s": round(K / wall_max, 1), "cell_steps_per_s": round(value * nx, 1)},
             "alt": alt or None,

@@ -225,7 +225,12 @@ int chain_usable(const hf_model *m) {
 
 extern "C" {
 
-const char *hf_version(void) { return "hybridflux 0.1 gfx950"; }
+#ifndef HF_SOURCE_HASH
+#define HF_SOURCE_HASH "unknown"
+#endif
+// "hybridflux <version> gfx950 src:<hash>": the hash covers every source,
+// header and the Makefile the library was built from (Makefile SRC_HASH).
+const char *hf_version(void) { return "hybridflux 0.2 gfx950 src:" HF_SOURCE_HASH; }
 
 const char *hf_last_error(void) { return g_err.c_str(); }
 
@@ -551,15 +556,63 @@ int hf_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, i
   return HF_OK;
 }
 
+int64_t hf_run_workspace_bytes(int op, int B, int nx, int T) {
+  if (B < 0 || nx < 1 || T < 0 || op < HF_OP_STEP || op > HF_OP_COMPARE) return -1;
+  const int64_t S = 4LL * 3 * nx, F = 4LL * nx, al = 256;
+  auto up = [&](int64_t v) { return (v + al - 1) / al * al; };
+  switch (op) {
+    case HF_OP_STEP: return up(B * F);
+    case HF_OP_RUN: return 2 * up(B * S) + up(B * F);
+    default: return 2 * up(B * (T + 1) * S) + up(B * S) + up(B * F);
+  }
+}
+
+namespace {
+
+// Scratch for the generic (non-fused) sequencing: carved from the caller's
+// workspace when given (hf_run_workspace_bytes), else one stream-ordered
+// allocation released on the same stream after the work it backs.
+struct Scratch {
+  char *base = nullptr;
+  bool owned = false;
+  int64_t used = 0, cap = 0;
+  hipStream_t s = nullptr;
+  int init(void *ws, int64_t ws_bytes, int64_t need, hipStream_t st, const char *fn) {
+    s = st;
+    cap = need;
+    if (need == 0) return HF_OK;
+    if (ws) {
+      if (ws_bytes < need)
+        return fail(HF_EINVAL, std::string(fn) + ": workspace smaller than hf_run_workspace_bytes");
+      base = static_cast<char *>(ws);
+      return HF_OK;
+    }
+    if (hipMallocAsync((void **)&base, need, s) != hipSuccess)
+      return fail(HF_ENOMEM, std::string(fn) + ": scratch allocation");
+    owned = true;
+    return HF_OK;
+  }
+  float *take(int64_t bytes) {
+    float *p = reinterpret_cast<float *>(base + used);
+    used += (bytes + 255) / 256 * 256;
+    return p;
+  }
+  ~Scratch() {
+    if (owned) (void)hipFreeAsync(base, s);
+  }
+};
+
+}  // namespace
+
 int hf_step(hf_model_t m, const float *in, float *out, const float *x, const double *pc, int B, int nx,
-            float c, float dt, float nu, float dx2, float *ff, float *metrics, void *stream) {
+            float c, float dt, float nu, float dx2, float *ff, float *metrics, void *ws, int64_t ws_bytes,
+            void *stream) {
   if (B < 0 || nx < 1) return fail(HF_EINVAL, "hf_step: need B >= 0, nx >= 1");
   if (B == 0) return HF_OK;
   if (!in || !out || !pc) return fail(HF_EINVAL, "hf_step: NULL state or Poisson coefficients");
   if (in == out) return fail(HF_EINVAL, "hf_step: state_in and state_out must not alias");
-  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_step: nx too large for the LDS solve");
+  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_step: nx > 6144 (LDS bound of the FV/Poisson kernel)");
   hipStream_t s = as_stream(stream);
-  if (B == 0) return HF_OK;
   if (!m) {  // BaselineSolver.step
     HF_CHECK_HIP(hf::launch_fv_step(in, 3LL * nx, out, 3LL * nx, nullptr, pc, B, nx, c, dt, nu, dx2, ff,
                                     nx, metrics, HF_NUM_METRICS, s),
@@ -575,40 +628,38 @@ int hf_step(hf_model_t m, const float *in, float *out, const float *x, const dou
       HF_CHECK_HIP(hf::launch_state_metrics(out, 3LL * nx, B, nx, metrics, HF_NUM_METRICS, s), "hf_step metrics");
     return HF_OK;
   }
-  float *F = ff;
-  if (!F) HF_CHECK_HIP(hipMallocAsync((void **)&F, sizeof(float) * (size_t)B * nx, s), "hf_step scratch");
-  hipError_t e = hf::launch_chain_flux(m->chain, nullptr, in, 3LL * nx, x, B, nx, nullptr, F, s);
-  if (e == hipSuccess)
-    e = hf::launch_fv_step(in, 3LL * nx, out, 3LL * nx, F, pc, B, nx, c, dt, nu, dx2, nullptr, nx, metrics,
-                           HF_NUM_METRICS, s);
-  if (!ff) (void)hipFreeAsync(F, s);
-  HF_CHECK_HIP(e, "hf_step(hybrid)");
+  Scratch sc;
+  if (int rc = sc.init(ws, ws_bytes, ff ? 0 : hf_run_workspace_bytes(HF_OP_STEP, B, nx, 1), s, "hf_step"))
+    return rc;
+  float *F = ff ? ff : sc.take(sizeof(float) * (int64_t)B * nx);
+  HF_CHECK_HIP(hf::launch_chain_flux(m->chain, nullptr, in, 3LL * nx, x, B, nx, nullptr, F, s), "hf_step(flux)");
+  HF_CHECK_HIP(hf::launch_fv_step(in, 3LL * nx, out, 3LL * nx, F, pc, B, nx, c, dt, nu, dx2, nullptr, nx, metrics,
+                                  HF_NUM_METRICS, s),
+               "hf_step(fv)");
   return HF_OK;
 }
 
 int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B,
            int nx, int T, float c, float dt, float nu, float dx2, float *traj, float *flux_traj,
-           float *metrics, void *stream) {
+           float *metrics, void *ws, int64_t ws_bytes, void *stream) {
   if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run: need B >= 0, nx >= 1, T >= 0");
   if (B == 0) return HF_OK;
   if (!state0 || !state_final || !pc) return fail(HF_EINVAL, "hf_run: NULL state or Poisson coefficients");
-  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run: nx too large for the LDS solve");
+  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run: nx > 6144 (LDS bound of the FV/Poisson kernel)");
   if (m && !x) return fail(HF_EINVAL, "hf_run: NULL x");
   if (m) {
     if (int rc = chain_usable(m)) return rc;
   }
   hipStream_t s = as_stream(stream);
-  if (B == 0) return HF_OK;
   const int64_t S = 3LL * nx;  // floats per state
-  if (m && fused_nx(nx)) {  // state0 may alias state_final: read whole before written
+  if (m && fused_nx(nx)) {  // the kernel reads each IC's state0 whole before writing its state_final
     HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, state0, state_final, x, pc, B, nx, T, c, dt, traj,
                                           flux_traj, metrics, s),
                  "hf_run(hybrid fused)");
     return HF_OK;
   }
-  // Generic sequencing: [chain flux ->] FV+Poisson per step.
-  if (state0 == state_final && T > 0 && !traj)
-    return fail(HF_EINVAL, "hf_run: state0 and state_final may alias only in the fused path");
+  // Generic sequencing: [chain flux ->] FV+Poisson per step, ping-ponging
+  // through scratch (or the trajectory); state0 may alias state_final.
   const int64_t ldT = (T + 1) * S, ldM = (int64_t)(T + 1) * HF_NUM_METRICS;
   if (traj)
     HF_CHECK_HIP(hipMemcpy2DAsync(traj, sizeof(float) * ldT, state0, sizeof(float) * S, sizeof(float) * S, B,
@@ -616,16 +667,18 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
                  "hf_run traj[0]");
   if (metrics) HF_CHECK_HIP(hf::launch_state_metrics(state0, S, B, nx, metrics, ldM, s), "hf_run metrics[0]");
   if (T == 0) {
-    HF_CHECK_HIP(hipMemcpyAsync(state_final, state0, sizeof(float) * B * S, hipMemcpyDeviceToDevice, s),
-                 "hf_run copy");
+    if (state_final != state0)
+      HF_CHECK_HIP(hipMemcpyAsync(state_final, state0, sizeof(float) * B * S, hipMemcpyDeviceToDevice, s),
+                   "hf_run copy");
     return HF_OK;
   }
-  float *scratch = nullptr, *F = nullptr;
-  if (!traj) HF_CHECK_HIP(hipMallocAsync((void **)&scratch, sizeof(float) * (size_t)B * S, s), "hf_run scratch");
-  if (m && hipMallocAsync((void **)&F, sizeof(float) * (size_t)B * nx, s) != hipSuccess) {
-    if (scratch) (void)hipFreeAsync(scratch, s);
-    return fail(HF_ENOMEM, "hf_run: face-flux scratch");
-  }
+  // scratch: two state buffers unless the trajectory is the ping-pong, the face flux for the hybrid step
+  const int64_t sbytes = (sizeof(float) * B * S + 255) / 256 * 256, fbytes = (sizeof(float) * B * nx + 255) / 256 * 256;
+  Scratch sc;
+  if (int rc = sc.init(ws, ws_bytes, (traj ? 0 : 2 * sbytes) + (m ? fbytes : 0), s, "hf_run")) return rc;
+  float *buf[2] = {nullptr, nullptr};
+  if (!traj) buf[0] = sc.take(sbytes), buf[1] = sc.take(sbytes);
+  float *F = m ? sc.take(fbytes) : nullptr;
   hipError_t e = hipSuccess;
   const float *cur = state0;
   int64_t ld_cur = S;
@@ -635,8 +688,11 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
     if (traj) {
       dst = traj + (int64_t)(t + 1) * S;
       ld_dst = ldT;
+    } else if (t == T - 1 && state_final != state0) {
+      dst = state_final;
+      ld_dst = S;
     } else {
-      dst = ((T - 1 - t) % 2 == 0) ? state_final : scratch;
+      dst = buf[t & 1];
       ld_dst = S;
     }
     if (m) e = hf::launch_chain_flux(m->chain, nullptr, cur, ld_cur, x, B, nx, nullptr, F, s);
@@ -647,23 +703,21 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
     cur = dst;
     ld_cur = ld_dst;
   }
-  if (e == hipSuccess && traj)
-    e = hipMemcpy2DAsync(state_final, sizeof(float) * S, cur, sizeof(float) * ldT, sizeof(float) * S, B,
+  if (e == hipSuccess && cur != state_final)
+    e = hipMemcpy2DAsync(state_final, sizeof(float) * S, cur, sizeof(float) * ld_cur, sizeof(float) * S, B,
                          hipMemcpyDeviceToDevice, s);
-  if (scratch) (void)hipFreeAsync(scratch, s);
-  if (F) (void)hipFreeAsync(F, s);
   HF_CHECK_HIP(e, "hf_run");
   return HF_OK;
 }
 
 int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B,
                    int nx, int T, float c, float dt, float nu, float dx2, float *mse, float *metrics,
-                   float *metrics_cl, void *stream) {
+                   float *metrics_cl, void *ws, int64_t ws_bytes, void *stream) {
   if (!m) return fail(HF_EINVAL, "hf_run_compare: NULL model");
   if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run_compare: need B >= 0, nx >= 1, T >= 0");
   if (B == 0) return HF_OK;
   if (!state0 || !state_final || !pc || !x || !mse) return fail(HF_EINVAL, "hf_run_compare: NULL pointer");
-  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run_compare: nx too large for the LDS solve");
+  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run_compare: nx > 6144 (LDS bound of the FV/Poisson kernel)");
   if (int rc = chain_usable(m)) return rc;
   hipStream_t s = as_stream(stream);
   if (fused_nx(nx)) {
@@ -677,25 +731,50 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
                  "hf_run_compare(fused)");
     return HF_OK;
   }
-  // generic nx: both trajectories through HBM, then the MSE reduction
-  const size_t traj_bytes = sizeof(float) * (size_t)B * (T + 1) * 3 * nx;
-  float *th = nullptr, *tc = nullptr, *fin_c = nullptr;
-  HF_CHECK_HIP(hipMallocAsync((void **)&th, traj_bytes, s), "hf_run_compare scratch");
-  if (hipMallocAsync((void **)&tc, traj_bytes, s) != hipSuccess ||
-      hipMallocAsync((void **)&fin_c, sizeof(float) * (size_t)B * 3 * nx, s) != hipSuccess) {
-    (void)hipFreeAsync(th, s);
-    if (tc) (void)hipFreeAsync(tc, s);
-    return fail(HF_ENOMEM, "hf_run_compare: trajectory scratch");
-  }
-  int rc = hf_run(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, th, nullptr, metrics, stream);
-  if (rc == HF_OK) rc = hf_run(nullptr, state0, fin_c, x, pc, B, nx, T, c, dt, nu, dx2, tc, nullptr, metrics_cl, stream);
-  hipError_t e = hipSuccess;
-  if (rc == HF_OK) e = hf::launch_traj_mse(th, tc, B, T + 1, nx, mse, s);
-  (void)hipFreeAsync(th, s);
-  (void)hipFreeAsync(tc, s);
-  (void)hipFreeAsync(fin_c, s);
+  // generic nx: both trajectories through HBM, then the MSE reduction.  The
+  // classical twin runs first: state_final may alias state0, and the hybrid
+  // run is the one that writes it.
+  Scratch sc;
+  if (int rc = sc.init(ws, ws_bytes, hf_run_workspace_bytes(HF_OP_COMPARE, B, nx, T), s, "hf_run_compare"))
+    return rc;
+  const int64_t traj_bytes = sizeof(float) * (int64_t)B * (T + 1) * 3 * nx;
+  float *th = sc.take(traj_bytes), *tc = sc.take(traj_bytes), *fin_c = sc.take(sizeof(float) * (int64_t)B * 3 * nx);
+  const int64_t fbytes = (sizeof(float) * (int64_t)B * nx + 255) / 256 * 256;
+  float *F = sc.take(fbytes);
+  // with a trajectory buffer hf_run needs scratch only for the hybrid face flux
+  int rc = hf_run(nullptr, state0, fin_c, x, pc, B, nx, T, c, dt, nu, dx2, tc, nullptr, metrics_cl, nullptr, 0, stream);
+  if (rc == HF_OK)
+    rc = hf_run(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, th, nullptr, metrics, F, fbytes, stream);
   if (rc != HF_OK) return rc;
-  HF_CHECK_HIP(e, "hf_run_compare mse");
+  HF_CHECK_HIP(hf::launch_traj_mse(th, tc, B, T + 1, nx, mse, s), "hf_run_compare mse");
+  return HF_OK;
+}
+
+int hf_traj_metrics(const float *traj, int B, int T1, int nx, float *metrics, void *stream) {
+  if (B < 0 || T1 < 0 || nx < 1) return fail(HF_EINVAL, "hf_traj_metrics: bad shape");
+  if ((int64_t)B * T1 == 0) return HF_OK;
+  if (!traj || !metrics) return fail(HF_EINVAL, "hf_traj_metrics: NULL pointer");
+  if ((int64_t)B * T1 > 0x7fffffffLL) return fail(HF_EUNSUPPORTED, "hf_traj_metrics: > 2^31 states");
+  HF_CHECK_HIP(hf::launch_state_metrics(traj, 3LL * nx, B * T1, nx, metrics, HF_NUM_METRICS, as_stream(stream)),
+               "hf_traj_metrics");
+  return HF_OK;
+}
+
+int hf_traj_mse(const float *a, const float *b, int B, int T1, int nx, float *mse, void *stream) {
+  if (B < 0 || T1 < 0 || nx < 1) return fail(HF_EINVAL, "hf_traj_mse: bad shape");
+  if ((int64_t)B * T1 == 0) return HF_OK;
+  if (!a || !b || !mse) return fail(HF_EINVAL, "hf_traj_mse: NULL pointer");
+  HF_CHECK_HIP(hf::launch_traj_mse(a, b, B, T1, nx, mse, as_stream(stream)), "hf_traj_mse");
+  return HF_OK;
+}
+
+int hf_rollout_summary(const float *metrics, const float *mse, const float *metrics_ref, int B, int T,
+                       float *summary, float *drift, void *stream) {
+  if (B < 0 || T < 0) return fail(HF_EINVAL, "hf_rollout_summary: need B >= 0, T >= 0");
+  if (B == 0) return HF_OK;
+  if (!metrics || !summary) return fail(HF_EINVAL, "hf_rollout_summary: NULL metrics or summary");
+  HF_CHECK_HIP(hf::launch_rollout_summary(metrics, mse, metrics_ref, B, T, summary, drift, as_stream(stream)),
+               "hf_rollout_summary");
   return HF_OK;
 }
 

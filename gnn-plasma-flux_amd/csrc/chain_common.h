@@ -468,7 +468,7 @@ __global__ __launch_bounds__(64 * Core::kNW, 1) void chain_flux_kernel(ChainW W,
 // runs continuously across steps.
 template <class Core, int MT>
 __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
-    ChainW W, const float *__restrict__ state0, float *__restrict__ state_final,
+    ChainW W, const float *state0, float *state_final,  // may alias (read whole before written)
     const float *__restrict__ x, const double *__restrict__ pc, int B, int T, float c, float dt,
     float *__restrict__ traj, float *__restrict__ flux_traj, float *__restrict__ metrics, RolloutExtras ex) {
   constexpr int NX = 16 * MT;

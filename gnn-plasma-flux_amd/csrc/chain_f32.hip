@@ -334,7 +334,8 @@ constexpr int kCellsLds =
 
 template <int WPI>
 __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
-    ChainW W, const float *__restrict__ state0, float *__restrict__ state_final, const float *__restrict__ x,
+    ChainW W, const float *state0, float *state_final,  // may alias (read whole before written)
+    const float *__restrict__ x,
     const double *__restrict__ pc, int B, int T, float c, float dt, float *__restrict__ traj,
     float *__restrict__ flux_traj, float *__restrict__ metrics) {
   constexpr int NX = 16 * WPI;

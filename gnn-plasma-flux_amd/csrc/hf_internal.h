@@ -158,6 +158,8 @@ inline hipError_t launch_chain_rollout(const ChainW &w, const float *state0, flo
 
 // Per-step channel MSE between two trajectories [B][T+1][3][nx] -> [B][T+1][3].
 hipError_t launch_traj_mse(const float *a, const float *b, int B, int T1, int nx, float *mse, hipStream_t s);
+hipError_t launch_rollout_summary(const float *met, const float *mse, const float *met_ref, int B, int T,
+                                  float *summary, float *drift, hipStream_t s);
 
 // One FV + Poisson update (any nx).  face_flux != nullptr => hybrid update
 // with that F; nullptr => classical (F = n*u, viscosity).  IC strides in floats.

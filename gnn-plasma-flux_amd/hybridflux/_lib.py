@@ -21,6 +21,10 @@ HF_WDTYPE_F32 = 0
 HF_WDTYPE_BF16 = 1
 HF_WDTYPE_F16X3 = 2
 HF_NUM_METRICS = 4
+HF_NUM_SUMMARY = 8
+HF_OP_STEP = 0
+HF_OP_RUN = 1
+HF_OP_COMPARE = 2
 
 # name -> (restype, argtypes); mirrors include/hybridflux.h exactly.
 SIGNATURES = {
@@ -54,12 +58,18 @@ SIGNATURES = {
     "hf_poisson_plan_len": (c_int, [c_int]),
     "hf_poisson_coeffs": (c_int, [c_int, c_double, c_void_p]),
     "hf_poisson": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "hf_run_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int]),
     "hf_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                        c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+                        c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "hf_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                       c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+                       c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                       c_void_p]),
     "hf_run_compare": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                               c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+                               c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                               c_void_p]),
+    "hf_traj_metrics": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "hf_traj_mse": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "hf_rollout_summary": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None
@@ -88,6 +98,33 @@ def lib():
             f.argtypes = args
         _lib = h
     return _lib
+
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+
+
+def version():
+    """hf_version() of the loaded library: "hybridflux <ver> gfx950 src:<hash>"."""
+    return lib().hf_version().decode()
+
+
+def source_hash():
+    """The hash the Makefile embeds (SRC_HASH): sha256 prefix of SRCS, HDRS and the
+    Makefile, in that order, recomputed from the tree (None when the sources are absent)."""
+    import hashlib
+    import re
+    mk = os.path.join(CSRC, "Makefile")
+    if not os.path.exists(mk):
+        return None
+    text = open(mk).read()
+    files = []
+    for var in ("SRCS", "HDRS"):
+        files += re.search(rf"^{var} := (.*)$", text, flags=re.M).group(1).split()
+    h = hashlib.sha256()
+    for f in files + ["Makefile"]:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def check(rc):

@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import HF_NUM_METRICS, check, lib, ptr
+from ._lib import HF_NUM_METRICS, HF_OP_COMPARE, HF_OP_RUN, HF_OP_STEP, check, lib, ptr
 
 PARAM_ORDER_DOC = "input_mlp.0.{weight,bias}, update_mlps.<l>.0.{weight,bias}, edge_mlp.0.*, edge_mlp.2.*"
 
@@ -132,7 +132,24 @@ def _state(t, nx):
     return t.contiguous()
 
 
-def step(model, grid, state, flux_face=False, metrics=False):
+def workspace(op, B, nx, T, dev, given=None):
+    """Scratch for the generic (non-fused) sequencing of hf_step / hf_run /
+    hf_run_compare: the caller's uint8 device tensor (checked), or one from
+    torch's stream-ordered caching allocator, so no hipMalloc runs inside a
+    rollout.  Returns (tensor or None, bytes)."""
+    nbytes = int(lib().hf_run_workspace_bytes(op, B, nx, T))
+    if nbytes < 0:
+        raise ValueError(f"bad workspace query (op={op}, B={B}, nx={nx}, T={T})")
+    if given is not None:
+        if not (given.is_cuda and given.device == dev and given.numel() * given.element_size() >= nbytes):
+            raise ValueError(f"workspace must be a device tensor of >= {nbytes} bytes on {dev}")
+        return given, given.numel() * given.element_size()
+    if nbytes == 0:
+        return None, 0
+    return torch.empty(nbytes, dtype=torch.uint8, device=dev), nbytes
+
+
+def step(model, grid, state, flux_face=False, metrics=False, ws=None):
     """One hybrid (model) or classical (model=None) step for state [B,3,nx]."""
     state = _state(state, grid.nx)
     B, dev = state.shape[0], state.device
@@ -140,9 +157,10 @@ def step(model, grid, state, flux_face=False, metrics=False):
     F = torch.empty(B, grid.nx, device=dev) if flux_face else None
     M = torch.empty(B, HF_NUM_METRICS, device=dev) if metrics else None
     x, pc = grid.on(dev)
+    w, wb = workspace(HF_OP_STEP, B, grid.nx, 1, dev, ws)
     with torch.cuda.device(dev):
         check(lib().hf_step(model.handle if model else None, ptr(state), ptr(out), ptr(x), ptr(pc), B,
-                            grid.nx, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(F), ptr(M),
+                            grid.nx, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(F), ptr(M), ptr(w), wb,
                             stream_of(dev)))
     return out, F, M
 
@@ -157,9 +175,10 @@ def _buf(want, given, shape, dev):
     return torch.empty(shape, device=dev) if want else None
 
 
-def run(model, grid, state0, T, traj=True, flux=False, metrics=False, out=None):
+def run(model, grid, state0, T, traj=True, flux=False, metrics=False, out=None, ws=None):
     """T-step rollout; returns dict(final, traj [B,T+1,3,nx], flux [B,T,nx], metrics [B,T+1,4]).
-    traj/flux/metrics may be bools or preallocated tensors (kept out of timed regions)."""
+    traj/flux/metrics may be bools or preallocated tensors, and ws a preallocated
+    workspace (kept out of timed regions).  out may be state0 itself."""
     state0 = _state(state0, grid.nx)
     B, dev = state0.shape[0], state0.device
     T = int(T)
@@ -168,29 +187,31 @@ def run(model, grid, state0, T, traj=True, flux=False, metrics=False, out=None):
     fl = _buf(flux, flux, (B, T, grid.nx), dev)
     me = _buf(metrics, metrics, (B, T + 1, HF_NUM_METRICS), dev)
     x, pc = grid.on(dev)
+    w, wb = workspace(HF_OP_RUN, B, grid.nx, T, dev, ws)
     with torch.cuda.device(dev):
         check(lib().hf_run(model.handle if model else None, ptr(state0), ptr(final), ptr(x), ptr(pc), B,
                            grid.nx, T, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(tr), ptr(fl),
-                           ptr(me), stream_of(dev)))
+                           ptr(me), ptr(w), wb, stream_of(dev)))
     return {"final": final, "traj": tr, "flux": fl, "metrics": me}
 
 
-def run_compare(model, grid, state0, T, metrics=True):
+def run_compare(model, grid, state0, T, metrics=True, out=None, ws=None):
     """Hybrid rollout and its classical twin from the same ICs, scored per step
     (scripts/evaluation/evaluate_multi_ic.py:21-94).  Returns dict(final,
     mse [B,T+1,3] (n,u,E), metrics [B,T+1,4], metrics_classical [B,T+1,4])."""
     state0 = _state(state0, grid.nx)
     B, dev = state0.shape[0], state0.device
     T = int(T)
-    final = torch.empty_like(state0)
+    final = torch.empty_like(state0) if out is None else out
     mse = torch.empty(B, T + 1, 3, device=dev)
     me = torch.empty(B, T + 1, HF_NUM_METRICS, device=dev) if metrics else None
     mc = torch.empty(B, T + 1, HF_NUM_METRICS, device=dev) if metrics else None
     x, pc = grid.on(dev)
+    w, wb = workspace(HF_OP_COMPARE, B, grid.nx, T, dev, ws)
     with torch.cuda.device(dev):
         check(lib().hf_run_compare(model.handle, ptr(state0), ptr(final), ptr(x), ptr(pc), B, grid.nx, T,
                                    grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(mse), ptr(me), ptr(mc),
-                                   stream_of(dev)))
+                                   ptr(w), wb, stream_of(dev)))
     return {"final": final, "mse": mse, "metrics": me, "metrics_classical": mc}
 
 
@@ -289,3 +310,57 @@ def poisson(grid, n):
     with torch.cuda.device(n.device):
         check(lib().hf_poisson(ptr(n), grid.nx, ptr(E), grid.nx, ptr(pc), B, grid.nx, stream_of(n.device)))
     return E
+
+
+def _series(t, shape_tail, what):
+    require_device(t, what)
+    if t.dtype != torch.float32 or tuple(t.shape[2:]) != shape_tail or not t.is_contiguous():
+        raise ValueError(f"{what} must be contiguous float32 [B,T+1,{','.join(map(str, shape_tail))}], "
+                         f"got {tuple(t.shape)} {t.dtype}")
+    return t
+
+
+def traj_metrics(traj):
+    """Metric series [B,T1,4] of trajectories [B,T1,3,nx] (hf_traj_metrics)."""
+    require_device(traj, "traj")
+    traj = traj.to(torch.float32).contiguous()
+    B, T1, _, nx = traj.shape
+    out = torch.empty(B, T1, HF_NUM_METRICS, device=traj.device)
+    with torch.cuda.device(traj.device):
+        check(lib().hf_traj_metrics(ptr(traj), B, T1, nx, ptr(out), stream_of(traj.device)))
+    return out
+
+
+def traj_mse(a, b):
+    """Per-step channel MSE [B,T1,3] of two trajectories [B,T1,3,nx] (hf_traj_mse)."""
+    require_device(a, "traj a")
+    require_device(b, "traj b")
+    a, b = a.to(torch.float32).contiguous(), b.to(device=a.device, dtype=torch.float32).contiguous()
+    if a.shape != b.shape or a.dim() != 4 or a.shape[2] != 3:
+        raise ValueError(f"trajectories must both be [B,T1,3,nx], got {tuple(a.shape)} and {tuple(b.shape)}")
+    B, T1, _, nx = a.shape
+    out = torch.empty(B, T1, 3, device=a.device)
+    with torch.cuda.device(a.device):
+        check(lib().hf_traj_mse(ptr(a), ptr(b), B, T1, nx, ptr(out), stream_of(a.device)))
+    return out
+
+
+def rollout_summary(metrics, mse=None, metrics_ref=None, drift=False):
+    """hf_rollout_summary: (summary [B,8], drift [B,T+1,4] or None); fields in
+    include/hybridflux.h (HF_NUM_SUMMARY)."""
+    metrics = _series(metrics, (HF_NUM_METRICS,), "metrics")
+    B, T1 = metrics.shape[:2]
+    dev = metrics.device
+    if mse is not None:
+        mse = _series(mse, (3,), "mse")
+    if metrics_ref is not None:
+        metrics_ref = _series(metrics_ref, (HF_NUM_METRICS,), "metrics_ref")
+    for o in (mse, metrics_ref):
+        if o is not None and (o.shape[:2] != (B, T1) or o.device != dev):
+            raise ValueError("metric series must share [B,T+1] and the device")
+    summ = torch.empty(B, _lib.HF_NUM_SUMMARY, device=dev)
+    dr = torch.empty(B, T1, 4, device=dev) if drift else None
+    with torch.cuda.device(dev):
+        check(lib().hf_rollout_summary(ptr(metrics), ptr(mse), ptr(metrics_ref), B, T1 - 1, ptr(summ), ptr(dr),
+                                       stream_of(dev)))
+    return summ, dr

@@ -80,16 +80,19 @@ class HybridSolver:
                                 metrics=metrics)
         return (out, F, M) if (return_flux or metrics) else out
 
-    def compare_batch(self, states0, n_steps, metrics=True):
+    def compare_batch(self, states0, n_steps, metrics=True, out=None, ws=None):
         """Roll B ICs out with this solver AND with the classical BaselineSolver
         (same dt, nu = 1e-3 as BaselineSolver's default) in one launch and score
         them per step.  Returns dict(final, mse [B,T+1,3] for (n,u,E),
         metrics, metrics_classical).  mse.sum(-1).mean(-1) is the per-IC number
         of scripts/evaluation/evaluate_multi_ic.py:88-94."""
-        return engine.run_compare(self._dm(), self.grid, self._upload(states0), n_steps, metrics=metrics)
+        return engine.run_compare(self._dm(), self.grid, self._upload(states0), n_steps, metrics=metrics, out=out,
+                                  ws=ws)
 
-    def run_batch(self, states0, n_steps, traj=True, flux=False, metrics=False, out=None):
+    def run_batch(self, states0, n_steps, traj=True, flux=False, metrics=False, out=None, ws=None):
         """Rollout of B ICs: dict(final [B,3,nx], traj [B,T+1,3,nx] | None,
-        flux [B,T,nx] | None, metrics [B,T+1,4] | None), all on the device."""
+        flux [B,T,nx] | None, metrics [B,T+1,4] | None), all on the device.
+        out (may be states0 itself) and ws (engine.workspace) are optional
+        preallocated buffers, so a timed loop allocates nothing."""
         return engine.run(self._dm(), self.grid, self._upload(states0), n_steps, traj=traj, flux=flux,
-                          metrics=metrics, out=out)
+                          metrics=metrics, out=out, ws=ws)

@@ -47,15 +47,46 @@ def gather_ic_rows(local, n_total, group=None):
     return out.to(local.device) if stage else out
 
 
-def sharded_rollout(run_local, make_ics, seed0, n_total, T, group=None):
+def max_over_ranks(value, group=None, device="cpu"):
+    """The job's wall time: the MAX of each rank's value (bench.py's timing rule:
+    the slowest shard ends the job).  float64 all_reduce on `device` (the
+    rank's GPU for RCCL, the CPU for gloo); the value itself when not distributed."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def gather_rollout(res, n_total, group=None):
+    """The end-of-rollout exchange of an IC-sharded job: this rank's per-step
+    metric series res['metrics'] [b, T+1, K] (and the MSE series res['mse']
+    [b, T+1, 3] when the rollout was scored against the classical twin) are
+    summarised on the device (hf_rollout_summary: first non-finite step, drifts,
+    MSE totals), then series and summaries are all_gathered in global IC order.
+    Returns dict(metrics [n_total, T+1, K], summary [n_total, 8], mse or None)."""
+    from . import engine
+    summ, _ = engine.rollout_summary(res["metrics"], res.get("mse"), res.get("metrics_classical"))
+    out = {"metrics": gather_ic_rows(res["metrics"], n_total, group),
+           "summary": gather_ic_rows(summ, n_total, group), "mse": None}
+    if res.get("mse") is not None:
+        out["mse"] = gather_ic_rows(res["mse"], n_total, group)
+    return out
+
+
+def sharded_rollout(run_local, make_ics, seed0, n_total, T, group=None, summarize=True):
     """Run this rank's shard and gather every IC's metrics.
 
     run_local(ics, T) -> dict with 'metrics' [b, T+1, K] (device tensor) and 'final'.
     make_ics(seeds) -> [b, 3, nx] states for those seeds.
-    Returns (local_result, global_metrics [n_total, T+1, K]).
+    Returns (local_result, gathered): gathered is gather_rollout's dict when
+    summarize (a HIP device is needed for the summary kernel), else the
+    gathered metrics [n_total, T+1, K] alone.
     """
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     ics = make_ics(shard_seeds(seed0, n_total, world, rank))
     res = run_local(ics, T)
+    if summarize:
+        return res, gather_rollout(res, n_total, group)
     return res, gather_ic_rows(res["metrics"], n_total, group)

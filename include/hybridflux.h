@@ -46,15 +46,37 @@ extern "C" {
 #define HF_WDTYPE_F16X3 2   /* fp32-accurate: fp16 hi+lo split of weights and
                                activations, 3 MFMA products, f32 accumulate   */
 
-/* Number of per-(IC, step) rollout metrics written by hf_run / hf_fv_step:
- * [0] energy 0.5*mean(u^2+E^2)  [1] charge mean(n)  [2] 1.0 if every state
- * value is finite else 0.0  [3] max |n-1| over the chain.
- * (scripts/evaluation/evaluate_all.py:324-334, evaluate_long_rollout.py:331) */
+/* Number of per-(IC, step) rollout metrics written by hf_run / hf_step /
+ * hf_run_compare / hf_traj_metrics:
+ * [0] energy 0.5*mean(u^2+E^2)   (scripts/evaluation/evaluate_all.py:135,
+ *                                  evaluate_long_rollout.py:38-42)
+ * [1] charge mean(n)              (evaluate_all.py:141)
+ * [2] 1.0 if every state value is finite else 0.0
+ *                                 (evaluate_long_rollout.py:57-60)
+ * [3] max |n-1| over the chain (NaN when [2] is 0; no reference counterpart).
+ * Sums are float64, rounded to float32 once. */
 #define HF_NUM_METRICS 4
+
+/* Per-IC rollout summary written by hf_rollout_summary:
+ * [0] exploded_at: first step t >= 1 whose state is not finite, -1 if none
+ *     (evaluate_long_rollout.py:53-66)
+ * [1] actual_steps: exploded_at - 1, or T (evaluate_long_rollout.py:74)
+ * [2] final energy drift |e[a] - e[0]|, a = actual_steps
+ *     (evaluate_long_rollout.py:72; evaluate_all.py:137,157)
+ * [3] final charge drift |q[a] - q[0]| (evaluate_all.py:143,158)
+ * [4] final_mse = mse_total[T], mse_total = mse_n + mse_u + mse_E
+ *     (evaluate_all.py:132,155); NaN without an MSE series
+ * [5] mean_mse = mean over t = 0..T of mse_total (evaluate_all.py:156,
+ *     evaluate_multi_ic.py:91-94); NaN without an MSE series
+ * [6], [7] final energy / charge drift of the reference (classical) series
+ *     at T (energy_drift_true, charge_drift_true); NaN without one. */
+#define HF_NUM_SUMMARY 8
 
 typedef struct hf_model *hf_model_t;
 
-/* Library version string, e.g. "hybridflux 0.1 gfx950". */
+/* Library version string, "hybridflux <ver> gfx950 src:<16 hex>": the hex is a
+ * sha256 prefix of the sources, headers and Makefile the library was built
+ * from, so a record that prints it names the exact sources that ran. */
 const char *hf_version(void);
 
 /* Thread-local message describing the last failure on this thread. */
@@ -190,6 +212,20 @@ int hf_poisson(const float *dev_n, int ld_n, float *dev_E, int ld_E,
                const double *dev_c, int B, int nx, void *stream);
 
 /*
+ * Scratch of the generic (non-fused) sequencing.  hf_step, hf_run and
+ * hf_run_compare take (dev_workspace, workspace_bytes): a device buffer of at
+ * least hf_run_workspace_bytes(op, B, nx, T) bytes that the call may use as
+ * scratch until the work it enqueued has run; the caller keeps it alive and
+ * unshared until then.  dev_workspace == NULL makes the call allocate its
+ * scratch stream-ordered (hipMallocAsync / hipFreeAsync on `stream`).  The
+ * fused paths (nx in {16,32,48,64} with a model) use no scratch.
+ */
+#define HF_OP_STEP 0
+#define HF_OP_RUN 1
+#define HF_OP_COMPARE 2
+int64_t hf_run_workspace_bytes(int op, int B, int nx, int T);
+
+/*
  * One timestep for B ICs (state_in -> state_out, may not alias).
  * model != NULL: HybridSolver.step (src/hybrid_solver.py:34-64):
  *   GNN flux -> symmetrise -> FV continuity -> Burgers u (no viscosity) -> Poisson.
@@ -200,16 +236,19 @@ int hf_poisson(const float *dev_n, int ld_n, float *dev_E, int ld_E,
  * dev_x [nx]: float32 cell centres (node feature x); dev_c: Poisson coeffs.
  * dev_flux_face [B][nx] (may be NULL): the F used this step (F_n classically).
  * dev_metrics [B][HF_NUM_METRICS] (may be NULL) for state_out.
+ * nx <= 6144 (LDS bound of the FV/Poisson kernel; larger nx -> HF_EUNSUPPORTED).
  */
 int hf_step(hf_model_t model, const float *dev_state_in, float *dev_state_out,
             const float *dev_x, const double *dev_c, int B, int nx,
             float c, float dt, float nu, float dx2,
-            float *dev_flux_face, float *dev_metrics, void *stream);
+            float *dev_flux_face, float *dev_metrics,
+            void *dev_workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * T-step rollout (HybridSolver.run src/hybrid_solver.py:66-73 when model !=
  * NULL, BaselineSolver.run src/baseline_solver.py:103-118 when NULL), batched.
- * dev_state0 [B][3][nx] -> dev_state_final [B][3][nx].
+ * dev_state0 [B][3][nx] -> dev_state_final [B][3][nx]; the two may alias
+ * (the same buffer holds the initial and, after the call, the final states).
  * dev_traj [B][T+1][3][nx] (may be NULL) receives every state incl. t=0.
  * dev_flux_traj [B][T][nx] (may be NULL) receives the face flux of each step
  *   (the classical run's `fluxes`).
@@ -220,7 +259,8 @@ int hf_step(hf_model_t model, const float *dev_state_in, float *dev_state_out,
 int hf_run(hf_model_t model, const float *dev_state0, float *dev_state_final,
            const float *dev_x, const double *dev_c, int B, int nx, int T,
            float c, float dt, float nu, float dx2,
-           float *dev_traj, float *dev_flux_traj, float *dev_metrics, void *stream);
+           float *dev_traj, float *dev_flux_traj, float *dev_metrics,
+           void *dev_workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * Hybrid rollout scored against the classical solver from the same ICs, in
@@ -229,16 +269,42 @@ int hf_run(hf_model_t model, const float *dev_state0, float *dev_state_final,
  * state0, HybridSolver.run from state0, per-step channel MSE; and the
  * energy/charge series of scripts/evaluation/evaluate_all.py:118-159).
  * The classical twin uses the same dt/dx and viscosity `nu`.
- * dev_mse [B][T+1][3] (required): mean over cells of (hybrid - classical)^2
- *   for n, u, E at every step (step 0 is 0).
+ * dev_mse [B][T+1][3] float32 (required): mean over cells of
+ *   (hybrid - classical)^2 for n, u, E at every step (step 0 is 0), summed in
+ *   float64 and rounded once.
  * dev_metrics / dev_metrics_classical [B][T+1][HF_NUM_METRICS] (may be NULL).
- * dev_state_final receives the hybrid final state.  For nx in {16,32,48,64}
- * both solvers advance inside the one persistent kernel.
+ * dev_state_final receives the hybrid final state; it may alias dev_state0.
+ * For nx in {16,32,48,64} both solvers advance inside the one persistent kernel.
  */
 int hf_run_compare(hf_model_t model, const float *dev_state0, float *dev_state_final,
                    const float *dev_x, const double *dev_c, int B, int nx, int T,
                    float c, float dt, float nu, float dx2, float *dev_mse,
-                   float *dev_metrics, float *dev_metrics_classical, void *stream);
+                   float *dev_metrics, float *dev_metrics_classical,
+                   void *dev_workspace, int64_t workspace_bytes, void *stream);
+
+/*
+ * Metric series of recorded trajectories (the host-side scoring of
+ * scripts/evaluation/evaluate_all.py:118-159 and evaluate_multi_ic.py:88-94,
+ * on the device):
+ * hf_traj_metrics: dev_traj [B][T1][3][nx] -> dev_metrics [B][T1][HF_NUM_METRICS].
+ * hf_traj_mse: per-step channel MSE of two trajectories [B][T1][3][nx] ->
+ *   dev_mse [B][T1][3] (n, u, E), float64 sums rounded once.
+ */
+int hf_traj_metrics(const float *dev_traj, int B, int T1, int nx, float *dev_metrics, void *stream);
+int hf_traj_mse(const float *dev_traj_a, const float *dev_traj_b, int B, int T1, int nx, float *dev_mse,
+                void *stream);
+
+/*
+ * Per-IC summary of a T-step rollout from its metric series (SURVEY.md 8f
+ * rank 1; fields at HF_NUM_SUMMARY).  dev_metrics [B][T+1][HF_NUM_METRICS]
+ * (required), dev_mse [B][T+1][3] (may be NULL), dev_metrics_ref
+ * [B][T+1][HF_NUM_METRICS] (may be NULL: the classical twin's series).
+ * dev_summary [B][HF_NUM_SUMMARY] (required); dev_drift [B][T+1][4] (may be
+ * NULL): |energy_t - energy_0|, |charge_t - charge_0| of the rollout, then
+ * of the reference series (NaN without one).
+ */
+int hf_rollout_summary(const float *dev_metrics, const float *dev_mse, const float *dev_metrics_ref, int B,
+                       int T, float *dev_summary, float *dev_drift, void *stream);
 
 #ifdef __cplusplus
 }

@@ -44,8 +44,24 @@ baselines.npz         the reference's other rollout models
                       graph, and 10-step rollouts of ICs 1000..1003 with the
                       loops of scripts/evaluation/evaluate_multi_ic.py:45-83.
 
+metrics.npz           the reference's rollout scoring:
+                      evaluate_all.compute_metrics (scripts/evaluation/
+                      evaluate_all.py:118-159) of the hybrid W1_r1 rollouts of
+                      hybrid_W1_r1_nx64.npz against the classical ones of
+                      classical.npz (seeds 1000..1015, T=30);
+                      evaluate_multi_ic.evaluate_model_on_ic('hybrid', W1_r1, 1,
+                      seed, 30) for the same seeds (evaluate_multi_ic.py:21-94);
+                      evaluate_long_rollout.evaluate_long_rollout (evaluate_long_
+                      rollout.py:18-81) on seed 2000 for W1_r1 (300 steps) and for
+                      W1_r1 with edge_mlp.2.weight scaled x30 (100 steps) and x100
+                      (60 steps): exploded_at, actual_steps, the drift series.
+                      Those scripts build HybridSolver(path, r) with the
+                      reference's default device='cuda'; they are run with the
+                      class bound to device='cpu' (this container has no GPU).
+
     python tests/golden/make_golden.py grads       # regenerate grads.npz only
     python tests/golden/make_golden.py baselines   # regenerate baselines.npz only
+    python tests/golden/make_golden.py metrics     # regenerate metrics.npz only
 """
 import json
 import os
@@ -363,7 +379,56 @@ def make_baselines():
     save("baselines.npz", **arrs)
 
 
+LONG_ROLLOUTS = ((1.0, 300), (30.0, 100), (100.0, 60))  # (edge_mlp.2.weight scale, steps), seed 2000
+
+
+def make_metrics():
+    import functools
+
+    sys.path.insert(0, str(REF / "scripts" / "evaluation"))
+    import evaluate_all
+    import evaluate_long_rollout
+    import evaluate_multi_ic
+
+    cpu_solver = functools.partial(HybridSolver, device="cpu")
+    evaluate_long_rollout.HybridSolver = cpu_solver
+    evaluate_multi_ic.HybridSolver = cpu_solver
+    arrs = {}
+    hyb = np.load(OUT / "hybrid_W1_r1_nx64.npz")
+    cla = np.load(OUT / "classical.npz")
+    assert list(hyb["seeds"]) == list(range(1000, 1016))
+    per_ic = [evaluate_all.compute_metrics(hyb["states"][i], cla["b16_states"][i]) for i in range(16)]
+    for k in per_ic[0]:
+        arrs[f"cm_{k}"] = np.array([m[k] for m in per_ic], dtype=np.float64)
+    w1 = np.load(OUT / "weights_W1_r1.npz")
+    with tempfile.TemporaryDirectory() as wd:
+        pt = os.path.join(wd, "W1_r1.pt")
+        write_pt(OUT / "weights_W1_r1.npz", pt)
+        arrs["multi_ic_seeds"] = np.arange(1000, 1016)
+        arrs["multi_ic_mse"] = np.array([evaluate_multi_ic.evaluate_model_on_ic("hybrid", pt, 1, s, 30)
+                                         for s in range(1000, 1016)])
+        for i, (scale, steps) in enumerate(LONG_ROLLOUTS):
+            p = os.path.join(wd, f"scaled{i}.pt")
+            sd = {k: torch.from_numpy(w1[k].copy()) for k in w1.files}
+            sd["edge_mlp.2.weight"] = sd["edge_mlp.2.weight"] * scale
+            torch.save(sd, p)
+            r = evaluate_long_rollout.evaluate_long_rollout(p, 1, 2000, n_steps=steps)
+            drift = np.full(steps + 1, np.nan)
+            drift[: len(r["energy_drift_pred"])] = r["energy_drift_pred"]
+            base = np.array(r["energy_drift_baseline"])
+            arrs[f"long{i}_scale"] = np.float32(scale)
+            arrs[f"long{i}_steps"] = np.int64(steps)
+            arrs[f"long{i}_exploded_at"] = np.int64(-1 if r["exploded_at"] is None else r["exploded_at"])
+            arrs[f"long{i}_actual_steps"] = np.int64(r["actual_steps"])
+            arrs[f"long{i}_energy_drift_pred"] = drift
+            arrs[f"long{i}_energy_drift_baseline"] = base
+    save("metrics.npz", **arrs)
+
+
 def main():
+    if sys.argv[1:] == ["metrics"]:
+        make_metrics()
+        return
     if sys.argv[1:] == ["grads"]:
         make_grads()
         return
@@ -384,6 +449,7 @@ def main():
         make_random_graph()
         make_grads()
         make_baselines()
+        make_metrics()
     meta = {"torch": torch.__version__, "numpy": np.__version__,
             "reference": "shanedirksen/gnn-plasma-flux @ /root/reference (2026-01-02 snapshot)",
             "generator": "tests/golden/make_golden.py"}

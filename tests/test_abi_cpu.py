@@ -38,6 +38,13 @@ def test_version_and_codes():
         assert getattr(_lib, name) == val
 
 
+def test_library_built_from_these_sources():
+    """hf_version() carries the hash of the sources the .so was built from; it must
+    be this tree's, so no record is ever produced by a stale binary."""
+    v = _lib.version()
+    assert v.split("src:")[-1] == _lib.source_hash(), f"stale libhybridflux.so ({v}); rebuild with make"
+
+
 def test_param_count_matches_reference_model():
     lib = _lib.lib()
     w = golden("weights_W0.npz")

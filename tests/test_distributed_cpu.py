@@ -62,11 +62,16 @@ def _worker(rank, world, port, out_dir):
         m, S = _oracle_local(seeds)
         return {"metrics": m, "final": torch.from_numpy(S[:, -1])}
 
-    res, gathered = sharded_rollout(run_local, make_ics, 1000, N_TOTAL, T)
-    t = torch.tensor([float(rank + 1)])
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)           # bench.py's max-over-ranks timing
-    torch.save({"gathered": gathered, "max": t.item(), "local_n": res["metrics"].shape[0]},
-               os.path.join(out_dir, f"rank{rank}.pt"))
+    res, gathered = sharded_rollout(run_local, make_ics, 1000, N_TOTAL, T, summarize=False)
+    # the other per-IC rows bench.py gathers: an [b, 8] summary and an [b, T+1, 3] series
+    lo, hi = shard_bounds(N_TOTAL, world, rank)
+    summ = torch.arange(lo * 8, hi * 8, dtype=torch.float32).reshape(-1, 8)
+    ser = torch.arange(lo * (T + 1) * 3, hi * (T + 1) * 3, dtype=torch.float32).reshape(-1, T + 1, 3)
+    g_summ, g_ser = gather_ic_rows(summ, N_TOTAL), gather_ic_rows(ser, N_TOTAL)
+    from hybridflux.rollout import max_over_ranks
+    mx = max_over_ranks(0.25 * (rank + 1))               # bench.py's max-over-ranks timing
+    torch.save({"gathered": gathered, "max": mx, "local_n": res["metrics"].shape[0], "summ": g_summ,
+                "series": g_ser}, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -77,10 +82,13 @@ def test_two_rank_gloo_sharded_rollout(tmp_path):
     want, _ = _oracle_local(list(range(1000, 1000 + N_TOTAL)))
     for r in range(2):
         d = torch.load(tmp_path / f"rank{r}.pt", weights_only=True)
-        assert d["max"] == 2.0
+        assert d["max"] == 0.5
         assert d["local_n"] == (3 if r == 0 else 2)
         assert d["gathered"].shape == (N_TOTAL, T + 1, 4)
         assert torch.equal(d["gathered"], want)   # same ICs, same order as one process
+        assert torch.equal(d["summ"], torch.arange(N_TOTAL * 8, dtype=torch.float32).reshape(N_TOTAL, 8))
+        assert torch.equal(d["series"], torch.arange(N_TOTAL * (T + 1) * 3, dtype=torch.float32)
+                           .reshape(N_TOTAL, T + 1, 3))
 
 
 def test_gather_single_process_passthrough():

@@ -141,3 +141,73 @@ def test_oracle_pure_gnn_and_pinn_vs_reference():
                 s = O.pinn_forward(pn, s[None])[0]
                 traj.append(s.numpy())
             np.testing.assert_allclose(np.array(traj), b["pinn_traj"][j], atol=1e-5, rtol=1e-5)
+
+
+# ------------------------------------------------------------ rollout scoring (8f rank 1)
+def test_oracle_compute_metrics_vs_reference():
+    """oracle.compute_metrics == the reference's evaluate_all.compute_metrics
+    (scripts/evaluation/evaluate_all.py:118-159) on its own hybrid-vs-classical
+    rollouts, key by key, bit for bit (same float32 numpy arithmetic)."""
+    m = golden("metrics.npz")
+    hyb, cla = golden("hybrid_W1_r1_nx64.npz"), golden("classical.npz")
+    got = O.compute_metrics(hyb["states"], cla["b16_states"])
+    for k, v in got.items():
+        np.testing.assert_array_equal(np.asarray(v, np.float64), m[f"cm_{k}"], err_msg=k)
+
+
+def test_oracle_multi_ic_mse_vs_reference():
+    """mean over t of mse_total (scripts/evaluation/evaluate_multi_ic.py:88-94) from
+    the oracle's hybrid and classical rollouts == evaluate_model_on_ic('hybrid', ...)."""
+    m = golden("metrics.npz")
+    w = golden("weights_W1_r1.npz")
+    grid = O.Grid(64)
+    ics = np.stack([O.initial_condition(grid, int(s)) for s in m["multi_ic_seeds"]])
+    S, _ = O.hybrid_run(O.params_from({k: w[k] for k in w.files}), grid, ics, 30)
+    C = np.stack([O.classical_run(grid, ic, 30)[0] for ic in ics])
+    got = O.compute_metrics(S, C)["mean_mse"]
+    np.testing.assert_allclose(got, m["multi_ic_mse"], rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_oracle_long_rollout_explosion_vs_reference(i):
+    """Explosion tracking of scripts/evaluation/evaluate_long_rollout.py:18-81 (seed
+    2000; W1_r1 and W1_r1 with edge_mlp.2.weight scaled): the oracle finds the same
+    first non-finite step and the same energy-drift series."""
+    m = golden("metrics.npz")
+    w = {k: v for k, v in golden("weights_W1_r1.npz").items()}
+    w["edge_mlp.2.weight"] = w["edge_mlp.2.weight"] * m[f"long{i}_scale"]
+    grid = O.Grid(64)
+    ex, actual, drift = O.long_rollout(O.params_from(w), grid, O.initial_condition(grid, 2000),
+                                       int(m[f"long{i}_steps"]))
+    assert (-1 if ex is None else ex) == int(m[f"long{i}_exploded_at"])
+    assert actual == int(m[f"long{i}_actual_steps"])
+    want = m[f"long{i}_energy_drift_pred"][: actual + 1]
+    np.testing.assert_array_equal(drift, want)
+
+
+def test_bf16_emulation_structure():
+    """oracle.hybrid_flux_edge_bf16 without its activation rounding is the float32
+    forward on bf16-rounded weights (same edge order, P/Q split, halved W_b,
+    aggregation): pins the emulation the bf16 kernels are held to."""
+    w = dict(golden("weights_W1_r2.npz"))
+    grid = O.Grid(64)
+    ics = np.stack([O.initial_condition(grid, s) for s in (1000, 1001, 1002)])
+    pb = O.params_from(O.bf16_weights(w))
+    want = O.hybrid_flux_edge(pb, grid, ics)
+    got = O.hybrid_flux_edge_bf16(O.params_from(w), grid, ics, act_round=lambda a: a)
+    np.testing.assert_allclose(got, want, atol=2e-6, rtol=0)
+    full = O.hybrid_flux_edge_bf16(O.params_from(w), grid, ics)
+    assert 1e-4 < np.abs(full - want).max() < 1e-2   # the activation rounding is what differs
+
+
+def test_bf16_fixture_reproducible():
+    """tests/golden/bf16_nx1024.npz (made by make_oracle_vectors.py) is the
+    oracle's current output (first-step fluxes and one step)."""
+    g = golden("bf16_nx1024.npz")
+    w = dict(golden("weights_W1_r2.npz"))
+    G = O.Grid(1024, dt=3.125e-4)
+    ics = g["states_emul"][:, 0]
+    fe = O.hybrid_flux_edge_bf16(O.params_from(w), G, ics)
+    np.testing.assert_array_equal(fe, g["flux_edge0_emul"])
+    s1, _ = O.hybrid_step(O.params_from(w), G, ics, O.hybrid_flux_edge_bf16)
+    np.testing.assert_array_equal(s1, g["states_emul"][:, 1])

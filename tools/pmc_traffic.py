@@ -1,7 +1,12 @@
 """Turn the FETCH_SIZE / WRITE_SIZE rocprofv3 passes of `bench.py` into the
 per-launch HBM traffic that bench.py reports as roofline.traffic.
 
-    python tools/pmc_traffic.py TAG STEPS ICS NX TRAJ(0|1) > profiles/pmc_traffic.json
+    python tools/pmc_traffic.py TAG_A STEPS_A TAG_B STEPS_B ICS NX TRAJ(0|1) > profiles/pmc_traffic.json
+
+Two passes at different step counts (tools/gpu_pmc.sh TAG_A STEPS_A, then TAG_B
+STEPS_B) separate a fixed part (state, weight stream, launch) from a per-step
+part (trajectory and metric writes), so bench.py can state the traffic of a
+launch of any --steps: traffic(K) = fixed_bytes + per_step_bytes * K.
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are
 in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane)
@@ -24,17 +29,26 @@ def last_value(db, counter):
     return rows[-1]
 
 
-def main(tag, steps, ics, nx, traj):
+def traffic(tag):
     f = last_value(glob(f"gpurun_out/pmc_fetch_{tag}/*.db")[0], "FETCH_SIZE")
     w = last_value(glob(f"gpurun_out/pmc_write_{tag}/*.db")[0], "WRITE_SIZE")
-    fetch = 2 * f[1] * 1024
-    write = w[1] * 1024
-    print(json.dumps({"kernel": KERNEL, "steps": int(steps), "ics_per_gpu": int(ics), "nx": int(nx),
-                      "traj": bool(int(traj)), "fetch_bytes": fetch, "write_bytes": write,
-                      "traffic_bytes": fetch + write, "dispatch_us": f[2] / 1e3,
-                      "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({tag}); "
-                                "FETCH_SIZE x2 (gfx950 wide-load correction), KiB -> B"}, indent=1))
+    return 2 * f[1] * 1024, w[1] * 1024, f[2] / 1e3
+
+
+def main(tag_a, steps_a, tag_b, steps_b, ics, nx, traj):
+    ka, kb = int(steps_a), int(steps_b)
+    fa, wa, da = traffic(tag_a)
+    fb, wb, db = traffic(tag_b)
+    per_step = ((fb + wb) - (fa + wa)) / (kb - ka)
+    fixed = (fa + wa) - per_step * ka
+    print(json.dumps({"kernel": KERNEL, "ics_per_gpu": int(ics), "nx": int(nx), "traj": bool(int(traj)),
+                      "fixed_bytes": fixed, "per_step_bytes": per_step,
+                      "passes": {str(ka): {"fetch_bytes": fa, "write_bytes": wa, "dispatch_us": da},
+                                 str(kb): {"fetch_bytes": fb, "write_bytes": wb, "dispatch_us": db}},
+                      "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py at {ka} and {kb} steps "
+                                f"({tag_a}, {tag_b}); FETCH_SIZE x2 (gfx950 wide-load correction), KiB -> B; "
+                                "linear in steps"}, indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:6])
+    main(*sys.argv[1:8])
