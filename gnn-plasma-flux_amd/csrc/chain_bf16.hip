@@ -8,22 +8,31 @@
 // 16x16 accumulator tile holds 16 cells along the lanes, and the output tile
 // pair (2q, 2q+1) of one layer is, lane for lane, k-block q of the next
 // layer's B operand (element e of the 8-wide fragment = tile 2q + (e>>2),
-// row e&3; capi.cpp packs the weights in that k order).  The neighbour sum
-// h[i+1] + h[i-1] is taken in fp32 on the interleaved cell layout (one VALU per
-// value) and rounded into its own B fragments; the 1/deg is folded into W_b.
+// row e&3; capi.cpp packs the weights in that k order).
 //
-// Why a separate core: at 16 cycles per v_mfma_f32_16x16x32_bf16 the layer
-// epilogue (ReLU, neighbour sums, bf16 packing: ~3 VALU per activated value)
-// costs as much issue time as the matrix work, and with one wave per SIMD
-// nothing overlaps an epilogue that waits for its whole layer.  This core
-// walks each layer in OUTPUT-PAIR order (pair q = tiles 2q, 2q+1, accumulated
-// over the 4 k-blocks of h and the 4 of the neighbour sums: 64 MFMAs at
-// MT=4) and spreads the epilogue of pair q-1 over the MFMAs of pair q, one
-// fragment dword per unit of 16 MFMAs.  The new fragments of pairs 0..2 are
-// parked in LDS (the old ones still feed the layer) and read back when the
-// layer ends; the epilogue of pair 3 runs under the first three k-blocks of
-// the next layer's pair 0 (or the first readout tile), which produce nothing
-// it needs.  The readout is pipelined the same way, tile by tile.
+// Aggregation by linearity, on the output side:
+//   W_b (h[i-1] + h[i+1]) / 2 = G(i-1) + G(i+1),   G = (W_b/2) bf16(h),
+// so a layer's MFMAs read ONE activation fragment set, bf16(h): A = W_a h + b
+// and G accumulate side by side (the packer already halves W_b, exactly:
+// bf16(w/2) == bf16(w)/2), and the epilogue forms z = A + (G(i-1) + G(i+1))
+// on the interleaved cell layout (one fp32 add of the two neighbours, a plain
+// v_add or a DPP row rotation at the tile seam, then one add into A), ReLU,
+// bf16 pairs.  Against a neighbour-sum B fragment this halves the activation
+// registers; a wave fits in 256 VGPRs, so the windowed kernel runs NW = 8
+// waves: two per SIMD, which hide each other's LDS, barrier and epilogue
+// latency.  cfg4 (4096 ICs x 1024 cells) measured 35.3 % of the dense bf16
+// peak with the neighbour-sum fragment at one wave per SIMD, 37.6 % with the
+// sum as two shifted B operands (3 MFMAs per fragment, two waves per SIMD) and
+// 43.2 % in this form (profiles/r02_cfg4_core_ab.json).  The arithmetic is
+// oracle.hybrid_flux_edge_bf16 (float64-emulated f32 accumulation).
+//
+// Schedule: a layer is walked in OUTPUT-PAIR order (pair q = tiles 2q, 2q+1,
+// 4 units = the 4 k-blocks of h, 2 x 2 x MT MFMAs each) and the epilogue of
+// pair q-1 is spread over pair q's units, one fragment dword per unit.  The new
+// fragments of pairs 0..2 are parked in LDS (the old ones still feed the
+// layer) and read back when the layer ends; the epilogue of pair 3 runs under
+// the first three k-blocks of the next layer's pair 0 (or the first readout
+// tile), which produce nothing it needs.  The readout is pipelined tile by tile.
 #include "chain_common.h"
 
 namespace hf {
@@ -44,10 +53,10 @@ __device__ __forceinline__ f4 mma(const u4 &a, const u4 &b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
 }
 
-// Closes one unit's scheduling region: the next unit's 4 ds_reads first (so
-// LDS latency hides under this unit's matrix work), then one MFMA and up to NV
-// VALU (epilogue work of the previous pair) at a time.  The sched_barrier keeps
-// the next unit's reads from being picked for this unit's DS group.
+// Closes one unit's scheduling region: the unit's 4 ds_reads first, then one
+// MFMA and up to NV VALU (epilogue work of the previous pair) at a time.  The
+// sched_barrier keeps the next unit's reads from being picked for this unit's
+// DS group.
 template <int NM, int NV>
 __device__ __forceinline__ void interleave() {
   __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
@@ -59,38 +68,38 @@ __device__ __forceinline__ void interleave() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// NW = waves per workgroup sharing the weight ring; the kernels use NW = 4
-// (one wave per SIMD, up to 64 cells per wave).  NW = 8 (two waves per SIMD
-// at 191 registers, 32-cell windows) was measured for the windowed flux
-// kernel: per FLOP 7 % faster, but 32-cell windows recompute 41 % halo
-// against 19 % at 64 cells, so cfg4 ran at 2.18 M IC-steps/s against 2.41 M.
-// WMT = m-tiles per wave of the windowed flux kernel: 80-cell windows (WMT = 5,
-// 389 registers, 8 KiB chunks, the only ring that fits beside a 5-tile park)
-// recompute 13 % halo instead of 16 % but ran 2.7 % slower at cfg4.
-// UPC = units (4 fragments, 4 KiB) per ring chunk: 2 (8 KiB chunks, 4 slots)
-// or 4 (16 KiB chunks, 3 slots: half the ring barriers, +16 KiB of LDS, which
-// the windowed flux kernel has and the rollout, with its per-IC scratch, has not).
-template <int NW, int UPC = 2, int WMT = (NW == 8 ? 2 : 4)>
-struct CoreBF16T {
+// NW = waves per workgroup sharing the weight ring: 8 (two per SIMD) for the
+// flux kernels, 4 for the rollout kernel (one IC per wave beside its per-IC
+// LDS scratch).  UPC = units (4 fragments, 4 KiB) per ring chunk: 4 (16 KiB
+// chunks, 3 slots: one ring barrier per output pair) or 2 (8 KiB, 4 slots:
+// the rollout, whose scratch leaves no room for the larger ring).  WMT =
+// m-tiles per wave of the windowed flux kernel (64-cell windows).  PF = read
+// the next unit's fragments one unit ahead (16 more registers: the rollout's
+// one wave per SIMD has them; at two waves per SIMD the partner wave covers
+// the latency and the registers are what let two waves fit).
+template <int NW, int UPC, int WMT = 4, bool PF = false>
+struct CoreBF16 {
   static constexpr int kNW = NW;
   static constexpr int kUPC = UPC;
   static constexpr int kSlots = UPC == 4 ? 3 : 4;
-  static constexpr int kWinMT = WMT;  // m-tiles per wave in the windowed flux kernel
-  static constexpr int kParkMT = kWinMT;          // largest MT the park holds
+  static constexpr int kWinMT = WMT;
+  static constexpr int kParkMT = WMT;
   static constexpr int kChunkFloats = 1024 * UPC;
-  static constexpr int kKB = kH / 32;        // k-blocks per 128-wide operand
-  // parked fragments of k-blocks 0..2: [kb 3][h|agg 2][mt kParkMT][lane 64][4 dwords]
-  static constexpr int kParkFloats = 3 * 2 * kParkMT * 64 * 4;
+  static constexpr int kKB = kH / 32;
+  // parked h fragments of k-blocks 0..2: [kb 3][mt kParkMT][lane 64][4 dwords]
+  static constexpr int kParkFloats = 3 * kParkMT * 64 * 4;
   using R_t = Ring<kChunkFloats, NW, kSlots>;
 
   template <int MT>
   struct Acts {
-    u4 h[MT][kKB], a[MT][kKB];  // B fragments of h and of its neighbour sums
+    u4 h[MT][kKB];  // B fragments of bf16(h)
+  };
+  // A (= b + W_a h) and G (= (W_b/2) h) accumulators of one output pair
+  template <int MT>
+  struct Pair {
+    f4 a[MT][2], g[MT][2];
   };
 
-  // Register-prefetched weight feed: the next unit's 4 ds_read_b128 issue
-  // before this unit's MFMAs; the ring's wait + barrier for chunk p+1 precede
-  // the last unit of chunk p.  Runs continuously over forward passes.
   struct Feed {
     const float *slot;
     u4 cur[4];
@@ -101,100 +110,96 @@ struct CoreBF16T {
   }
   static __device__ __forceinline__ void begin(R_t &R, Feed &F) {
     F.slot = R.next();
-    load_unit(F, 0, R.lane);
+    if constexpr (PF) load_unit(F, 0, R.lane);
   }
+  // The 4 fragments of ring unit U (the last unit of a chunk also waits for,
+  // and releases, the next chunk).
   template <int U>
   static __device__ __forceinline__ void take(R_t &R, Feed &F, u4 (&w)[4]) {
+    if constexpr (PF) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = F.cur[i];
-    if constexpr (U == UPC - 1) F.slot = R.next();
-#ifndef HF_DIAG_NODS  // timing diagnostic only: results are wrong
-    load_unit(F, (U + 1) % UPC, R.lane);
-#endif
-  }
-
-  static __device__ __forceinline__ float *park_at(float *park, int kb, int ha, int mt, int lane) {
-    return park + (((kb * 2 + ha) * kParkMT + mt) * 64 + lane) * 4;
-  }
-
-  // Dword K (tile t = K>>1, rows 2(K&1), 2(K&1)+1) of the k-block fragments
-  // made from one output pair's accumulators: ReLU, then (AGG) the fp32
-  // neighbour sums (src/flux_gnn.py:55-59; / deg is in W_b), then bf16 pairs.
-  template <int MT, int K, bool AGG>
-  static __device__ __forceinline__ void piece(const f4 (&acc)[MT][2], u4 (&nh)[MT], u4 (&na)[MT]) {
-    constexpr int t = K >> 1, r = 2 * (K & 1);
-#ifdef HF_DIAG_NOPIECE  // timing diagnostic only: results are wrong (no epilogue VALU)
+      for (int i = 0; i < 4; ++i) w[i] = F.cur[i];
+      if constexpr (U == UPC - 1) F.slot = R.next();
+      load_unit(F, (U + 1) % UPC, R.lane);
+    } else {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) nh[mt][K] = na[mt][K] = __float_as_uint(acc[mt][t][r]);
-    return;
-#endif
-    float v0[MT], v1[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      v0[mt] = relu(acc[mt][t][r]);
-      v1[mt] = relu(acc[mt][t][r + 1]);
-      nh[mt][K] = pk_bf16(v0[mt], v1[mt]);
-    }
-    if constexpr (AGG) {
-      float s0[MT], s1[MT];
-#ifdef HF_DIAG_NONB  // timing diagnostic only: results are wrong
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) s0[mt] = v0[mt], s1[mt] = v1[mt];
-#else
-      nb_sum<MT>(v0, s0);
-      nb_sum<MT>(v1, s1);
-#endif
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) na[mt][K] = pk_bf16(s0[mt], s1[mt]);
+      for (int i = 0; i < 4; ++i) w[i] = __builtin_bit_cast(u4, ldf4(F.slot + ((4 * U + i) * 64 + R.lane) * 4));
+      if constexpr (U == UPC - 1) F.slot = R.next();
     }
   }
 
-  // One unit of an update pair: k-block KB, fragments (t, W_a | W_b/2) = w[2t + ab].
+  static __device__ __forceinline__ float *park_at(float *park, int kb, int mt, int lane) {
+    return park + ((kb * kParkMT + mt) * 64 + lane) * 4;
+  }
+
+  // One unit of an update pair: k-block KB, fragments w[2t] = W_a, w[2t+1] = W_b/2 of tile t.
   template <int MT, int KB, int U>
-  static __device__ __forceinline__ void unit(R_t &R, Feed &F, const Acts<MT> &X, f4 (&acc)[MT][2]) {
+  static __device__ __forceinline__ void unit(R_t &R, Feed &F, const Acts<MT> &X, Pair<MT> &P) {
     u4 w[4];
     take<U>(R, F, w);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        acc[mt][i >> 1] = mma(w[i], (i & 1) ? X.a[mt][KB] : X.h[mt][KB], acc[mt][i >> 1]);
+      for (int mt = 0; mt < MT; ++mt) {
+        P.a[mt][t] = mma(w[2 * t], X.h[mt][KB], P.a[mt][t]);
+        P.g[mt][t] = mma(w[2 * t + 1], X.h[mt][KB], P.g[mt][t]);
+      }
   }
 
+  // b_l enters A as the C operand of its first MFMA
   template <int MT>
-  static __device__ __forceinline__ void init_pair(const float *bias, int q, int g4, f4 (&acc)[MT][2]) {
+  static __device__ __forceinline__ void init(const float *bias, int q, int g4, Pair<MT> &P) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const f4 b = ldf4(bias + 16 * (2 * q + t) + g4);  // b_l enters as the first MFMA's C operand
+      const f4 b = ldf4(bias + 16 * (2 * q + t) + g4);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt][t] = b;
+      for (int mt = 0; mt < MT; ++mt) {
+        P.a[mt][t] = b;
+        P.g[mt][t] = f4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   }
 
-  // Output pair q >= 1 of an update layer, with the epilogue of pair q-1
-  // (prev) spread over its 4 units and parked as k-block q-1.
+  // Dword K of the k-block fragment made from one output pair (tile t = K>>1,
+  // rows r0 = 2(K&1), r0+1): z = A + (G(i-1) + G(i+1)), ReLU, bf16 pairs.
+  template <int MT, int K>
+  static __device__ __forceinline__ void piece(Pair<MT> &P, u4 (&nh)[MT]) {
+    constexpr int t = K >> 1, r0 = 2 * (K & 1);
+    float z[2][MT];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      float v[MT], sm[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) v[mt] = P.g[mt][t][r0 + rr];
+      nb_sum<MT>(v, sm);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) z[rr][mt] = __fadd_rn(P.a[mt][t][r0 + rr], sm[mt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) nh[mt][K] = pk_bf16(relu(z[0][mt]), relu(z[1][mt]));
+  }
+
+  // Output pair q >= 1, with the epilogue of pair q-1 (prev) spread over its 4
+  // units and parked as k-block q-1.
   template <int MT>
   static __device__ __forceinline__ void pair_with_prev(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int q,
-                                                        int g4, f4 (&acc)[MT][2], const f4 (&prev)[MT][2],
-                                                        float *park, int lane) {
-    init_pair<MT>(bias, q, g4, acc);
-    u4 nh[MT], na[MT];
+                                                        int g4, Pair<MT> &acc, Pair<MT> &prev, float *park,
+                                                        int lane) {
+    init<MT>(bias, q, g4, acc);
+    u4 nh[MT];
     unit<MT, 0, 0 % UPC>(R, F, X, acc);
-    piece<MT, 0, true>(prev, nh, na);
+    piece<MT, 0>(prev, nh);
     interleave<4 * MT, 2>();
     unit<MT, 1, 1 % UPC>(R, F, X, acc);
-    piece<MT, 1, true>(prev, nh, na);
+    piece<MT, 1>(prev, nh);
     interleave<4 * MT, 2>();
     unit<MT, 2, 2 % UPC>(R, F, X, acc);
-    piece<MT, 2, true>(prev, nh, na);
+    piece<MT, 2>(prev, nh);
     interleave<4 * MT, 2>();
     unit<MT, 3, 3 % UPC>(R, F, X, acc);
-    piece<MT, 3, true>(prev, nh, na);
+    piece<MT, 3>(prev, nh);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      *reinterpret_cast<u4 *>(park_at(park, q - 1, 0, mt, lane)) = nh[mt];
-      *reinterpret_cast<u4 *>(park_at(park, q - 1, 1, mt, lane)) = na[mt];
-    }
+    for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<u4 *>(park_at(park, q - 1, mt, lane)) = nh[mt];
     interleave<4 * MT, 2>();
   }
 
@@ -203,33 +208,26 @@ struct CoreBF16T {
   // first three units.
   template <int MT>
   static __device__ __forceinline__ void pair0_after(R_t &R, Feed &F, Acts<MT> &X, const float *bias, int g4,
-                                                     f4 (&acc)[MT][2], const f4 (&pend)[MT][2], float *park,
-                                                     int lane) {
+                                                     Pair<MT> &acc, Pair<MT> &pend, float *park, int lane) {
     wave_lds_sync();  // this wave's park writes of the previous layer have landed
 #pragma unroll
     for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        X.h[mt][kb] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, 0, mt, lane)));
-        X.a[mt][kb] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, 1, mt, lane)));
-      }
-    init_pair<MT>(bias, 0, g4, acc);
-    u4 nh[MT], na[MT];
+      for (int mt = 0; mt < MT; ++mt) X.h[mt][kb] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, mt, lane)));
+    init<MT>(bias, 0, g4, acc);
+    u4 nh[MT];
     unit<MT, 0, 0 % UPC>(R, F, X, acc);
-    piece<MT, 0, true>(pend, nh, na);
-    piece<MT, 1, true>(pend, nh, na);
+    piece<MT, 0>(pend, nh);
+    piece<MT, 1>(pend, nh);
     interleave<4 * MT, 4>();
     unit<MT, 1, 1 % UPC>(R, F, X, acc);
-    piece<MT, 2, true>(pend, nh, na);
+    piece<MT, 2>(pend, nh);
     interleave<4 * MT, 2>();
     unit<MT, 2, 2 % UPC>(R, F, X, acc);
-    piece<MT, 3, true>(pend, nh, na);
+    piece<MT, 3>(pend, nh);
     interleave<4 * MT, 2>();
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      X.h[mt][3] = nh[mt];
-      X.a[mt][3] = na[mt];
-    }
+    for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
     unit<MT, 3, 3 % UPC>(R, F, X, acc);
     interleave<4 * MT, 0>();
   }
@@ -237,8 +235,8 @@ struct CoreBF16T {
   // Pair 0 of the first layer (X complete from the input layer).
   template <int MT>
   static __device__ __forceinline__ void pair0_first(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
-                                                     f4 (&acc)[MT][2]) {
-    init_pair<MT>(bias, 0, g4, acc);
+                                                     Pair<MT> &acc) {
+    init<MT>(bias, 0, g4, acc);
     unit<MT, 0, 0 % UPC>(R, F, X, acc);
     interleave<4 * MT, 0>();
     unit<MT, 1, 1 % UPC>(R, F, X, acc);
@@ -249,16 +247,17 @@ struct CoreBF16T {
     interleave<4 * MT, 0>();
   }
 
-  // Pairs 1..3 of a layer; returns pair 3's accumulators (its epilogue is pending).
+  // Pairs 1..3 of a layer; leaves pair 3 in pend (its epilogue is pending).
   template <int MT>
   static __device__ __forceinline__ void pairs_rest(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
-                                                    f4 (&acc0)[MT][2], f4 (&pend)[MT][2], float *park, int lane) {
-    f4 acc1[MT][2], acc2[MT][2];
+                                                    Pair<MT> &acc0, Pair<MT> &pend, float *park, int lane) {
+    Pair<MT> acc1, acc2;
     pair_with_prev<MT>(R, F, X, bias, 1, g4, acc1, acc0, park, lane);
     pair_with_prev<MT>(R, F, X, bias, 2, g4, acc2, acc1, park, lane);
     pair_with_prev<MT>(R, F, X, bias, 3, g4, pend, acc2, park, lane);
   }
 
+  // ------------------------------------------------------------- readout
   // Readout unit U of output tile ot: fragment i = 2*(kb - 2U) + (P|Q), kb = 2U, 2U+1;
   // T = its index in the ring chunk.
   template <int MT, int U, int T>
@@ -337,26 +336,26 @@ struct CoreBF16T {
   // 0..2 comes from the park, k-block 3 is finished under the first readout unit.
   template <int MT>
   static __device__ __forceinline__ void readout(const ChainW &W, const Small &S, R_t &R, Feed &F, Acts<MT> &X,
-                                                 const f4 (&pend)[MT][2], float *park, int lane, int g4,
-                                                 float (&ffwd)[MT], float (&fbwd)[MT]) {
+                                                 Pair<MT> &pend, float *park, int lane, int g4, float (&ffwd)[MT],
+                                                 float (&fbwd)[MT]) {
     wave_lds_sync();
 #pragma unroll
     for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) X.h[mt][kb] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, 0, mt, lane)));
+      for (int mt = 0; mt < MT; ++mt) X.h[mt][kb] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, mt, lane)));
     float pf[MT], pb[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
     f4 P[MT], Q[MT];
     init_ro<MT>(S, 0, g4, P, Q);
     {
-      u4 nh[MT], na[MT];
+      u4 nh[MT];
       ro_unit<MT, 0, 0>(R, F, X, P, Q);
-      piece<MT, 0, false>(pend, nh, na);
-      piece<MT, 1, false>(pend, nh, na);
-      piece<MT, 2, false>(pend, nh, na);
-      piece<MT, 3, false>(pend, nh, na);
-      interleave<4 * MT, 3>();
+      piece<MT, 0>(pend, nh);
+      piece<MT, 1>(pend, nh);
+      piece<MT, 2>(pend, nh);
+      piece<MT, 3>(pend, nh);
+      interleave<4 * MT, 4>();
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
       ro_unit<MT, 1, 1>(R, F, X, P, Q);
@@ -383,7 +382,7 @@ struct CoreBF16T {
     const int lane = R.lane;
     const int g4 = 4 * (lane >> 4);
     Acts<MT> X;
-    f4 pend[MT][2];
+    Pair<MT> pend;
     {
       f4 h[MT][kNT];
       input_layer<MT>(S, lane, feat, h);  // f32 MFMA, ReLU applied
@@ -392,41 +391,34 @@ struct CoreBF16T {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int t = k >> 1, r = 2 * (k & 1);
-          float v0[MT], v1[MT], s0[MT], s1[MT];
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            v0[mt] = h[mt][2 * kb + t][r];
-            v1[mt] = h[mt][2 * kb + t][r + 1];
-            X.h[mt][kb][k] = pk_bf16(v0[mt], v1[mt]);
-          }
-          nb_sum<MT>(v0, s0);
-          nb_sum<MT>(v1, s1);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) X.a[mt][kb][k] = pk_bf16(s0[mt], s1[mt]);
+          for (int mt = 0; mt < MT; ++mt) X.h[mt][kb][k] = pk_bf16(h[mt][2 * kb + t][r], h[mt][2 * kb + t][r + 1]);
         }
       if (W.layers == 0) {
         // no update layer: hand the readout the input layer's output the way
-        // a last layer would (k-blocks 0..2 parked, tiles 6, 7 pending; ReLU is idempotent)
+        // a last layer would (k-blocks 0..2 parked, tiles 6, 7 pending with a
+        // zero aggregation term; ReLU is idempotent)
 #pragma unroll
         for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<u4 *>(park_at(park, kb, 0, mt, lane)) = X.h[mt][kb];
+          for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<u4 *>(park_at(park, kb, mt, lane)) = X.h[mt][kb];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          pend[mt][0] = h[mt][6];
-          pend[mt][1] = h[mt][7];
+          pend.a[mt][0] = h[mt][6];
+          pend.a[mt][1] = h[mt][7];
+          pend.g[mt][0] = pend.g[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
     // message passing (src/flux_gnn.py:53-60), pair-pipelined
     if (W.layers > 0) {
-      f4 acc0[MT][2];
+      Pair<MT> acc0;
       pair0_first<MT>(R, F, X, S.bl, g4, acc0);
       pairs_rest<MT>(R, F, X, S.bl, g4, acc0, pend, park, lane);
     }
     for (int l = 1; l < W.layers; ++l) {
       const float *bias = S.bl + l * kH;
-      f4 acc0[MT][2];
+      Pair<MT> acc0;
       pair0_after<MT>(R, F, X, bias, g4, acc0, pend, park, lane);
       pairs_rest<MT>(R, F, X, bias, g4, acc0, pend, park, lane);
     }
@@ -438,17 +430,16 @@ struct CoreBF16T {
 
 hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                   const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
-  if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
-    return chain::launch_flux_core<CoreBF16T<4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
-  // windowed (e.g. cfg4's 1024 cells): 16 KiB chunks in 3 slots
-  return chain::launch_flux_windowed<CoreBF16T<4, 4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  // exact kernels (nx = 16..64) and windows of 64 cells (any other nx, e.g.
+  // cfg4's 1024): 8 waves, two per SIMD, 16 KiB chunks in 3 slots
+  return chain::launch_flux_core<CoreBF16<8, 4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float *state_final, const float *x,
                                      const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                      float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
-  return chain::launch_rollout_core<CoreBF16T<4>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj,
-                                              metrics, ex, s);
+  return chain::launch_rollout_core<CoreBF16<4, 2, 4, true>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
+                                                             flux_traj, metrics, ex, s);
 }
 
 }  // namespace hf

@@ -65,6 +65,10 @@ class DeviceModel:
       "f32"   v_mfma_f32_16x16x4_f32, exact float32 (parity reference)
       "f16x3" fp16 hi+lo split of weights and activations, 3 products on
               v_mfma_f32_16x16x32_f16, f32 accumulate: float32-level accuracy
+              while every GEMM input stays within the fp16 range (|value| <
+              65504; the physical states of this model are O(1), ~1e3x inside
+              it); past it the split overflows and the flux is reported
+              non-finite where f32 would still be finite (tests: test_f16x3_range)
       "bf16"  bf16 weights and activations, f32 accumulate (BASELINE config 4)
     The generic-graph path always computes in float32."""
 

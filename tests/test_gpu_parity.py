@@ -259,6 +259,41 @@ def test_ragged_batches(hf, B):
         close(out["traj"].cpu().numpy(), want, ROLL_ATOL, ROLL_RTOL)
 
 
+@pytest.mark.parametrize("nx", [64, 100])
+def test_aliased_state_buffers(hf, nx):
+    """state0 may alias state_final (include/hybridflux.h) in the fused (nx=64) and
+    the generic (nx=100) sequencing, for hf_run with and without a trajectory and
+    for hf_run_compare: same bits as separate buffers (the generic
+    compare used to start the classical twin from the hybrid's final state)."""
+    w = weights("W1_r1")
+    G = O.Grid(nx, dt=5e-3 * min(1.0, nx / 64.0))
+    solver = hf.HybridSolver(w, radius=1, nx=nx, dt=G.dt, device=DEV)
+    ics = torch.as_tensor(np.stack([O.initial_condition(G, s) for s in (1000, 1001, 1002)]), device=DEV)
+    for T in (1, 4):
+        for traj in (False, True):
+            want = solver.run_batch(ics, T, traj=traj)["final"]
+            buf = ics.clone()
+            got = solver.run_batch(buf, T, traj=traj, out=buf)["final"]
+            assert got.data_ptr() == buf.data_ptr() and torch.equal(got, want), (T, traj)
+    want = solver.compare_batch(ics, 6)
+    buf = ics.clone()
+    got = solver.compare_batch(buf, 6, out=buf)
+    for k in ("mse", "metrics", "metrics_classical"):
+        assert torch.equal(got[k], want[k]), k
+    assert torch.equal(buf, want["final"])
+
+
+def test_large_nx_is_a_clean_error(hf):
+    """nx > 6144 exceeds the FV/Poisson kernel's LDS plan: a HF_EUNSUPPORTED error,
+    never a launch (the BASELINE configs stop at nx = 1024)."""
+    from hybridflux._lib import HF_EUNSUPPORTED, HybridFluxError
+    solver = hf.BaselineSolver(nx=6160, dt=1e-5, device=DEV)
+    st = torch.ones(2, 3, 6160, device=DEV)
+    with pytest.raises(HybridFluxError) as e:
+        solver.step_batch(st)
+    assert e.value.code == HF_EUNSUPPORTED
+
+
 def test_zero_steps(hf):
     ics = golden("ics.npz")["ics_nx64"][:4]
     solver = hf.HybridSolver(weights("W0"), radius=1, device=DEV)

@@ -1,14 +1,14 @@
 #!/bin/bash
-# cfg4 (nx=1024, bf16) PMC pass: shader clock and MFMA-busy for the windowed
-# flux kernel, then a 2-rank gloo rehearsal of bench.py's N>1 path on one GPU.
+# cfg4 (nx=1024, bf16, W1_r2) PMC passes for the windowed flux kernel: shader
+# clock + MFMA busy, then instruction mix / waits, one pass each.
 set -o pipefail
 cd "$(dirname "$0")/.."
-TAG=${1:-r01}
+TAG=${1:-r02}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-B="python3 bench.py --nx 1024 --precision bf16 --steps 5 --warmup 1 --also= --no-cpu-baseline --no-other-configs"
-timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -d gpurun_out/pmc_c4_$TAG -o p -- $B > gpurun_out/pmc_c4_$TAG.log 2>&1 \
- && timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 --dist-backend gloo --no-cpu-baseline --no-other-configs > gpurun_out/gloo2_$TAG.json 2> gpurun_out/gloo2_$TAG.err
+B="python3 bench.py --nx 1024 --precision bf16 --steps 5 --warmup 1 --weights tests/golden/weights_W1_r2.npz --no-traj --also= --no-cpu-baseline --no-other-configs"
+timeout -k 10 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES --kernel-trace -d gpurun_out/pmc_c4_$TAG -o p -- $B > gpurun_out/pmc_c4_$TAG.log 2>&1 \
+ && timeout -k 10 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU --kernel-trace -d gpurun_out/pmc_c4sq_$TAG -o p -- $B > gpurun_out/pmc_c4sq_$TAG.log 2>&1
 rc=$?
-tail -1 gpurun_out/gloo2_$TAG.json
+python3 tools/pmc_summary.py chain_flux_kernel gpurun_out/pmc_c4_$TAG/*.db gpurun_out/pmc_c4sq_$TAG/*.db 2>&1 | tail -12
 exit $rc
