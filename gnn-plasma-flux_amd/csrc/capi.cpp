@@ -536,11 +536,16 @@ int hf_poisson_coeffs(int nx, double length, double *c) {
       tw[2 * m] = (double)cosl(a);
       tw[2 * m + 1] = (double)sinl(a);
     }
-    const double dx = length / nx;  // k = 2 pi fftfreq(nx, d=dx)   (src/baseline_solver.py:26)
+    // k = 2 pi fftfreq(nx, d=dx) (src/baseline_solver.py:26).  The k = 0 mode
+    // is zeroed as in the reference; so is the Nyquist mode q = nx/2: for a real
+    // rho its term i X/k is purely imaginary, which the reference's Re() drops,
+    // and zeroing it lets two ICs share one complex transform (z = rho_a + i
+    // rho_b) without that term leaking from one into the other.
+    const double dx = length / nx;
     for (int q = 0; q < nx; ++q) {
       const int f = q < (nx + 1) / 2 ? q : q - nx;
       const double k = 2.0 * pi * ((double)f / (nx * dx));
-      inv_k[q] = f == 0 ? 0.0 : 1.0 / k;
+      inv_k[q] = (f == 0 || 2 * q == nx) ? 0.0 : 1.0 / k;
     }
   }
   return HF_OK;

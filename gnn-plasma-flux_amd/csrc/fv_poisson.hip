@@ -1,9 +1,11 @@
-// Finite-volume update + spectral (circulant) Poisson solve for any nx.
+// Finite-volume update + spectral Poisson solve for any nx
+// (src/baseline_solver.py:59-101, src/hybrid_solver.py:45-63).
 //
-// One 256-thread workgroup per IC; the IC's chain lives in LDS for the
-// update and the O(nx^2) float64 circulant product (src/baseline_solver.py:
-// 59-101, src/hybrid_solver.py:45-63).  HBM traffic per cell-step is the
-// 12 B state read + 12 B state write (+4 B face flux in hybrid mode).
+// FFT sizes (power-of-two nx in 256..2048): one wave per pair of ICs, the
+// transform in registers + a wave-private LDS buffer (hf_device.h
+// poisson_wave).  Other nx: one 256-thread workgroup per IC, the chain in
+// LDS and the exact O(nx^2) float64 circulant.  HBM traffic per cell-step is
+// the 12 B state read + 12 B state write (+4 B face flux in hybrid mode).
 #include "hf_device.h"
 #include "hf_internal.h"
 
@@ -38,45 +40,22 @@ __device__ __forceinline__ void block_metrics(MetricAcc &m, float *dst, int nx) 
   }
 }
 
-// LDS, circulant nx: c[nx] (double) | u, F, rho, E (float).
-// LDS, FFT nx: u, F (float) | FFT buffers 2 x nx double2 | twiddles nx/4 double2.
-__host__ __device__ inline size_t fv_fft_offset(int nx) { return ((size_t)nx * 2 * sizeof(float) + 15) & ~size_t(15); }
-inline size_t fv_lds_bytes(int nx) {
-  return poisson_uses_fft(nx) ? fv_fft_offset(nx) + (2 * (size_t)nx + nx / 4) * sizeof(double2)
-                              : (size_t)nx * (sizeof(double) + 4 * sizeof(float));
-}
+// LDS of the circulant kernels (nx not an FFT size): c[nx] (double) | u, F, rho, E (float).
+inline size_t fv_lds_bytes(int nx) { return (size_t)nx * (sizeof(double) + 4 * sizeof(float)); }
 
-// Carve of the dynamic LDS (see fv_lds_bytes).
 struct FvLds {
   double *c;
   float *u, *F, *rho, *E;
-  double2 *fa, *fb, *tw;
   __device__ FvLds(double *s_dyn, int nx) {
-    if (poisson_uses_fft(nx)) {
-      c = nullptr;
-      u = reinterpret_cast<float *>(s_dyn);
-      F = u + nx;
-      rho = E = nullptr;
-      fa = reinterpret_cast<double2 *>(reinterpret_cast<char *>(s_dyn) + fv_fft_offset(nx));
-      fb = fa + nx;
-      tw = fb + nx;
-    } else {
-      c = s_dyn;
-      u = reinterpret_cast<float *>(c + nx);
-      F = u + nx;
-      rho = F + nx;
-      E = rho + nx;
-      fa = fb = tw = nullptr;
-    }
+    c = s_dyn;
+    u = reinterpret_cast<float *>(c + nx);
+    F = u + nx;
+    rho = F + nx;
+    E = rho + nx;
   }
 };
 
-// Stage the first quarter of the plan's twiddles (after the circulant column c[nx]) into LDS.
-__device__ __forceinline__ void stage_twiddles(const double *pc, double2 *s_tw, int nx) {
-  const double2 *tw = reinterpret_cast<const double2 *>(pc + nx);
-  for (int q = threadIdx.x; q < nx / 4; q += blockDim.x) s_tw[q] = tw[q];
-}
-
+// Circulant nx (any nx that is not an FFT size): one 256-thread workgroup per IC.
 template <bool HYBRID>
 __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     const float *__restrict__ in, int64_t ld_in, float *__restrict__ out, int64_t ld_out,
@@ -85,7 +64,6 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     int64_t ld_metrics) {
   extern __shared__ double s_dyn[];
   const FvLds L(s_dyn, nx);
-  const bool fft = poisson_uses_fft(nx);
   const int64_t b = blockIdx.x;
   const float *st = in + b * ld_in;
   float *so = out + b * ld_out;
@@ -93,9 +71,8 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     const float u = st[nx + i];
     L.u[i] = u;
     L.F[i] = HYBRID ? face_flux[b * nx + i] : __fmul_rn(st[i], u);  // F_n = n*u (:70-71)
-    if (!fft) L.c[i] = pc[i];
+    L.c[i] = pc[i];
   }
-  if (fft) stage_twiddles(pc, L.tw, nx);
   __syncthreads();
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
     const int im = i == 0 ? nx - 1 : i - 1;
@@ -105,116 +82,170 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     const float E = st[2 * nx + i];
     const float u_new = HYBRID ? velocity_hybrid(L.u[i], L.u[im], E, c, dt)
                                : velocity_classical(L.u[i], L.u[im], L.u[ip], E, c, dt, nu, dx2);
-    const float rho = __fsub_rn(n_new, 1.0f);
-    if (fft) L.fa[i] = make_double2((double)rho, 0.0);
-    else L.rho[i] = rho;
+    L.rho[i] = __fsub_rn(n_new, 1.0f);
     so[i] = n_new;
     so[nx + i] = u_new;
     if (flux_out) flux_out[b * ld_flux + i] = F;
   }
-  const double2 *X = nullptr;
-  if (fft) X = poisson_fft(L.fa, L.fb, L.tw, pc + 2 * nx, nx);
-  else __syncthreads();
+  __syncthreads();
   MetricAcc m;
   m.init();
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-    const float E_new = fft ? (float)(X[i].x / nx) : poisson_cell(L.rho, L.c, i, nx);
+    const float E_new = poisson_cell(L.rho, L.c, i, nx);
     so[2 * nx + i] = E_new;
     if (metrics) m.add(so[i], so[nx + i], E_new);
   }
   if (metrics) block_metrics(m, metrics + b * ld_metrics, nx);
 }
 
-// FFT sizes: two ICs per workgroup share one complex transform pair.  The
-// spectral operator T = i/k (k = 0 zeroed) maps the FFT of a real signal to
-// the FFT of a real signal, so with z = rho_a + i rho_b,
-//   ifft(T fft(z)) = ifft(T fft(rho_a)) + i ifft(T fft(rho_b)) = E_a + i E_b:
-// the real part is IC a's field and the imaginary part IC b's, for half the
-// transform work per IC (src/baseline_solver.py:59-68 evaluates each
-// separately; the two agree to float64 rounding, far below the float32 result).
-// Every global read is issued up front (one HBM round trip): n and E into
-// registers, u and F (read at i-1, i+1) into LDS, where they share the second
-// FFT buffer (first written by the transform, after its opening barrier).
-// LDS: FFT buffer a [nx] double2 | buffer b [nx] double2 = u, F [2][nx] float |
-// twiddles nx/4 double2: 36 KiB at nx = 1024, four workgroups per CU.
-constexpr int kFvPer = kFftMaxNx / kFvThreads;  // cells per thread, at most
-inline size_t fv_pair_lds_bytes(int nx) { return (2 * (size_t)nx + nx / 4) * sizeof(double2); }
+// ------------------------------------------------------------ FFT sizes
+// One WAVE per pair of ICs (4 waves per workgroup, no workgroup barrier):
+// lane l owns cells l + 64v (v < N/64) of both ICs.  It reads n, u, E (and F
+// in hybrid mode) once, coalesced; the chain neighbours u[i-1], F[i-1] (and
+// u[i+1] for the viscous term) come from the adjacent lane by a wave rotation
+// (DPP wave_ror / wave_rol: lane 0's left neighbour is lane 63 of the
+// previous register, the periodic wrap included).  The update writes n', u'
+// and packs rho = n' - 1 of the two ICs as one complex value, which
+// poisson_wave<N> turns into N (E_a + i E_b) in the same registers.
+// HBM: 12 B read + 12 B write per cell (+4 B F).  The transforms use a
+// wave-private padded LDS buffer.
+constexpr int kDppWaveShl1 = 0x130;  // lane l <- lane l+1 (lane 63: no source)
+constexpr int kDppWaveRol1 = 0x134;  // lane l <- lane l+1 (lane 63 <- lane 0)
+constexpr int kDppWaveShr1 = 0x138;  // lane l <- lane l-1 (lane 0: no source)
+constexpr int kDppWaveRor1 = 0x13C;  // lane l <- lane l-1 (lane 0 <- lane 63)
+// src moved by CTRL; lanes without a source keep `old`
+template <int CTRL>
+__device__ __forceinline__ float wave_dpp(float old, float src) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL, 0xF, 0xF, false));
+}
+// value at cell i-1 (left) or i+1 (right) for every register of a lane's
+// cells: a wave shift, and for the lane that shifts out of the wave (lane 0
+// left, lane 63 right) the rotated neighbour register (periodic wrap included)
+template <int V>
+__device__ __forceinline__ void left_of(const float (&x)[V], float (&l)[V]) {
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+    l[i] = wave_dpp<kDppWaveShr1>(wave_dpp<kDppWaveRor1>(0.f, x[(i + V - 1) % V]), x[i]);
+}
+template <int V>
+__device__ __forceinline__ void right_of(const float (&x)[V], float (&rt)[V]) {
+#pragma unroll
+  for (int i = 0; i < V; ++i) rt[i] = wave_dpp<kDppWaveShl1>(wave_dpp<kDppWaveRol1>(0.f, x[(i + 1) % V]), x[i]);
+}
 
-template <bool HYBRID>
-__global__ __launch_bounds__(kFvThreads) void fv_step_pair_kernel(
+constexpr int kFftWaves = 4;
+
+// The update of one IC's cells (lane + 64v) held by this lane: writes n', u'
+// (and F), accumulates the n, u part of the metrics, returns rho = n' - 1.
+template <bool HYBRID, int N>
+__device__ __forceinline__ void fv_update_lane(const float *__restrict__ st, float *__restrict__ so,
+                                               const float *__restrict__ Fb, float c, float dt, float nu, float dx2,
+                                               float *__restrict__ fo, bool want_m, MetricAcc &m, int lane,
+                                               double (&rho)[N / 64]) {
+  constexpr int V = N / 64;
+  float n[V], u[V], E[V], F[V], ul[V], Fl[V], ur[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int cell = lane + 64 * i;
+    n[i] = st[cell];
+    u[i] = st[N + cell];
+    E[i] = st[2 * N + cell];
+    F[i] = HYBRID ? Fb[cell] : __fmul_rn(n[i], u[i]);  // F_n = n*u (src/baseline_solver.py:70-71)
+  }
+  left_of<V>(u, ul);
+  left_of<V>(F, Fl);
+  if constexpr (!HYBRID) right_of<V>(u, ur);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int cell = lane + 64 * i;
+    const float n_new = continuity(n[i], F[i], Fl[i], c);
+    float u_new;
+    if constexpr (HYBRID) u_new = velocity_hybrid(u[i], ul[i], E[i], c, dt);
+    else u_new = velocity_classical(u[i], ul[i], ur[i], E[i], c, dt, nu, dx2);
+    so[cell] = n_new;
+    so[N + cell] = u_new;
+    if (fo) fo[cell] = F[i];
+    if (want_m) m.add_nu(n_new, u_new);
+    rho[i] = (double)__fsub_rn(n_new, 1.0f);
+  }
+}
+
+template <int N, bool IMAG>
+__device__ __forceinline__ void fv_finish_lane(float *__restrict__ so, const double2 (&v)[N / 64], MetricAcc &m,
+                                               float *__restrict__ mo, int lane) {
+#pragma unroll
+  for (int i = 0; i < N / 64; ++i) {
+    const float E_new = (float)((IMAG ? v[i].y : v[i].x) / N);
+    so[2 * N + lane + 64 * i] = E_new;
+    if (mo) m.add_E(E_new);
+  }
+  if (mo) {
+    m.wave_reduce();
+    if (lane == 0) m.store(mo, N);
+  }
+}
+
+template <bool HYBRID, int N>
+__global__ __launch_bounds__(64 * kFftWaves, 2) void fv_step_fft_kernel(
     const float *__restrict__ in, int64_t ld_in, float *__restrict__ out, int64_t ld_out,
-    const float *__restrict__ face_flux, const double *__restrict__ pc, int nx, float c, float dt,
-    float nu, float dx2, float *__restrict__ flux_out, int64_t ld_flux, float *__restrict__ metrics,
-    int64_t ld_metrics, int B) {
-  extern __shared__ double s_dyn[];
-  double2 *fa = reinterpret_cast<double2 *>(s_dyn);
-  double2 *fb = fa + nx, *tw = fb + nx;
-  float *s_u = reinterpret_cast<float *>(fb);  // [2][nx], then [2][nx] F: the 16*nx bytes of fb
-  float *s_F = s_u + 2 * nx;
-  const int64_t b0 = 2 * (int64_t)blockIdx.x;
-  const int nic = b0 + 1 < B ? 2 : 1;
-  float n_r[2][kFvPer], E_r[2][kFvPer];
+    const float *__restrict__ face_flux, const double *__restrict__ pc, float c, float dt, float nu, float dx2,
+    float *__restrict__ flux_out, int64_t ld_flux, float *__restrict__ metrics, int64_t ld_metrics, int B) {
+  constexpr int V = N / 64;
+  __shared__ double2 s_fft[kFftWaves][fft_lds_elems<N>()];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t a = 2 * ((int64_t)blockIdx.x * kFftWaves + wave), b = a + 1;
+  if (a >= B) return;  // a whole wave; nothing below synchronises the workgroup
+  const bool two = b < B;
+  double *rho_a = reinterpret_cast<double *>(s_fft[wave]);  // the transform's buffer, free until it starts
+  MetricAcc ma, mb;
+  ma.init();
+  mb.init();
+  double2 v[V];
+  {
+    double r[V];
+    fv_update_lane<HYBRID, N>(in + a * ld_in, out + a * ld_out, HYBRID ? face_flux + a * N : nullptr, c, dt, nu,
+                              dx2, flux_out ? flux_out + a * ld_flux : nullptr, metrics != nullptr, ma, lane, r);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if (q < nic) {
-      const float *st = in + (b0 + q) * ld_in;
-#pragma unroll
-      for (int k = 0; k < kFvPer; ++k) {
-        const int i = threadIdx.x + k * kFvThreads;
-        if (i < nx) {
-          const float n = st[i], u = st[nx + i];
-          n_r[q][k] = n;
-          E_r[q][k] = st[2 * nx + i];
-          s_u[q * nx + i] = u;
-          s_F[q * nx + i] = HYBRID ? face_flux[(b0 + q) * nx + i] : __fmul_rn(n, u);  // F_n = n*u (:70-71)
-        }
-      }
-    }
+    for (int i = 0; i < V; ++i) rho_a[lane + 64 * i] = r[i];  // parked while IC b's update holds the registers
   }
-  stage_twiddles(pc, tw, nx);
-  __syncthreads();
+  {
+    double r[V];
+    if (two)
+      fv_update_lane<HYBRID, N>(in + b * ld_in, out + b * ld_out, HYBRID ? face_flux + b * N : nullptr, c, dt, nu,
+                                dx2, flux_out ? flux_out + b * ld_flux : nullptr, metrics != nullptr, mb, lane, r);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int k = 0; k < kFvPer; ++k) {
-    const int i = threadIdx.x + k * kFvThreads;
-    if (i >= nx) break;
-    const int im = i == 0 ? nx - 1 : i - 1;
-    const int ip = i == nx - 1 ? 0 : i + 1;
-    double rho[2] = {0.0, 0.0};
+    for (int i = 0; i < V; ++i) v[i] = make_double2(rho_a[lane + 64 * i], two ? r[i] : 0.0);
+  }
+  poisson_wave<N>(v, s_fft[wave], pc, lane);
+  fv_finish_lane<N, false>(out + a * ld_out, v, ma, metrics ? metrics + a * ld_metrics : nullptr, lane);
+  if (two) fv_finish_lane<N, true>(out + b * ld_out, v, mb, metrics ? metrics + b * ld_metrics : nullptr, lane);
+}
+
+// hf_poisson at FFT sizes: one wave per pair of ICs, as above.
+template <int N>
+__global__ __launch_bounds__(64 * kFftWaves, 2) void poisson_fft_kernel(const float *__restrict__ n, int ld_n,
+                                                                     float *__restrict__ E, int ld_E,
+                                                                     const double *__restrict__ pc, int B) {
+  constexpr int V = N / 64;
+  __shared__ double2 s_fft[kFftWaves][fft_lds_elems<N>()];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b0 = 2 * ((int64_t)blockIdx.x * kFftWaves + wave);
+  if (b0 >= B) return;
+  const bool two = b0 + 1 < B;
+  double2 v[V];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (q >= nic) break;
-      float *so = out + (b0 + q) * ld_out;
-      const float *u = s_u + q * nx, *Fq = s_F + q * nx;
-      const float F = Fq[i];
-      const float n_new = continuity(n_r[q][k], F, Fq[im], c);
-      const float E = E_r[q][k];
-      const float u_new = HYBRID ? velocity_hybrid(u[i], u[im], E, c, dt)
-                                 : velocity_classical(u[i], u[im], u[ip], E, c, dt, nu, dx2);
-      rho[q] = (double)__fsub_rn(n_new, 1.0f);
-      so[i] = n_new;
-      so[nx + i] = u_new;
-      if (flux_out) flux_out[(b0 + q) * ld_flux + i] = F;
-    }
-    fa[i] = make_double2(rho[0], rho[1]);
+  for (int i = 0; i < V; ++i) {
+    const int cell = lane + 64 * i;
+    v[i].x = (double)__fsub_rn(n[b0 * ld_n + cell], 1.0f);  // rho = n - n0 (:60)
+    v[i].y = two ? (double)__fsub_rn(n[(b0 + 1) * ld_n + cell], 1.0f) : 0.0;
   }
-  const double2 *X = poisson_fft(fa, fb, tw, pc + 2 * nx, nx);
-  MetricAcc m[2];
-  m[0].init();
-  m[1].init();
-  for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-    for (int q = 0; q < nic; ++q) {
-      float *so = out + (b0 + q) * ld_out;
-      const float E_new = (float)((q == 0 ? X[i].x : X[i].y) / nx);
-      so[2 * nx + i] = E_new;
-      if (metrics) m[q].add(so[i], so[nx + i], E_new);
-    }
-  }
-  if (metrics) {
-    block_metrics(m[0], metrics + b0 * ld_metrics, nx);
-    if (nic == 2) {
-      __syncthreads();  // block_metrics' shared partials are reused
-      block_metrics(m[1], metrics + (b0 + 1) * ld_metrics, nx);
-    }
+  poisson_wave<N>(v, s_fft[wave], pc, lane);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int cell = lane + 64 * i;
+    E[b0 * ld_E + cell] = (float)(v[i].x / N);
+    if (two) E[(b0 + 1) * ld_E + cell] = (float)(v[i].y / N);
   }
 }
 
@@ -236,26 +267,13 @@ __global__ __launch_bounds__(kFvThreads) void poisson_kernel(const float *__rest
                                                              int nx) {
   extern __shared__ double s_dyn[];
   const FvLds L(s_dyn, nx);
-  const bool fft = poisson_uses_fft(nx);
   const int64_t b = blockIdx.x;
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-    const float rho = __fsub_rn(n[b * ld_n + i], 1.0f);  // rho = n - n0 (:60)
-    if (fft) {
-      L.fa[i] = make_double2((double)rho, 0.0);
-    } else {
-      L.c[i] = pc[i];
-      L.rho[i] = rho;
-    }
+    L.c[i] = pc[i];
+    L.rho[i] = __fsub_rn(n[b * ld_n + i], 1.0f);  // rho = n - n0 (:60)
   }
-  const double2 *X = nullptr;
-  if (fft) {
-    stage_twiddles(pc, L.tw, nx);
-    X = poisson_fft(L.fa, L.fb, L.tw, pc + 2 * nx, nx);
-  } else {
-    __syncthreads();
-  }
-  for (int i = threadIdx.x; i < nx; i += kFvThreads)
-    E[b * ld_E + i] = fft ? (float)(X[i].x / nx) : poisson_cell(L.rho, L.c, i, nx);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nx; i += kFvThreads) E[b * ld_E + i] = poisson_cell(L.rho, L.c, i, nx);
 }
 
 // Per-step channel MSE of two trajectories (scripts/evaluation/evaluate_multi_ic.py:88-90).
@@ -292,21 +310,33 @@ hipError_t launch_traj_mse(const float *a, const float *b, int B, int T1, int nx
   return hipGetLastError();
 }
 
+template <int N>
+hipError_t fv_fft_launch(const float *in, int64_t ld_in, float *out, int64_t ld_out, const float *face_flux,
+                         const double *pc, int B, float c, float dt, float nu, float dx2, float *flux_out,
+                         int64_t ld_flux, float *metrics, int64_t ld_metrics, hipStream_t s) {
+  const unsigned grid = (unsigned)((B + 2 * kFftWaves - 1) / (2 * kFftWaves));
+  if (face_flux)
+    hipLaunchKernelGGL((fv_step_fft_kernel<true, N>), dim3(grid), dim3(64 * kFftWaves), 0, s, in, ld_in, out, ld_out,
+                       face_flux, pc, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
+  else
+    hipLaunchKernelGGL((fv_step_fft_kernel<false, N>), dim3(grid), dim3(64 * kFftWaves), 0, s, in, ld_in, out,
+                       ld_out, face_flux, pc, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
+  return hipGetLastError();
+}
+
 hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld_out,
                           const float *face_flux, const double *pc, int B, int nx, float c,
                           float dt, float nu, float dx2, float *flux_out, int64_t ld_flux,
                           float *metrics, int64_t ld_metrics, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (poisson_uses_fft(nx)) {  // two ICs per workgroup, one transform pair
-    const size_t lds = fv_pair_lds_bytes(nx);
-    const unsigned grid = (unsigned)((B + 1) / 2);
-    if (face_flux)
-      hipLaunchKernelGGL(fv_step_pair_kernel<true>, dim3(grid), dim3(kFvThreads), lds, s, in, ld_in, out, ld_out,
-                         face_flux, pc, nx, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
-    else
-      hipLaunchKernelGGL(fv_step_pair_kernel<false>, dim3(grid), dim3(kFvThreads), lds, s, in, ld_in, out, ld_out,
-                         face_flux, pc, nx, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
-    return hipGetLastError();
+  if (poisson_uses_fft(nx)) {
+    switch (nx) {
+      case 256: return fv_fft_launch<256>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, s);
+      case 512: return fv_fft_launch<512>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, s);
+      case 1024: return fv_fft_launch<1024>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, s);
+      case 2048: return fv_fft_launch<2048>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, s);
+      default: return hipErrorInvalidValue;
+    }
   }
   const size_t lds = fv_lds_bytes(nx);
   if (face_flux)
@@ -328,9 +358,23 @@ hipError_t launch_state_metrics(const float *st, int64_t ld, int B, int nx, floa
   return hipGetLastError();
 }
 
+template <int N>
+hipError_t poisson_fft_launch(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B, hipStream_t s) {
+  const unsigned grid = (unsigned)((B + 2 * kFftWaves - 1) / (2 * kFftWaves));
+  hipLaunchKernelGGL((poisson_fft_kernel<N>), dim3(grid), dim3(64 * kFftWaves), 0, s, n, ld_n, E, ld_E, pc, B);
+  return hipGetLastError();
+}
+
 hipError_t launch_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B,
                           int nx, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  switch (poisson_uses_fft(nx) ? nx : 0) {
+    case 256: return poisson_fft_launch<256>(n, ld_n, E, ld_E, pc, B, s);
+    case 512: return poisson_fft_launch<512>(n, ld_n, E, ld_E, pc, B, s);
+    case 1024: return poisson_fft_launch<1024>(n, ld_n, E, ld_E, pc, B, s);
+    case 2048: return poisson_fft_launch<2048>(n, ld_n, E, ld_E, pc, B, s);
+    default: break;
+  }
   const size_t lds = fv_lds_bytes(nx);
   hipLaunchKernelGGL(poisson_kernel, dim3(B), dim3(kFvThreads), lds, s, n, ld_n, E, ld_E, pc, nx);
   return hipGetLastError();

@@ -69,84 +69,158 @@ __device__ __forceinline__ float poisson_cell(const float *s_rho, const double *
 }
 
 // ---------------------------------------------------------------- FFT Poisson
-// For power-of-two nx >= kFftMinNx the spectral operator is applied as the
-// reference writes it (src/baseline_solver.py:59-68), E = Re(ifft(1j*fft(rho)/k)),
-// with a float64 Stockham radix-2 FFT in LDS instead of the O(nx^2) circulant.
-// The plan buffer (hf_poisson_coeffs) then holds, after the circulant column
-// c[nx]: twiddles exp(-2 pi i m / nx) for m < nx/2 as (re, im), and 1/k_q (0 at q = 0).
+// For power-of-two nx in [kFftMinNx, kFftMaxNx] the spectral operator is
+// applied as the reference writes it (src/baseline_solver.py:59-68),
+// E = Re(ifft(1j*fft(rho)/k)), k=0 mode zeroed, by float64 FFTs run by ONE
+// wave: lane l holds the N/64 values at indices l + 64v in registers, the
+// transform is a mixed-radix Stockham sequence (radix R = min(N/64, 16,
+// what is left): 256 = 4^4, 512 = 8^3, 1024 = 16*16*4, 2048 = 16*16*8) whose
+// butterflies a lane evaluates in registers, and the passes exchange values
+// through a wave-private LDS buffer (the wave's own s_waitcnt orders it: no
+// workgroup barrier).  The first pass reads, and the last pass writes, the
+// lane's own indices l + 64v, so the FV update feeds the transform and takes
+// E back without LDS.  Twiddles exp(-+2 pi i e/N) come from the plan
+// (hf_poisson_coeffs: e < N/2 as (re, im); e >= N/2 by negation), so each is
+// exactly the plan's value.  tests/test_abi_cpu.py::_stockham models the same
+// passes in numpy.
+// float64 complex product as 2 multiplies + 2 FMAs (this header turns
+// contraction off for the float32 FV expressions; the transforms round at
+// 1e-16 and do not need it)
 __device__ __forceinline__ double2 cmul(double2 a, double2 w) {
-  return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+  return make_double2(fma(a.x, w.x, -(a.y * w.y)), fma(a.x, w.y, a.y * w.x));
 }
-// exp(-+2 pi i m / n) for 0 <= m < n from the quarter table tw[m < n/4] (the
-// plan holds m < n/2; only the first quarter is staged): quadrant q multiplies
-// by (-i)^q, a swap and sign flips, so every twiddle is exactly the table's.
-__device__ __forceinline__ double2 twiddle(const double2 *__restrict__ tw, int m, int n, bool inverse) {
-  const int n4 = n / 4, q = m / n4;
-  const double2 t = tw[m - q * n4];
-  double2 w = q == 0 ? t : q == 1 ? make_double2(t.y, -t.x) : q == 2 ? make_double2(-t.x, -t.y)
-                                                                    : make_double2(-t.y, t.x);
-  if (inverse) w.y = -w.y;
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+
+// exp(-+2 pi i e / N) for 0 <= e < N from the plan's half table
+template <int N, bool INV>
+__device__ __forceinline__ double2 plan_twiddle(const double2 *__restrict__ tw, int e) {
+  const bool hi = e >= N / 2;
+  double2 w = tw[hi ? e - N / 2 : e];
+  if (hi) w = make_double2(-w.x, -w.y);
+  if (INV) w.y = -w.y;
   return w;
 }
 
-// Block FFT, Stockham autosort: radix-4 passes (one radix-2 pass first when
-// log2 n is odd), one barrier per pass.  Returns the buffer holding the
-// result (a or b).  tests/test_abi_cpu.py::_stockham models the same passes.
-__device__ __forceinline__ double2 *fft_block(double2 *a, double2 *b, const double2 *__restrict__ tw, int n,
-                                              bool inverse) {
-  int ns = 1;
-  if ((__builtin_ctz(n) & 1) != 0) {  // radix-2 pass, ns = 1: twiddle 1
-    __syncthreads();
-    for (int jj = threadIdx.x; jj < n / 2; jj += blockDim.x) {
-      const double2 a0 = a[jj], a1 = a[jj + n / 2];
-      b[2 * jj] = make_double2(a0.x + a1.x, a0.y + a1.y);
-      b[2 * jj + 1] = make_double2(a0.x - a1.x, a0.y - a1.y);
-    }
-    double2 *s = a;
-    a = b;
-    b = s;
-    ns = 2;
+// t * exp(-+2 pi i q / 16) with the constant's exact special cases (q % 4 == 0)
+template <int Q, bool INV>
+__device__ __forceinline__ double2 mul_w16(double2 t) {
+  constexpr double kC[16] = {1.0, 0.92387953251128675613, 0.70710678118654752440, 0.38268343236508977173,
+                             0.0, -0.38268343236508977173, -0.70710678118654752440, -0.92387953251128675613,
+                             -1.0, -0.92387953251128675613, -0.70710678118654752440, -0.38268343236508977173,
+                             0.0, 0.38268343236508977173, 0.70710678118654752440, 0.92387953251128675613};
+  constexpr int q = Q & 15;
+  if constexpr (q == 0) return t;
+  else if constexpr (q == 8) return make_double2(-t.x, -t.y);
+  else if constexpr (q == 4) return INV ? make_double2(-t.y, t.x) : make_double2(t.y, -t.x);   // * (+-i)
+  else if constexpr (q == 12) return INV ? make_double2(t.y, -t.x) : make_double2(-t.y, t.x);
+  else {
+    constexpr double c = kC[q], sn = kC[(q + 12) & 15];  // sin(2 pi q/16) = cos(2 pi (q - 4)/16)
+    const double si = INV ? sn : -sn;
+    return make_double2(fma(t.x, c, -(t.y * si)), fma(t.x, si, t.y * c));
   }
-  for (; ns < n; ns <<= 2) {
-    __syncthreads();
-    for (int jj = threadIdx.x; jj < n / 4; jj += blockDim.x) {
-      const int k = jj & (ns - 1);
-      const int m = k * (n / (4 * ns));
-      const double2 a0 = a[jj];
-      const double2 a1 = cmul(a[jj + n / 4], twiddle(tw, m, n, inverse));
-      const double2 a2 = cmul(a[jj + n / 2], twiddle(tw, 2 * m, n, inverse));
-      const double2 a3 = cmul(a[jj + 3 * n / 4], twiddle(tw, 3 * m, n, inverse));
-      const double2 b0 = make_double2(a0.x + a2.x, a0.y + a2.y), b1 = make_double2(a0.x - a2.x, a0.y - a2.y);
-      const double2 b2 = make_double2(a1.x + a3.x, a1.y + a3.y);
-      const double2 t = make_double2(a1.x - a3.x, a1.y - a3.y);
-      const double2 b3 = inverse ? make_double2(-t.y, t.x) : make_double2(t.y, -t.x);  // (a1 - a3) * (+-i)
-      const int d = (jj - k) * 4 + k;
-      b[d] = make_double2(b0.x + b2.x, b0.y + b2.y);
-      b[d + ns] = make_double2(b1.x + b3.x, b1.y + b3.y);
-      b[d + 2 * ns] = make_double2(b0.x - b2.x, b0.y - b2.y);
-      b[d + 3 * ns] = make_double2(b1.x - b3.x, b1.y - b3.y);
-    }
-    double2 *s = a;
-    a = b;
-    b = s;
-  }
-  __syncthreads();
-  return a;
 }
 
-// Spectral Poisson for the whole IC (block-wide).  On entry a[q] = (rho_q, 0),
-// written before the call by any thread (fft_block opens with a barrier);
-// s_tw holds the plan's twiddles (staged in LDS).  Returns the buffer X with
-// E_q = X[q].x / nx (the caller rounds to float32).
-__device__ __forceinline__ double2 *poisson_fft(double2 *a, double2 *b, const double2 *s_tw, const double *inv_k,
-                                               int nx) {
-  double2 *X = fft_block(a, b, s_tw, nx, false);
-  double2 *Y = X == a ? b : a;
-  for (int q = threadIdx.x; q < nx; q += blockDim.x) {
-    const double ik = inv_k[q];                       // 1j * X / k, k = 0 mode zeroed
-    X[q] = make_double2(-X[q].y * ik, X[q].x * ik);
+// Butterfly combine of a radix-2 DIT step: y_s = e_s + W_R^s o_s,
+// y_{s+R/2} = e_s - W_R^s o_s for s = S..R/2-1 (W_R^s as a constant).
+template <int R, bool INV, int S = 0>
+__device__ __forceinline__ void dit_combine(const double2 (&e)[R / 2], const double2 (&o)[R / 2], double2 (&y)[R]) {
+  if constexpr (S < R / 2) {
+    const double2 t = mul_w16<S * (16 / R), INV>(o[S]);
+    y[S] = cadd(e[S], t);
+    y[S + R / 2] = csub(e[S], t);
+    dit_combine<R, INV, S + 1>(e, o, y);
   }
-  return fft_block(X, Y, s_tw, nx, true);
+}
+
+// In-register DFT of size R (1..16): y_s = sum_r y_r exp(-+2 pi i r s / R),
+// radix-2 decimation in time.
+template <int R, bool INV>
+__device__ __forceinline__ void dft_reg(double2 (&y)[R]) {
+  if constexpr (R > 1) {
+    double2 e[R / 2], o[R / 2];
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) {
+      e[i] = y[2 * i];
+      o[i] = y[2 * i + 1];
+    }
+    dft_reg<R / 2, INV>(e);
+    dft_reg<R / 2, INV>(o);
+    dit_combine<R, INV>(e, o, y);
+  }
+}
+
+// Padded wave-private LDS index: one double2 of padding per 16 keeps the
+// strided butterfly writes off a single bank group.
+__device__ __forceinline__ int fft_pad(int idx) { return idx + (idx >> 4); }
+template <int N>
+constexpr int fft_lds_elems() { return N + N / 16; }
+
+// Stockham passes NS.. of an N-point transform.  v[t + r*(V/R)] holds index
+// lane + 64t + r*N/R; the first pass (NS == 1) reads v, the last writes it.
+#ifndef HF_FFT_MAX_RADIX
+#define HF_FFT_MAX_RADIX 16
+#endif
+constexpr int kFftMaxRadix = HF_FFT_MAX_RADIX;
+template <int N, int NS, bool INV>
+__device__ __forceinline__ void fft_passes(double2 (&v)[N / 64], double2 *lds, const double2 *__restrict__ tw,
+                                           int lane) {
+  constexpr int V = N / 64;
+  constexpr int RV = V < kFftMaxRadix ? V : kFftMaxRadix;
+  constexpr int R = RV < N / NS ? RV : N / NS;
+  constexpr int B = V / R;  // butterflies per lane
+  constexpr bool kLast = NS * R == N;
+  // the pass's inputs: the registers (first pass) or the previous pass's LDS output
+  if constexpr (NS > 1) {
+#pragma unroll
+    for (int t = 0; t < B; ++t)
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[t + r * B] = lds[fft_pad(lane + 64 * t + r * (N / R))];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's reads before any write
+  }
+  double2 (&x)[V] = v;
+#pragma unroll
+  for (int t = 0; t < B; ++t) {
+    const int j = lane + 64 * t;
+    const int k = j & (NS - 1);
+    const int m = k * (N / (R * NS));
+    double2 y[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) y[r] = (NS == 1 || r == 0) ? x[t + r * B] : cmul(x[t + r * B], plan_twiddle<N, INV>(tw, r * m));
+    dft_reg<R, INV>(y);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (kLast) v[t + r * B] = y[r];                    // index j + r*NS = lane + 64(t + rB)
+      else lds[fft_pad((j - k) * R + k + r * NS)] = y[r];
+    }
+  }
+  if constexpr (!kLast) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    fft_passes<N, NS * R, INV>(v, lds, tw, lane);
+  }
+}
+
+// Spectral Poisson of one wave's N-cell chain pair: on entry v[i] = (rho_a,
+// rho_b) at cell lane + 64i; on exit v[i] = N * (E_a, E_b) there.  The operator
+// i/k maps the FFT of a real signal to the FFT of a real signal, so the real
+// and imaginary parts of the packed transform are the two fields.  plan =
+// hf_poisson_coeffs (twiddles at plan + N, 1/k at plan + 2N).
+template <int N>
+__device__ __forceinline__ void poisson_wave(double2 (&v)[N / 64], double2 *lds, const double *__restrict__ plan,
+                                             int lane) {
+  const double2 *tw = reinterpret_cast<const double2 *>(plan + N);
+  const double *inv_k = plan + 2 * N;
+#ifndef HF_DIAG_NOFFT  // timing diagnostic only: results are wrong (no transforms)
+  fft_passes<N, 1, false>(v, lds, tw, lane);
+#endif
+#pragma unroll
+  for (int i = 0; i < N / 64; ++i) {
+    const double ik = inv_k[lane + 64 * i];  // 1j * X / k, k = 0 mode zeroed
+    v[i] = make_double2(-v[i].y * ik, v[i].x * ik);
+  }
+#ifndef HF_DIAG_NOFFT
+  fft_passes<N, 1, true>(v, lds, tw, lane);
+#endif
 }
 
 // Per-state rollout metrics, partial sums for one cell.
@@ -162,6 +236,18 @@ struct MetricAcc {
     float dv = fabsf(n - 1.0f);
     maxdev = dv > maxdev ? dv : maxdev;
     finite &= (isfinite(n) && isfinite(u) && isfinite(E)) ? 1 : 0;
+  }
+  // the same sums split in two: n, u when the update produces them, E after the solve
+  __device__ void add_nu(float n, float u) {
+    energy += (double)u * u;
+    charge += n;
+    float dv = fabsf(n - 1.0f);
+    maxdev = dv > maxdev ? dv : maxdev;
+    finite &= (isfinite(n) && isfinite(u)) ? 1 : 0;
+  }
+  __device__ void add_E(float E) {
+    energy += (double)E * E;
+    finite &= isfinite(E) ? 1 : 0;
   }
   __device__ void wave_reduce() {
 #pragma unroll

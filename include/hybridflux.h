@@ -199,7 +199,7 @@ int hf_pinn_run(const float *dev_params, int dim, int hidden, int layers, const 
  * E[i] = sum_j c[(i-j) mod nx] * (n[j]-1), computed in float64.  For power-of-two
  * nx in [256, 2048] the kernels apply the operator by float64 FFT instead and
  * the plan continues with the twiddles exp(-2 pi i m/nx), m < nx/2, as (re, im)
- * pairs, then 1/k_q (0 for q = 0).  Every dev_c argument below is a device copy
+ * pairs, then 1/k_q (0 for q = 0 and, for even nx, q = nx/2: that term is imaginary for real rho, dropped by the reference's Re()).  Every dev_c argument below is a device copy
  * of this plan.
  */
 int hf_poisson_plan_len(int nx);

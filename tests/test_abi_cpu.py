@@ -67,9 +67,20 @@ def test_poisson_coefficients_reproduce_spectral_solve(nx):
     assert np.abs(E - g[f"E_nx{nx}"]).max() < 1e-7
 
 
+def _radices(n, max_radix=16):
+    """hf_device.h fft_passes: radix R = min(n/64, 16, what is left) per pass."""
+    out, ns = [], 1
+    while ns < n:
+        r = min(n // 64, max_radix, n // ns)
+        out.append(r)
+        ns *= r
+    return out
+
+
 def _stockham(x, tw, inverse):
-    """The Stockham passes of hf_device.h fft_block, in numpy: one radix-2 pass
-    when log2 n is odd, then radix-4 passes."""
+    """The mixed-radix Stockham passes of hf_device.h fft_passes, in numpy: pass
+    (ns, R) takes x[j + r n/R] * W^(r m), m = (j mod ns) n/(R ns), for
+    butterfly j, and writes its DFT_R to (j - j mod ns) R + j mod ns + s ns."""
     n = x.size
     w_all = np.conj(tw) if inverse else tw
 
@@ -79,20 +90,17 @@ def _stockham(x, tw, inverse):
         return np.where(hi, -v, v)
 
     ns = 1
-    if (n.bit_length() - 1) % 2 == 1:
-        y = np.empty_like(x)
-        y[0::2], y[1::2] = x[: n // 2] + x[n // 2:], x[: n // 2] - x[n // 2:]
-        x, ns = y, 2
-    j = np.arange(n // 4)
-    while ns < n:
-        k = j & (ns - 1)
-        m = k * (n // (4 * ns))
-        a0, a1, a2, a3 = x[j], x[j + n // 4] * w(m), x[j + n // 2] * w(2 * m), x[j + 3 * n // 4] * w(3 * m)
-        b0, b1, b2, b3 = a0 + a2, a0 - a2, a1 + a3, (a1 - a3) * (1j if inverse else -1j)
-        d = (j - k) * 4 + k
-        y = np.empty_like(x)
-        y[d], y[d + ns], y[d + 2 * ns], y[d + 3 * ns] = b0 + b2, b1 + b3, b0 - b2, b1 - b3
-        x, ns = y, ns * 4
+    for R in _radices(n):
+        j = np.arange(n // R)
+        k = j % ns
+        m = k * (n // (R * ns))
+        xr = np.stack([x[j + r * n // R] * w(r * m) for r in range(R)])
+        F = np.exp((1 if inverse else -1) * 2j * np.pi * np.outer(np.arange(R), np.arange(R)) / R)
+        y = F @ xr
+        out = np.empty_like(x)
+        for q in range(R):
+            out[(j - k) * R + k + q * ns] = y[q]
+        x, ns = out, ns * R
     return x
 
 
@@ -100,7 +108,9 @@ def _stockham(x, tw, inverse):
 def test_poisson_fft_plan(nx):
     """For power-of-two nx >= 256 the plan carries twiddles and 1/k; the kernel's
     FFT sequence applied with them equals the reference spectral solve
-    (src/baseline_solver.py:59-68) in float64 to 1e-12."""
+    (src/baseline_solver.py:59-68) in float64 to 1e-12.  Every pass's radix
+    divides the n/64 values a lane holds (one wave per transform)."""
+    assert all((nx // 64) % r == 0 for r in _radices(nx)) and np.prod(_radices(nx)) == nx
     lib = _lib.lib()
     L = lib.hf_poisson_plan_len(nx)
     assert L == 3 * nx
@@ -116,6 +126,14 @@ def test_poisson_fft_plan(nx):
     kk = np.where(k == 0, 1.0, k)
     ref = np.real(np.fft.ifft(np.where(k == 0, 0, 1j * np.fft.fft(rho) / kk)))
     assert np.abs(E - ref).max() < 1e-12
+    # two ICs in one complex transform (the kernels' packing): the zeroed Nyquist
+    # term keeps each field free of the other's
+    rho_b = np.random.default_rng(nx + 1).standard_normal(nx) * 0.1
+    Z = _stockham(rho + 1j * rho_b, tw, False)
+    EE = _stockham(1j * Z * inv_k, tw, True) / nx
+    ref_b = np.real(np.fft.ifft(np.where(k == 0, 0, 1j * np.fft.fft(rho_b) / kk)))
+    assert np.abs(EE.real - ref).max() < 1e-12 and np.abs(EE.imag - ref_b).max() < 1e-12
+    assert inv_k[0] == 0 and inv_k[nx // 2] == 0
     assert lib.hf_poisson_plan_len(64) == 64 and lib.hf_poisson_plan_len(384) == 384
     assert lib.hf_poisson_plan_len(4096) == 4096 and lib.hf_poisson_plan_len(0) == -1
 
