@@ -82,6 +82,7 @@ struct CoreBF16 {
   static constexpr int kNW = NW;
   static constexpr int kUPC = UPC;
   static constexpr int kSlots = UPC == 4 ? 3 : 4;
+  static constexpr int kAhead = 2;
   static constexpr int kWinMT = WMT;
   static constexpr int kParkMT = WMT;
   static constexpr int kChunkFloats = 1024 * UPC;

@@ -182,22 +182,25 @@ __device__ __forceinline__ Small stage_small(const ChainW &W, float *s) {
 
 // ----------------------------------------------------------------- the ring
 // CF = chunk size in floats (2048 = 8 KiB or 4096 = 16 KiB); NW = waves sharing
-// the ring; SLOTS = LDS slots (3 suffice: at next() every wave has passed the
-// barrier with its reads of chunk pos-1 retired, so pos+2 may take that slot;
-// 4 keep the slot arithmetic a mask).
-template <int CF, int NW = kWaves, int SLOTS = kRingSlots>
+// the ring; D = chunks in flight ahead of the one being consumed (the LDS-DMA
+// fill latency, ~1.1 us from issue to landing, must fit in D chunk times);
+// SLOTS = LDS slots, at least D + 1: at next() every wave has passed the
+// barrier with its reads of chunk pos-1 retired, so pos+D may take that slot
+// (D = 2 in 3 or 4 slots for the IC-per-wave kernels; 4 slots keep the slot
+// arithmetic a mask).
+template <int CF, int NW = kWaves, int SLOTS = kRingSlots, int D = 2>
 struct Ring {
-  static_assert(SLOTS == 3 || SLOTS == 4, "ring slots");
+  static_assert(SLOTS >= D + 1 && D >= 2 && D <= 6, "ring slots / prefetch distance");
   static constexpr int kPerWave = CF / (NW * 256);  // 1 KiB DMA instructions per wave per chunk
   static_assert(kPerWave == 1 || kPerWave == 2 || kPerWave == 4, "ring chunk split over the waves");
   __amdgpu_buffer_rsrc_t rsrc;  // packed weight stream (global)
   int lane_off;                 // lane * 16 bytes (the only per-lane address term)
-  float *lds;                   // 4 slots
+  float *lds;                   // SLOTS slots
   int chunks;        // chunks per forward pass
   int wave, lane;
   int pos;           // stream position being consumed
   int rd;            // its slot (pos % SLOTS)
-  int ahead;         // chunk id of stream position pos + 2
+  int ahead;         // chunk id of stream position pos + D
 
   // The DMA is issued from inline asm, hidden from hipcc's s_waitcnt
   // bookkeeping: with a visible LDS-DMA in the kernel hipcc gives every
@@ -209,7 +212,7 @@ struct Ring {
     const unsigned d = (unsigned)(uintptr_t)(lds_void *)(lds + slot * CF);
 #pragma unroll
     for (int jj = 0; jj < kPerWave; ++jj) {
-      const int j = kPerWave * wave + jj;  // this wave's quarter of the chunk
+      const int j = kPerWave * wave + jj;  // this wave's share of the chunk
       const unsigned dst = __builtin_amdgcn_readfirstlane(d + j * 1024);
       const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(chunk * CF + j * 256) * 4u);
       unsigned keep;
@@ -221,40 +224,46 @@ struct Ring {
           : "memory");
     }
   }
-  // Start the stream at chunk 0 (positions 0 and 1 in flight).
+  // Start the stream at chunk 0 (positions 0 .. D-1 in flight).
   __device__ __forceinline__ void prime() {
     pos = 0;
     rd = 0;
-    issue(0, 0);
-    issue(1 % chunks, 1);
-    ahead = 2 % chunks;
+#pragma unroll
+    for (int i = 0; i < D; ++i) issue(i % chunks, i);
+    ahead = D % chunks;
   }
-  // Wait for chunk `pos`, keep two chunks in flight, return its slot.
+  // Wait for chunk `pos`, keep D chunks in flight, return its slot.
   __device__ __forceinline__ const float *next() {
-    // own DMA for `pos` done (only pos+1's instructions may remain), every
-    // ds_read of this wave retired, then every wave has passed: the slot of
-    // pos-2, which pos+2 is about to overwrite, is no longer read by anyone.
-    // sched_barrier(0) on both sides: the compiler may otherwise move register-only
-    // MFMAs across the asm, which orders memory operations only.
+    // own DMA for `pos` done (only the D-1 later chunks' instructions may
+    // remain), every ds_read of this wave retired, then every wave has passed:
+    // the slot pos+D is about to overwrite (pos-1's or an older one) is no
+    // longer read by anyone.  sched_barrier(0) on both sides: the compiler may
+    // otherwise move register-only MFMAs across the asm, which orders memory
+    // operations only.
     __builtin_amdgcn_sched_barrier(0);
 #if defined(HF_DIAG_NOSYNC)  // timing diagnostic only: results are wrong (no wait, no barrier, no DMA)
     if (false) {
 #elif defined(HF_DIAG_NOBAR)  // timing diagnostic only: results are wrong
     asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
 #else
-    if constexpr (kPerWave == 1)
-      asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (kPerWave == 2)
-      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    constexpr int kVm = kPerWave * (D - 1);
+    if constexpr (kVm == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 3) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 5) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 10) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 12) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else static_assert(kVm == 1, "vmcnt of the ring");
 #endif
 #if defined(HF_DIAG_NOSYNC)
     }
 #endif
     __builtin_amdgcn_sched_barrier(0);
 #if !defined(HF_DIAG_NODMA) && !defined(HF_DIAG_NOSYNC)  // timing diagnostics only
-    issue(ahead, rd + 2 >= SLOTS ? rd + 2 - SLOTS : rd + 2);
+    issue(ahead, rd + D >= SLOTS ? rd + D - SLOTS : rd + D);
 #endif
     ahead = ahead + 1 == chunks ? 0 : ahead + 1;
     const float *slot = lds + rd * CF;
@@ -266,9 +275,9 @@ struct Ring {
 };
 
 template <class Core>
-__device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW, Core::kSlots> make_ring(const ChainW &W,
-                                                                                    float *ring_lds) {
-  Ring<Core::kChunkFloats, Core::kNW, Core::kSlots> R;
+__device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW, Core::kSlots, Core::kAhead> make_ring(const ChainW &W,
+                                                                                                  float *ring_lds) {
+  Ring<Core::kChunkFloats, Core::kNW, Core::kSlots, Core::kAhead> R;
   // the packed stream is chain_chunks() chunks of chain_chunk_bytes(); a core may move it in larger chunks
   R.chunks = chain_chunks(W.layers, W.prec) * chain_chunk_bytes(W.prec) / (Core::kChunkFloats * 4);
   R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0,

@@ -21,16 +21,22 @@ namespace {
 
 using namespace chain;
 
-struct CoreF32 {
+// D = weight chunks in flight ahead of the one consumed, SLOTS = ring slots
+// (chain_common.h Ring): 2 in 4 for the IC-per-wave kernels; the cell-split
+// kernels consume a chunk in a quarter of the time (16 cells per wave) and run
+// deeper (kCellsAhead).
+template <int D = 2, int SLOTS = kRingSlots>
+struct CoreF32T {
   static constexpr int kNW = kWaves;   // waves sharing the weight ring
-  static constexpr int kSlots = kRingSlots;
+  static constexpr int kSlots = SLOTS;
+  static constexpr int kAhead = D;
   static constexpr int kWinMT = 4;     // m-tiles per wave in the windowed flux kernel
   // units per ring chunk: 4 (8 KiB chunks); 8 (16 KiB, half the barriers)
   // measured no faster, for the IC-per-wave and the cell-split kernels alike
   static constexpr int kUPC = 4;
   static constexpr int kChunkFloats = 512 * kUPC;  // 4 units of 2 KiB (2 ds_read_b128 per lane)
   static constexpr int kParkFloats = 0;
-  using R_t = Ring<kChunkFloats, kNW>;
+  using R_t = Ring<kChunkFloats, kNW, kSlots, kAhead>;
 
   // Register-prefetched weight feed.  A chunk is 4 units; unit u is the lane's
   // fragments 2u, 2u+1 and feeds 32 MFMAs (one update k-step, or four readout
@@ -315,6 +321,8 @@ struct CoreF32 {
   }
 };
 
+using CoreF32 = CoreF32T<>;
+
 // ---------------------------------------------------------------------------
 // Cell-split persistent rollout for small batches: an IC of NX = 16*WPI cells
 // on WPI waves (16 consecutive cells each, CoreF32 at MT = 1), 4/WPI ICs per
@@ -327,10 +335,15 @@ struct CoreF32 {
 // per layer they swap boundary columns of h (CellHalo), per step column 0 of
 // the readout accumulators.  The IC's first wave does FV + Poisson + outputs
 // for all its cells, one per lane (src/hybrid_solver.py:45-63).
+#ifndef HF_CELLS_AHEAD
+#define HF_CELLS_AHEAD 4
+#endif
+constexpr int kCellsAhead = HF_CELLS_AHEAD;
+using CellCore = CoreF32T<kCellsAhead, kCellsAhead + 1>;
 constexpr int kXhF4 = 2 * kWaves * 2 * 4 * kNT;  // CellHalo::xh
 constexpr int kXqF4 = kWaves * kNT * 2 * 4;      // CellHalo::xq
 constexpr int kCellsLds =
-    kRingSlots * CoreF32::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats + 4 * (kXhF4 + kXqF4);
+    CellCore::kSlots * CellCore::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats + 4 * (kXhF4 + kXqF4);
 
 template <int WPI>
 __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
@@ -340,11 +353,11 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
     float *__restrict__ flux_traj, float *__restrict__ metrics) {
   constexpr int NX = 16 * WPI;
   constexpr int IPW = kWaves / WPI;  // ICs per workgroup
-  constexpr int kRingFloats = kRingSlots * CoreF32::kChunkFloats;
+  constexpr int kRingFloats = CellCore::kSlots * CellCore::kChunkFloats;
   __shared__ f4 lds4[kCellsLds / 4];
   float *lds = reinterpret_cast<float *>(lds4);
   const Small S = stage_small(W, lds + kRingFloats);
-  auto R = make_ring<CoreF32>(W, lds);
+  auto R = make_ring<CellCore>(W, lds);
   const int wave = R.wave, lane = R.lane, j = lane & 15, g = lane >> 4;
   const bool shadow = wave >= IPW * WPI;
   const int slot = shadow ? 0 : wave / WPI;  // IC of this wave within the workgroup
@@ -392,12 +405,12 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
   };
   if (lead) emit(0);
   R.prime();
-  CoreF32::Feed F;
-  CoreF32::begin(R, F);
+  CellCore::Feed F;
+  CellCore::begin(R, F);
   for (int t = 0; t < T; ++t) {
     const float feat[1] = {s_st[g * 64 + 16 * pos + j]};
     float ff[1], fb[1];
-    CoreF32::gnn_cells(W, S, R, F, feat, ff, fb, X);
+    CellCore::gnn_cells(W, S, R, F, feat, ff, fb, X);
     if (!shadow && g == 0) s_F[16 * pos + j] = face_flux(ff[0], fb[0]);
     lds_barrier();  // every wave's face fluxes in s_F
     if (lead) {     // src/hybrid_solver.py:45-63, one cell per lane
@@ -437,11 +450,11 @@ __global__ __launch_bounds__(256, 1) void chain_flux_cells_kernel(ChainW W, cons
                                                                   float *__restrict__ fe, float *__restrict__ ff) {
   constexpr int NX = 16 * WPI;
   constexpr int IPW = kWaves / WPI;
-  constexpr int kRingFloats = kRingSlots * CoreF32::kChunkFloats;
+  constexpr int kRingFloats = CellCore::kSlots * CellCore::kChunkFloats;
   __shared__ f4 lds4[kCellsLds / 4];
   float *lds = reinterpret_cast<float *>(lds4);
   const Small S = stage_small(W, lds + kRingFloats);
-  auto R = make_ring<CoreF32>(W, lds);
+  auto R = make_ring<CellCore>(W, lds);
   const int wave = R.wave, lane = R.lane, j = lane & 15, g = lane >> 4;
   const bool shadow = wave >= IPW * WPI;
   const int slot = shadow ? 0 : wave / WPI, pos = shadow ? 0 : wave % WPI;
@@ -461,10 +474,10 @@ __global__ __launch_bounds__(256, 1) void chain_flux_cells_kernel(ChainW W, cons
                             : (g < 3 ? state[b * ld_state + (int64_t)g * NX + cell] : x[cell])};
   __syncthreads();  // small weights staged (no DMA in flight yet)
   R.prime();
-  CoreF32::Feed F;
-  CoreF32::begin(R, F);
+  CellCore::Feed F;
+  CellCore::begin(R, F);
   float f_fwd[1], f_bwd[1];
-  CoreF32::gnn_cells(W, S, R, F, feat, f_fwd, f_bwd, X);
+  CellCore::gnn_cells(W, S, R, F, feat, f_fwd, f_bwd, X);
   R.drain();
   if (!out) return;
   if (fe && g == 0) fe[b * 2 * NX + cell] = f_fwd[0];

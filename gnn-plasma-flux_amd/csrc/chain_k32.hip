@@ -85,6 +85,7 @@ struct CoreF16x3T {
   static constexpr int kNW = kWaves;
   static constexpr int kUPC = UPC;
   static constexpr int kSlots = UPC == 2 ? 3 : 4;
+  static constexpr int kAhead = 2;
   static constexpr int kWinMT = 4;
   static constexpr int kChunkFloats = 2048 * UPC;
   static constexpr int kKB = kH / 32;
