@@ -77,11 +77,12 @@ __device__ __forceinline__ void interleave() {
 // the next unit's fragments one unit ahead (16 more registers: the rollout's
 // one wave per SIMD has them; at two waves per SIMD the partner wave covers
 // the latency and the registers are what let two waves fit).
-template <int NW, int UPC, int WMT = 4, bool PF = false>
+template <int NW, int UPC, int WMT = 4, bool PF = false, int SLOTS = (UPC == 4 ? 3 : 4), int WG = 1, int DMAU = 0>
 struct CoreBF16 {
   static constexpr int kNW = NW;
+  static constexpr int kWGPerCU = WG;
   static constexpr int kUPC = UPC;
-  static constexpr int kSlots = UPC == 4 ? 3 : 4;
+  static constexpr int kSlots = SLOTS;
   static constexpr int kAhead = 2;
   static constexpr int kWinMT = WMT;
   static constexpr int kParkMT = WMT;
@@ -89,7 +90,13 @@ struct CoreBF16 {
   static constexpr int kKB = kH / 32;
   // parked h fragments of k-blocks 0..2: [kb 3][mt kParkMT][lane 64][4 dwords]
   static constexpr int kParkFloats = 3 * kParkMT * 64 * 4;
-  using R_t = Ring<kChunkFloats, NW, kSlots>;
+  // DMAU >= 0: the ring's DMA for chunk p+2 is issued in unit DMAU of chunk p
+  // (after that unit's fragment reads) instead of right after the ring
+  // barrier, where all waves' DMA and fragment reads would queue together:
+  // cfg4 3-5 % less time at DMAU = 0 (unit 3: 2-3 %, units 1-2: 2 %; spreading
+  // the DMA over the units by wave number: 10 % more), tools/gpu_diag_cfg4.sh.
+  static constexpr int kDmaUnit = DMAU;
+  using R_t = Ring<kChunkFloats, NW, kSlots, 2, (DMAU >= 0)>;
 
   template <int MT>
   struct Acts {
@@ -120,11 +127,13 @@ struct CoreBF16 {
     if constexpr (PF) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) w[i] = F.cur[i];
+      if constexpr (U == kDmaUnit) R.issue_pending();
       if constexpr (U == UPC - 1) F.slot = R.next();
       load_unit(F, (U + 1) % UPC, R.lane);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) w[i] = __builtin_bit_cast(u4, ldf4(F.slot + ((4 * U + i) * 64 + R.lane) * 4));
+      if constexpr (U == kDmaUnit) R.issue_pending();
       if constexpr (U == UPC - 1) F.slot = R.next();
     }
   }
@@ -166,6 +175,11 @@ struct CoreBF16 {
   template <int MT, int K>
   static __device__ __forceinline__ void piece(Pair<MT> &P, u4 (&nh)[MT]) {
     constexpr int t = K >> 1, r0 = 2 * (K & 1);
+#ifdef HF_DIAG_NOPIECE  // timing diagnostic only: results are wrong (one convert per dword, no epilogue VALU)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) nh[mt][K] = pk_bf16(P.a[mt][t][r0], P.g[mt][t][r0 + 1]);
+    return;
+#endif
     float z[2][MT];
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
@@ -282,6 +296,11 @@ struct CoreBF16 {
   template <int MT, int RP>
   static __device__ __forceinline__ void ro_piece(const f4 (&P)[MT], const f4 (&Q)[MT], const f4 &w2, float (&pf)[MT],
                                                   float (&pb)[MT]) {
+#ifdef HF_DIAG_NOROPIECE  // timing diagnostic only: results are wrong (one add per accumulator pair)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) pf[mt] += P[mt][2 * RP] + Q[mt][2 * RP + 1];
+    return;
+#endif
 #pragma unroll
     for (int r = 2 * RP; r < 2 * RP + 2; ++r) {
       float pv[MT], qv[MT], pr[MT], qr[MT];
@@ -439,7 +458,7 @@ hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float 
 hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float *state_final, const float *x,
                                      const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                      float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
-  return chain::launch_rollout_core<CoreBF16<4, 2, 4, true>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
+  return chain::launch_rollout_core<CoreBF16<4, 2, 4, true, 4, 1, -1>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
                                                              flux_traj, metrics, ex, s);
 }
 

@@ -188,7 +188,9 @@ __device__ __forceinline__ Small stage_small(const ChainW &W, float *s) {
 // barrier with its reads of chunk pos-1 retired, so pos+D may take that slot
 // (D = 2 in 3 or 4 slots for the IC-per-wave kernels; 4 slots keep the slot
 // arithmetic a mask).
-template <int CF, int NW = kWaves, int SLOTS = kRingSlots, int D = 2>
+// DEFER: next() only waits and barriers; the DMA it owes (chunk pos+D into the
+// slot just released) is issued by issue_pending() at a point the core picks.
+template <int CF, int NW = kWaves, int SLOTS = kRingSlots, int D = 2, bool DEFER = false>
 struct Ring {
   static_assert(SLOTS >= D + 1 && D >= 2 && D <= 6, "ring slots / prefetch distance");
   static constexpr int kPerWave = CF / (NW * 256);  // 1 KiB DMA instructions per wave per chunk
@@ -201,6 +203,7 @@ struct Ring {
   int pos;           // stream position being consumed
   int rd;            // its slot (pos % SLOTS)
   int ahead;         // chunk id of stream position pos + D
+  int pend_chunk, pend_slot;  // DEFER: the DMA owed since the last next()
 
   // The DMA is issued from inline asm, hidden from hipcc's s_waitcnt
   // bookkeeping: with a visible LDS-DMA in the kernel hipcc gives every
@@ -208,10 +211,10 @@ struct Ring {
   // ring's own counted vmcnt + barrier in next() order the DMA for readers.
   // buffer_load ... lds: the chunk offset is an SGPR (soffset), the lane
   // offset a fixed VGPR, so an issue costs no VALU address arithmetic.
-  __device__ __forceinline__ void issue(int chunk, int slot) const {
+  __device__ __forceinline__ void issue(int chunk, int slot, int j0 = 0, int j1 = kPerWave) const {
     const unsigned d = (unsigned)(uintptr_t)(lds_void *)(lds + slot * CF);
 #pragma unroll
-    for (int jj = 0; jj < kPerWave; ++jj) {
+    for (int jj = j0; jj < j1; ++jj) {
       const int j = kPerWave * wave + jj;  // this wave's share of the chunk
       const unsigned dst = __builtin_amdgcn_readfirstlane(d + j * 1024);
       const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(chunk * CF + j * 256) * 4u);
@@ -263,7 +266,12 @@ struct Ring {
 #endif
     __builtin_amdgcn_sched_barrier(0);
 #if !defined(HF_DIAG_NODMA) && !defined(HF_DIAG_NOSYNC)  // timing diagnostics only
-    issue(ahead, rd + D >= SLOTS ? rd + D - SLOTS : rd + D);
+    if constexpr (DEFER) {
+      pend_chunk = ahead;
+      pend_slot = rd + D >= SLOTS ? rd + D - SLOTS : rd + D;
+    } else {
+      issue(ahead, rd + D >= SLOTS ? rd + D - SLOTS : rd + D);
+    }
 #endif
     ahead = ahead + 1 == chunks ? 0 : ahead + 1;
     const float *slot = lds + rd * CF;
@@ -271,13 +279,18 @@ struct Ring {
     ++pos;
     return slot;
   }
+  // DEFER: issue the DMA the last next() owes (before the next next()).
+  __device__ __forceinline__ void issue_pending(int j0 = 0, int j1 = kPerWave) const {
+#if !defined(HF_DIAG_NODMA) && !defined(HF_DIAG_NOSYNC)
+    if constexpr (DEFER) issue(pend_chunk, pend_slot, j0, j1);
+#endif
+  }
   __device__ __forceinline__ void drain() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 };
 
 template <class Core>
-__device__ __forceinline__ Ring<Core::kChunkFloats, Core::kNW, Core::kSlots, Core::kAhead> make_ring(const ChainW &W,
-                                                                                                  float *ring_lds) {
-  Ring<Core::kChunkFloats, Core::kNW, Core::kSlots, Core::kAhead> R;
+__device__ __forceinline__ typename Core::R_t make_ring(const ChainW &W, float *ring_lds) {
+  typename Core::R_t R;
   // the packed stream is chain_chunks() chunks of chain_chunk_bytes(); a core may move it in larger chunks
   R.chunks = chain_chunks(W.layers, W.prec) * chain_chunk_bytes(W.prec) / (Core::kChunkFloats * 4);
   R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0,
@@ -407,7 +420,7 @@ __device__ __forceinline__ void input_layer(const Small &S, int lane, const floa
 //         [L, 16MT-2-L] of the window (16MT - 1 - 2L per window, L = update
 //         layers) are exact, the rest discarded.
 template <class Core, int MT, bool EXACT>
-__global__ __launch_bounds__(64 * Core::kNW, 1) void chain_flux_kernel(ChainW W, const float *__restrict__ nf,
+__global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_flux_kernel(ChainW W, const float *__restrict__ nf,
                                                             const float *__restrict__ state,
                                                             int64_t ld_state,
                                                             const float *__restrict__ x, int nx,
@@ -431,30 +444,56 @@ __global__ __launch_bounds__(64 * Core::kNW, 1) void chain_flux_kernel(ChainW W,
   // artificial wrap; faces [L, 62 - L] of a 64-cell window are exact
   const int halo = W.layers, win_faces = win_faces_of(W.layers, 16 * MT);
   const int64_t groups = (items + Core::kNW - 1) / Core::kNW;
-  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+  // item (IC b, window w) of this wave in group grp; idle waves mirror a real item and write nothing
+  auto locate = [&](int64_t grp, int64_t &b, int &w) {
     const int64_t item_raw = grp * Core::kNW + R.wave;
-    const bool live = item_raw < items;
-    const int64_t item = live ? item_raw : items - 1;  // idle waves mirror a real item, write nothing
-    const int64_t b = item / nwin;
-    const int w = (int)(item - b * nwin);
-    const int start = EXACT ? 0 : w * win_faces - halo;
-    float feat[MT];
-    int cell[MT];
+    const int64_t item = item_raw < items ? item_raw : items - 1;
+    b = item / nwin;
+    w = (int)(item - b * nwin);
+    return item_raw < items;
+  };
+  auto cell_at = [&](int w, int mt) {
+    int cidx = ((EXACT ? 0 : w * win_faces - halo) + cell_of<MT>(mt, j)) % nx;
+    return cidx < 0 ? cidx + nx : cidx;
+  };
+  // node features of group grp: n, u, E, x of the wave's 16*MT cells (lane group g = feature g)
+  auto load_feat = [&](int64_t grp, float (&feat)[MT]) {
+    int64_t b;
+    int w;
+    locate(grp, b, w);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      int cidx = (start + cell_of<MT>(mt, j)) % nx;
-      if (cidx < 0) cidx += nx;
-      cell[mt] = cidx;
+      const int cidx = cell_at(w, mt);
+#ifdef HF_DIAG_NOFEAT  // timing diagnostic only: results are wrong (no feature loads, no flux stores)
+      feat[mt] = 0.01f * (float)(cidx + g);
+#else
       feat[mt] = nf ? nf[(b * nx + cidx) * kIn + g]
                     : (g < 3 ? state[b * ld_state + (int64_t)g * nx + cidx] : x[cidx]);
+#endif
     }
+  };
+  // The next group's features are loaded while this group's forward runs.
+  float pre[MT];
+  if (blockIdx.x < groups) load_feat(blockIdx.x, pre);
+  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    float feat[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) feat[mt] = pre[mt];
+    if (grp + gridDim.x < groups) load_feat(grp + gridDim.x, pre);
     float f_fwd[MT], f_bwd[MT];
     Core::template gnn<MT>(W, S, R, F, park_of<Core, false>(lds, R.wave), feat, f_fwd, f_bwd);
+    int64_t b;
+    int w;
+    const bool live = locate(grp, b, w);
+#ifdef HF_DIAG_NOFEAT
+    if (live && f_fwd[0] == 12345.f) {  // keeps the forward live; never true in practice
+#else
     if (live) {
+#endif
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int wc = cell_of<MT>(mt, j);
-        int face = cell[mt];
+        int face = cell_at(w, mt);
         bool ok = true;
         if (!EXACT) {
           face = w * win_faces + (wc - halo);
@@ -620,7 +659,8 @@ template <class Core, int MT, bool EXACT>
 hipError_t flux_launch(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
                        int nx, int nwin, int64_t items, float *fe, float *ff, hipStream_t s) {
   const int64_t groups = (items + Core::kNW - 1) / Core::kNW;
-  const int64_t blocks = groups < resident_groups() ? groups : resident_groups();  // persistent: 1 per CU
+  const int64_t res = (int64_t)resident_groups() * Core::kWGPerCU;  // persistent: kWGPerCU per CU
+  const int64_t blocks = groups < res ? groups : res;
   hipLaunchKernelGGL((chain_flux_kernel<Core, MT, EXACT>), dim3((unsigned)blocks), dim3(64 * Core::kNW), 0, s,
                      w, nf, state, ld_state, x, nx, nwin, items, fe, ff);
   return hipGetLastError();
