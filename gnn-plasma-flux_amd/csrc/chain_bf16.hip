@@ -396,6 +396,41 @@ struct CoreBF16 {
     readout_finish<MT>(pf, pb, W.b2, ffwd, fbwd);
   }
 
+  // Input MLP h0 = ReLU(W_in x + b_in) (src/flux_gnn.py:49), one bf16 MFMA per
+  // 16-feature tile: lane group g's k-slots 8g, 8g+1 hold x_hi = bf16(x_g) and
+  // x_lo = bf16(x_g - x_hi) against W_in[:, g] twice (W_in is bf16 in this
+  // precision), so the product is W_in x to ~2^-17 relative, accumulated in f32,
+  // at half the MFMA cycles of the f32 16x16x4 form.  ReLU, then bf16 pairs.
+  template <int MT>
+  static __device__ __forceinline__ void input(const Small &S, int lane, const float (&feat)[MT], Acts<MT> &X,
+                                               f4 (&h67)[MT][2]) {
+    const int g4 = 4 * (lane >> 4);
+    u4 bx[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const float hi = __uint_as_float(pk_bf16(feat[mt], 0.f) << 16);
+      bx[mt] = u4{pk_bf16(feat[mt], __fsub_rn(feat[mt], hi)), 0u, 0u, 0u};
+    }
+    const f4 a0 = ldf4(S.win + lane * 4), a1 = ldf4(S.win + 256 + lane * 4);
+#pragma unroll
+    for (int kb = 0; kb < kKB; ++kb) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int nt = 2 * kb + t;
+        const float w = nt < 4 ? a0[nt & 3] : a1[nt & 3];
+        const u4 aw = u4{pk_bf16(w, w), 0u, 0u, 0u};
+        const f4 bias = ldf4(S.bin + 16 * nt + g4);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const f4 h = relu4(mma(aw, bx[mt], bias));
+          X.h[mt][kb][2 * t] = pk_bf16(h[0], h[1]);
+          X.h[mt][kb][2 * t + 1] = pk_bf16(h[2], h[3]);
+          if (kb == kKB - 1) h67[mt][t] = h;
+        }
+      }
+    }
+  }
+
   template <int MT>
   static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &F, float *park,
                                              const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
@@ -404,16 +439,8 @@ struct CoreBF16 {
     Acts<MT> X;
     Pair<MT> pend;
     {
-      f4 h[MT][kNT];
-      input_layer<MT>(S, lane, feat, h);  // f32 MFMA, ReLU applied
-#pragma unroll
-      for (int kb = 0; kb < kKB; ++kb)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int t = k >> 1, r = 2 * (k & 1);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) X.h[mt][kb][k] = pk_bf16(h[mt][2 * kb + t][r], h[mt][2 * kb + t][r + 1]);
-        }
+      f4 h67[MT][2];  // tiles 6, 7 in f32 (the L = 0 hand-off below)
+      input<MT>(S, lane, feat, X, h67);
       if (W.layers == 0) {
         // no update layer: hand the readout the input layer's output the way
         // a last layer would (k-blocks 0..2 parked, tiles 6, 7 pending with a
@@ -424,8 +451,8 @@ struct CoreBF16 {
           for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<u4 *>(park_at(park, kb, mt, lane)) = X.h[mt][kb];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          pend.a[mt][0] = h[mt][6];
-          pend.a[mt][1] = h[mt][7];
+          pend.a[mt][0] = h67[mt][0];
+          pend.a[mt][1] = h67[mt][1];
           pend.g[mt][0] = pend.g[mt][1] = f4{0.f, 0.f, 0.f, 0.f};
         }
       }

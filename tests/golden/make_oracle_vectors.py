@@ -6,8 +6,9 @@ has no counterpart: the bf16 arithmetic of BASELINE config 4.
 bf16_nx1024.npz  W1_r2, seeds 1000..1003 (the first ICs of bench.py's cfg4
                  batch), nx=1024, dt=3.125e-4, T=30 (the cfg4 horizon):
                    states_emul  [4,31,3,1024]  oracle.hybrid_flux_edge_bf16 (the
-                                bf16 kernels' own arithmetic, emulated: shift-form
-                                aggregation, CoreBF16S)
+                                bf16 kernels' own arithmetic, emulated: bf16 weights
+                                and GEMM inputs, hi+lo split input features, f32
+                                accumulation; CoreBF16)
                    states_wbf16 [4,31,3,1024]  float32 reference forward on
                                 bf16-rounded weights (oracle.bf16_weights)
                  and the first-step edge fluxes of both.

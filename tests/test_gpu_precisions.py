@@ -125,14 +125,20 @@ def test_f16x3_range(hf):
 # profiles/r02_v3_parity_errors.json): flux vs EMUL 1.3e-5 (nx=64) / 5.3e-4
 # (nx=1024), vs WBF16 2.4e-3 / 3.4e-3 (flux range 0.40 / 0.53); 30-step
 # states vs EMUL 4.4e-4 / 3.5e-4, vs WBF16 1.9e-3 / 3.8e-3; random weights
-# (rand_sd, larger activations) flux vs EMUL up to 6.3e-4.  The EMUL errors
+# (rand_sd, larger activations) flux vs EMUL up to 1.8e-3.  The EMUL errors
 # are rare bf16 rounding flips of single activations (one bf16 ulp of one
-# GEMM input), so they grow with the number of values compared.
+# GEMM input), so their MAXIMUM is a lottery that grows with the number of
+# values compared: the oracle itself, accumulating in float32 instead of
+# float64, differs from its own float64 form by up to 1.3e-3 on the
+# random-weight cases (max over 5 ICs; mean 7e-6).  Random-weight cases are
+# therefore held to a flip-sized maximum plus a MEAN error bound, which a
+# systematic error (wrong neighbour, wrong weight, wrong rounding mode) breaks.
 BF16_FLUX_EMUL = 1.1e-3    # edge flux vs EMUL, one evaluation
 BF16_STATE_EMUL = 1e-3     # 30-step state vs EMUL
 BF16_FLUX_WBF16 = 7.5e-3   # edge flux vs WBF16
 BF16_STATE_WBF16 = 1e-2    # 30-step state vs WBF16
-BF16_FLUX_EMUL_RAND = 1.3e-3  # edge flux vs EMUL, random weights
+BF16_FLUX_EMUL_RAND = 4e-3    # edge flux vs EMUL, random weights: max (a few flips)
+BF16_FLUX_EMUL_RAND_MEAN = 5e-5  # ... and mean |error|
 
 
 def _bf16_solver(hf, nx, dt):
@@ -222,4 +228,6 @@ def test_bf16_flux_layers_and_nx(hf, record, layers, nx):
     with torch.no_grad():
         fe = m(nf, ei).cpu().numpy().reshape(5, 2 * nx)
     record(f"bf16_flux_L{layers}_nx{nx}", "max_abs_vs_emul", np.abs(fe - want).max())
+    record(f"bf16_flux_L{layers}_nx{nx}", "mean_abs_vs_emul", np.abs(fe - want).mean())
     close(fe, want, BF16_FLUX_EMUL_RAND)
+    assert np.abs(fe - want).mean() <= BF16_FLUX_EMUL_RAND_MEAN
