@@ -178,6 +178,13 @@ void pack_chain(const float *p, int L, int prec, ChainPack &P) {
             const int kb = j >> 1, pq = j & 1;
             frag(p + lay.w_e, 2 * kH, 16 * ot + (lane & 15), pq * kH, kb, lane, t, false);
           }
+    // bf16: a copy of the first two units (8 KiB) after the pass, so the
+    // super-window flux kernel can read the pass as 16 KiB chunks offset by two
+    // units (hf::kBF16StreamTail; chain_bf16.hip CoreBF16<..., XCH>)
+    if (prec == hf::kPrecBF16) {
+      const std::vector<unsigned char> head(out.begin(), out.begin() + hf::kBF16StreamTail);
+      out.insert(out.end(), head.begin(), head.end());
+    }
   }
   std::vector<float> &sm = P.small;
   sm.clear();

@@ -53,13 +53,13 @@ __device__ __forceinline__ f4 mma(const u4 &a, const u4 &b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
 }
 
-// Closes one unit's scheduling region: the unit's 4 ds_reads first, then one
-// MFMA and up to NV VALU (epilogue work of the previous pair) at a time.  The
-// sched_barrier keeps the next unit's reads from being picked for this unit's
-// DS group.
-template <int NM, int NV>
+// Closes one unit's scheduling region: ND ds_reads first (the unit's 4
+// fragments, or the seam reads after a ring barrier), then one MFMA and up to
+// NV VALU (epilogue work of the previous pair) at a time.  The sched_barrier
+// keeps the next unit's reads from being picked for this unit's DS group.
+template <int NM, int NV, int ND = 4>
 __device__ __forceinline__ void interleave() {
-  __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+  __builtin_amdgcn_sched_group_barrier(0x100, ND, 0);
 #pragma unroll
   for (int i = 0; i < NM; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -77,8 +77,19 @@ __device__ __forceinline__ void interleave() {
 // the next unit's fragments one unit ahead (16 more registers: the rollout's
 // one wave per SIMD has them; at two waves per SIMD the partner wave covers
 // the latency and the registers are what let two waves fit).
-template <int NW, int UPC, int WMT = 4, bool PF = false, int SLOTS = (UPC == 4 ? 3 : 4), int WG = 1, int DMAU = 0>
+//
+// XCH (super-windows, chain_flux_sw_kernel): the NW waves of a workgroup hold
+// consecutive 64-cell pieces of one long chain, overlapping by one cell, and
+// trade the G values of their edge cells through LDS every layer, so only the
+// workgroup's two outer edges see a wrong neighbour.  The trade needs a ring
+// barrier between the pair whose G it is and that pair's epilogue: the ring's
+// chunks start two units into a pair (the packed stream carries a copy of its
+// first two units after the pass, kBF16StreamTail), so the barrier falls
+// between unit 1's fragment reads and its MFMAs, after the seam publish in unit 0.
+template <int NW, int UPC, int WMT = 4, bool PF = false, int SLOTS = (UPC == 4 ? 3 : 4), int WG = 1, int DMAU = 0,
+          bool XCH = false>
 struct CoreBF16 {
+  static_assert(!XCH || (UPC == 4 && !PF && WMT == 4), "super-window core: 16 KiB chunks, 64-cell waves");
   static constexpr int kNW = NW;
   static constexpr int kWGPerCU = WG;
   static constexpr int kUPC = UPC;
@@ -88,8 +99,11 @@ struct CoreBF16 {
   static constexpr int kParkMT = WMT;
   static constexpr int kChunkFloats = 1024 * UPC;
   static constexpr int kKB = kH / 32;
+  static constexpr int kStreamOffset = XCH ? kBF16StreamTail : 0;
   // parked h fragments of k-blocks 0..2: [kb 3][mt kParkMT][lane 64][4 dwords]
   static constexpr int kParkFloats = 3 * kParkMT * 64 * 4;
+  // seam trade buffer (XCH): [parity 2][wave NW][side 2][g 4][tile 2] f4
+  static constexpr int kSeamF4 = XCH ? 2 * NW * 2 * 4 * 2 : 0;
   // DMAU >= 0: the ring's DMA for chunk p+2 is issued in unit DMAU of chunk p
   // (after that unit's fragment reads) instead of right after the ring
   // barrier, where all waves' DMA and fragment reads would queue together:
@@ -97,6 +111,8 @@ struct CoreBF16 {
   // the DMA over the units by wave number: 10 % more), tools/gpu_diag_cfg4.sh.
   static constexpr int kDmaUnit = DMAU;
   using R_t = Ring<kChunkFloats, NW, kSlots, 2, (DMAU >= 0)>;
+  // ring position of pair-unit U (of readout unit U: the same, counted from the readout's start)
+  static constexpr int pos(int U) { return XCH ? (U + 2) & 3 : U % UPC; }
 
   template <int MT>
   struct Acts {
@@ -108,6 +124,60 @@ struct CoreBF16 {
     f4 a[MT][2], g[MT][2];
   };
 
+  // XCH: this wave's view of the seam trade.  Side 0 = the wave's cell 1
+  // (tile 1, lane column 0), read by the LEFT wave for its cell 63's right
+  // neighbour; side 1 = cell 62 (tile 2, column 15), read by the RIGHT wave for
+  // its cell 0's left neighbour (waves overlap by one cell: cell 63 of wave w
+  // is cell 0 of wave w+1).
+  struct Seam {
+    f4 *pubw;  // this wave's side-0 slots at parity 0 (wave-uniform; side 1 is +8)
+    f4 *rdl;   // the left wave's side-1 slots at parity 0 (wave-uniform)
+    f4 *rdr;   // the right wave's side-0 slots at parity 0 (wave-uniform)
+    // (waves 0 and NW-1 read each other: the super-window's ends are wrong after
+    // any update layer and never output; with no update layer the traded G is
+    // zero, so the ends stay exact)
+    int par;
+    // [parity 2][wave NW][side 2][g 4][tile 2] f4
+    static __device__ __forceinline__ int slot(int w, int side) { return (w * 2 + side) * 8; }
+    // This lane's id, from v_mbcnt in an opaque statement at each use: the
+    // compiler then holds no per-lane seam address across the pass (held ones
+    // were spilled, and each scratch reload waited for the ring's DMA).
+    static __device__ __forceinline__ int lane_id() {
+      int l;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+      return l;
+    }
+  };
+  template <int MT>
+  static __device__ __forceinline__ void publish(const Seam &sm, const Pair<MT> &P) {
+#ifdef HF_DIAG_NOSEAM  // timing diagnostic only: results are wrong (no seam trade)
+    return;
+#endif
+    if constexpr (XCH) {
+      const int l = Seam::lane_id(), j = l & 15;
+      f4 *p = sm.pubw + sm.par * (NW * 16) + ((l >> 4) << 1);
+      if (j == 0) {
+        p[0] = P.g[1][0];
+        p[1] = P.g[1][1];
+      }
+      if (j == 15) {
+        p[8] = P.g[MT - 2][0];
+        p[9] = P.g[MT - 2][1];
+      }
+    }
+  }
+  // After the ring barrier that follows publish(): the neighbours' seam G of
+  // tile t (lanes j = 0 use L, lanes j = 15 use R).
+  static __device__ __forceinline__ void seam_read(const Seam &sm, int t, f4 &L, f4 &R) {
+#ifdef HF_DIAG_NOSEAM
+    L = R = f4{0.f, 0.f, 0.f, 0.f};
+    return;
+#endif
+    const int o = sm.par * (NW * 16) + ((Seam::lane_id() >> 4) << 1) + t;
+    L = sm.rdl[o];
+    R = sm.rdr[o];
+  }
+
   struct Feed {
     const float *slot;
     u4 cur[4];
@@ -118,10 +188,13 @@ struct CoreBF16 {
   }
   static __device__ __forceinline__ void begin(R_t &R, Feed &F) {
     F.slot = R.next();
+    // XCH starts at position 2 of the first chunk: no position kDmaUnit = 0
+    // comes before the next barrier, so the DMA owed now is issued now
+    if constexpr (XCH) R.issue_pending();
     if constexpr (PF) load_unit(F, 0, R.lane);
   }
-  // The 4 fragments of ring unit U (the last unit of a chunk also waits for,
-  // and releases, the next chunk).
+  // The 4 fragments at ring position U (the last position of a chunk also
+  // waits for, and releases, the next chunk).
   template <int U>
   static __device__ __forceinline__ void take(R_t &R, Feed &F, u4 (&w)[4]) {
     if constexpr (PF) {
@@ -142,11 +215,9 @@ struct CoreBF16 {
     return park + ((kb * kParkMT + mt) * 64 + lane) * 4;
   }
 
-  // One unit of an update pair: k-block KB, fragments w[2t] = W_a, w[2t+1] = W_b/2 of tile t.
-  template <int MT, int KB, int U>
-  static __device__ __forceinline__ void unit(R_t &R, Feed &F, const Acts<MT> &X, Pair<MT> &P) {
-    u4 w[4];
-    take<U>(R, F, w);
+  // MFMAs of one update unit: k-block KB, fragments w[2t] = W_a, w[2t+1] = W_b/2 of tile t.
+  template <int MT, int KB>
+  static __device__ __forceinline__ void unit_mfma(const u4 (&w)[4], const Acts<MT> &X, Pair<MT> &P) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -154,6 +225,12 @@ struct CoreBF16 {
         P.a[mt][t] = mma(w[2 * t], X.h[mt][KB], P.a[mt][t]);
         P.g[mt][t] = mma(w[2 * t + 1], X.h[mt][KB], P.g[mt][t]);
       }
+  }
+  template <int MT, int KB>
+  static __device__ __forceinline__ void unit(R_t &R, Feed &F, const Acts<MT> &X, Pair<MT> &P) {
+    u4 w[4];
+    take<pos(KB)>(R, F, w);
+    unit_mfma<MT, KB>(w, X, P);
   }
 
   // b_l enters A as the C operand of its first MFMA
@@ -172,26 +249,70 @@ struct CoreBF16 {
 
   // Dword K of the k-block fragment made from one output pair (tile t = K>>1,
   // rows r0 = 2(K&1), r0+1): z = A + (G(i-1) + G(i+1)), ReLU, bf16 pairs.
-  template <int MT, int K>
-  static __device__ __forceinline__ void piece(Pair<MT> &P, u4 (&nh)[MT]) {
+  // PART 0: every m-tile (periodic 16*MT-cell window); 1: the inner m-tiles
+  // 1..MT-2; 2 (XCH): the edge m-tiles 0 and MT-1, whose lane-column-0 left /
+  // column-15 right neighbours are the seam values L / R of tile t.
+  template <int MT, int K, int PART = 0>
+  static __device__ __forceinline__ void piece(Pair<MT> &P, u4 (&nh)[MT], const f4 &L = f4{}, const f4 &R = f4{}) {
     constexpr int t = K >> 1, r0 = 2 * (K & 1);
 #ifdef HF_DIAG_NOPIECE  // timing diagnostic only: results are wrong (one convert per dword, no epilogue VALU)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) nh[mt][K] = pk_bf16(P.a[mt][t][r0], P.g[mt][t][r0 + 1]);
+    for (int mt = 0; mt < MT; ++mt)
+      if (PART == 0 || (PART == 1) == (mt > 0 && mt < MT - 1)) nh[mt][K] = pk_bf16(P.a[mt][t][r0], P.g[mt][t][r0 + 1]);
     return;
 #endif
-    float z[2][MT];
+    if constexpr (PART == 0) {
+      float z[2][MT];
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      float v[MT], sm[MT];
+      for (int rr = 0; rr < 2; ++rr) {
+        float v[MT], sm[MT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) v[mt] = P.g[mt][t][r0 + rr];
-      nb_sum<MT>(v, sm);
+        for (int mt = 0; mt < MT; ++mt) v[mt] = P.g[mt][t][r0 + rr];
+        nb_sum<MT>(v, sm);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) z[rr][mt] = __fadd_rn(P.a[mt][t][r0 + rr], sm[mt]);
+        for (int mt = 0; mt < MT; ++mt) z[rr][mt] = __fadd_rn(P.a[mt][t][r0 + rr], sm[mt]);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) nh[mt][K] = pk_bf16(relu(z[0][mt]), relu(z[1][mt]));
+    } else if constexpr (PART == 1) {
+#pragma unroll
+      for (int mt = 1; mt < MT - 1; ++mt) {
+        float z[2];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          const int r = r0 + rr;
+          z[rr] = __fadd_rn(P.a[mt][t][r], __fadd_rn(P.g[mt - 1][t][r], P.g[mt + 1][t][r]));
+        }
+        nh[mt][K] = pk_bf16(relu(z[0]), relu(z[1]));
+      }
+    } else {
+      float z0[2], z1[2];
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int r = r0 + rr;
+        // cell 4j: left = cell 4j-1 (tile MT-1, column j-1), the seam value L at
+        // j = 0.  Every lane first forms L + G(4j+1); one v_add_f32_dpp row_shr:1
+        // without bound_ctrl then overwrites lanes j >= 1 with G(4j-1) + G(4j+1)
+        // and leaves lane 0 (no source lane) as it is: the same single fp32 add
+        // of the two neighbours in every lane.  (Inline asm: hipcc folds a DPP
+        // mov into an add only when the mov's old value is zero.  The output is
+        // tied to the compiler-written sum, and both sources are MFMA results of
+        // the previous pair, so the asm adds no register hazard.)
+        float sl = __fadd_rn(L[r], P.g[1][t][r]);
+        asm("v_add_f32_dpp %0, %1, %2 row_shr:1 row_mask:0xf bank_mask:0xf"
+            : "+v"(sl)
+            : "v"(P.g[MT - 1][t][r]), "v"(P.g[1][t][r]));
+        z0[rr] = __fadd_rn(P.a[0][t][r], sl);
+        // cell 4j+MT-1: right = cell 4j+MT (tile 0, column j+1), the seam value R at j = 15
+        float sr = __fadd_rn(R[r], P.g[MT - 2][t][r]);
+        asm("v_add_f32_dpp %0, %1, %2 row_shl:1 row_mask:0xf bank_mask:0xf"
+            : "+v"(sr)
+            : "v"(P.g[0][t][r]), "v"(P.g[MT - 2][t][r]));
+        z1[rr] = __fadd_rn(P.a[MT - 1][t][r], sr);
+      }
+      nh[0][K] = pk_bf16(relu(z0[0]), relu(z0[1]));
+      nh[MT - 1][K] = pk_bf16(relu(z1[0]), relu(z1[1]));
     }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) nh[mt][K] = pk_bf16(relu(z[0][mt]), relu(z[1][mt]));
   }
 
   // Output pair q >= 1, with the epilogue of pair q-1 (prev) spread over its 4
@@ -199,20 +320,46 @@ struct CoreBF16 {
   template <int MT>
   static __device__ __forceinline__ void pair_with_prev(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int q,
                                                         int g4, Pair<MT> &acc, Pair<MT> &prev, float *park,
-                                                        int lane) {
+                                                        int lane, Seam &sm) {
     init<MT>(bias, q, g4, acc);
     u4 nh[MT];
-    unit<MT, 0, 0 % UPC>(R, F, X, acc);
-    piece<MT, 0>(prev, nh);
-    interleave<4 * MT, 2>();
-    unit<MT, 1, 1 % UPC>(R, F, X, acc);
-    piece<MT, 1>(prev, nh);
-    interleave<4 * MT, 2>();
-    unit<MT, 2, 2 % UPC>(R, F, X, acc);
-    piece<MT, 2>(prev, nh);
-    interleave<4 * MT, 2>();
-    unit<MT, 3, 3 % UPC>(R, F, X, acc);
-    piece<MT, 3>(prev, nh);
+    if constexpr (XCH) {
+      unit<MT, 0>(R, F, X, acc);
+      piece<MT, 0, 1>(prev, nh);
+      piece<MT, 1, 1>(prev, nh);
+      interleave<4 * MT, 2>();
+      publish<MT>(sm, prev);
+      unit<MT, 1>(R, F, X, acc);  // ring barrier: every wave's seam is published
+      // each unit's seam VALU (waiting on the seam reads) come after
+      // independent inner-tile work, so the reads' latency is covered
+      f4 L0, R0;
+      seam_read(sm, 0, L0, R0);
+      piece<MT, 2, 1>(prev, nh);
+      piece<MT, 0, 2>(prev, nh, L0, R0);
+      interleave<4 * MT, 2, 2>();
+      unit<MT, 2>(R, F, X, acc);
+      f4 L1, R1;
+      seam_read(sm, 1, L1, R1);
+      piece<MT, 3, 1>(prev, nh);
+      piece<MT, 1, 2>(prev, nh, L0, R0);
+      interleave<4 * MT, 2, 6>();
+      unit<MT, 3>(R, F, X, acc);
+      piece<MT, 2, 2>(prev, nh, L1, R1);
+      piece<MT, 3, 2>(prev, nh, L1, R1);
+      sm.par ^= 1;
+    } else {
+      unit<MT, 0>(R, F, X, acc);
+      piece<MT, 0>(prev, nh);
+      interleave<4 * MT, 2>();
+      unit<MT, 1>(R, F, X, acc);
+      piece<MT, 1>(prev, nh);
+      interleave<4 * MT, 2>();
+      unit<MT, 2>(R, F, X, acc);
+      piece<MT, 2>(prev, nh);
+      interleave<4 * MT, 2>();
+      unit<MT, 3>(R, F, X, acc);
+      piece<MT, 3>(prev, nh);
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<u4 *>(park_at(park, q - 1, mt, lane)) = nh[mt];
     interleave<4 * MT, 2>();
@@ -223,7 +370,7 @@ struct CoreBF16 {
   // first three units.
   template <int MT>
   static __device__ __forceinline__ void pair0_after(R_t &R, Feed &F, Acts<MT> &X, const float *bias, int g4,
-                                                     Pair<MT> &acc, Pair<MT> &pend, float *park, int lane) {
+                                                     Pair<MT> &acc, Pair<MT> &pend, float *park, int lane, Seam &sm) {
     wave_lds_sync();  // this wave's park writes of the previous layer have landed
 #pragma unroll
     for (int kb = 0; kb < 3; ++kb)
@@ -231,19 +378,41 @@ struct CoreBF16 {
       for (int mt = 0; mt < MT; ++mt) X.h[mt][kb] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, mt, lane)));
     init<MT>(bias, 0, g4, acc);
     u4 nh[MT];
-    unit<MT, 0, 0 % UPC>(R, F, X, acc);
-    piece<MT, 0>(pend, nh);
-    piece<MT, 1>(pend, nh);
-    interleave<4 * MT, 4>();
-    unit<MT, 1, 1 % UPC>(R, F, X, acc);
-    piece<MT, 2>(pend, nh);
-    interleave<4 * MT, 2>();
-    unit<MT, 2, 2 % UPC>(R, F, X, acc);
-    piece<MT, 3>(pend, nh);
-    interleave<4 * MT, 2>();
+    if constexpr (XCH) {
+      unit<MT, 0>(R, F, X, acc);
+      piece<MT, 0, 1>(pend, nh);
+      piece<MT, 1, 1>(pend, nh);
+      piece<MT, 2, 1>(pend, nh);
+      interleave<4 * MT, 3>();
+      publish<MT>(sm, pend);
+      unit<MT, 1>(R, F, X, acc);  // ring barrier
+      f4 L0, R0, L1, R1;
+      seam_read(sm, 0, L0, R0);
+      seam_read(sm, 1, L1, R1);
+      piece<MT, 3, 1>(pend, nh);
+      piece<MT, 0, 2>(pend, nh, L0, R0);
+      interleave<4 * MT, 2, 4>();
+      unit<MT, 2>(R, F, X, acc);
+      piece<MT, 1, 2>(pend, nh, L0, R0);
+      piece<MT, 2, 2>(pend, nh, L1, R1);
+      piece<MT, 3, 2>(pend, nh, L1, R1);
+      interleave<4 * MT, 4>();
+      sm.par ^= 1;
+    } else {
+      unit<MT, 0>(R, F, X, acc);
+      piece<MT, 0>(pend, nh);
+      piece<MT, 1>(pend, nh);
+      interleave<4 * MT, 4>();
+      unit<MT, 1>(R, F, X, acc);
+      piece<MT, 2>(pend, nh);
+      interleave<4 * MT, 2>();
+      unit<MT, 2>(R, F, X, acc);
+      piece<MT, 3>(pend, nh);
+      interleave<4 * MT, 2>();
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
-    unit<MT, 3, 3 % UPC>(R, F, X, acc);
+    unit<MT, 3>(R, F, X, acc);
     interleave<4 * MT, 0>();
   }
 
@@ -252,33 +421,30 @@ struct CoreBF16 {
   static __device__ __forceinline__ void pair0_first(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
                                                      Pair<MT> &acc) {
     init<MT>(bias, 0, g4, acc);
-    unit<MT, 0, 0 % UPC>(R, F, X, acc);
+    unit<MT, 0>(R, F, X, acc);
     interleave<4 * MT, 0>();
-    unit<MT, 1, 1 % UPC>(R, F, X, acc);
+    unit<MT, 1>(R, F, X, acc);
     interleave<4 * MT, 0>();
-    unit<MT, 2, 2 % UPC>(R, F, X, acc);
+    unit<MT, 2>(R, F, X, acc);
     interleave<4 * MT, 0>();
-    unit<MT, 3, 3 % UPC>(R, F, X, acc);
+    unit<MT, 3>(R, F, X, acc);
     interleave<4 * MT, 0>();
   }
 
   // Pairs 1..3 of a layer; leaves pair 3 in pend (its epilogue is pending).
   template <int MT>
   static __device__ __forceinline__ void pairs_rest(R_t &R, Feed &F, const Acts<MT> &X, const float *bias, int g4,
-                                                    Pair<MT> &acc0, Pair<MT> &pend, float *park, int lane) {
+                                                    Pair<MT> &acc0, Pair<MT> &pend, float *park, int lane, Seam &sm) {
     Pair<MT> acc1, acc2;
-    pair_with_prev<MT>(R, F, X, bias, 1, g4, acc1, acc0, park, lane);
-    pair_with_prev<MT>(R, F, X, bias, 2, g4, acc2, acc1, park, lane);
-    pair_with_prev<MT>(R, F, X, bias, 3, g4, pend, acc2, park, lane);
+    pair_with_prev<MT>(R, F, X, bias, 1, g4, acc1, acc0, park, lane, sm);
+    pair_with_prev<MT>(R, F, X, bias, 2, g4, acc2, acc1, park, lane, sm);
+    pair_with_prev<MT>(R, F, X, bias, 3, g4, pend, acc2, park, lane, sm);
   }
 
   // ------------------------------------------------------------- readout
-  // Readout unit U of output tile ot: fragment i = 2*(kb - 2U) + (P|Q), kb = 2U, 2U+1;
-  // T = its index in the ring chunk.
-  template <int MT, int U, int T>
-  static __device__ __forceinline__ void ro_unit(R_t &R, Feed &F, const Acts<MT> &X, f4 (&P)[MT], f4 (&Q)[MT]) {
-    u4 w[4];
-    take<T>(R, F, w);
+  // MFMAs of readout unit U of one output tile: fragment i = 2*(kb - 2U) + (P|Q), kb = 2U, 2U+1.
+  template <int MT, int U>
+  static __device__ __forceinline__ void ro_mfma(const u4 (&w)[4], const Acts<MT> &X, f4 (&P)[MT], f4 (&Q)[MT]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kb = 2 * U + (i >> 1);
@@ -288,6 +454,13 @@ struct CoreBF16 {
         else P[mt] = mma(w[i], X.h[mt][kb], P[mt]);
       }
     }
+  }
+  // ... at ring position T.
+  template <int MT, int U, int T>
+  static __device__ __forceinline__ void ro_unit(R_t &R, Feed &F, const Acts<MT> &X, f4 (&P)[MT], f4 (&Q)[MT]) {
+    u4 w[4];
+    take<T>(R, F, w);
+    ro_mfma<MT, U>(w, X, P, Q);
   }
 
   // Rows 2RP, 2RP+1 of one readout tile's epilogue: z_fwd(i) = P(i) + Q(i+1),
@@ -329,7 +502,7 @@ struct CoreBF16 {
     }
   }
 
-  // Readout tile ot >= 1 (ring indices T0, T0+1), with the epilogue of tile
+  // Readout tile ot >= 1 (ring positions T0, T0+1), with the epilogue of tile
   // ot-1 (P, Q on entry; tile ot's on exit) spread over its two units.
   template <int MT, int T0>
   static __device__ __forceinline__ void ro_tile(R_t &R, Feed &F, const Acts<MT> &X, const Small &S, int ot,
@@ -353,11 +526,13 @@ struct CoreBF16 {
 
   // Edge readout, P/Q split (src/flux_gnn.py:62-66), pipelined tile by tile.
   // The last layer's pair 3 (pend) is still to be activated: h of k-blocks
-  // 0..2 comes from the park, k-block 3 is finished under the first readout unit.
+  // 0..2 comes from the park, k-block 3 is finished under the first readout unit
+  // (XCH: its edge m-tiles after the second unit's ring barrier, before the
+  // MFMAs that read k-block 3).
   template <int MT>
   static __device__ __forceinline__ void readout(const ChainW &W, const Small &S, R_t &R, Feed &F, Acts<MT> &X,
                                                  Pair<MT> &pend, float *park, int lane, int g4, float (&ffwd)[MT],
-                                                 float (&fbwd)[MT]) {
+                                                 float (&fbwd)[MT], Seam &sm) {
     wave_lds_sync();
 #pragma unroll
     for (int kb = 0; kb < 3; ++kb)
@@ -370,22 +545,48 @@ struct CoreBF16 {
     init_ro<MT>(S, 0, g4, P, Q);
     {
       u4 nh[MT];
-      ro_unit<MT, 0, 0>(R, F, X, P, Q);
-      piece<MT, 0>(pend, nh);
-      piece<MT, 1>(pend, nh);
-      piece<MT, 2>(pend, nh);
-      piece<MT, 3>(pend, nh);
-      interleave<4 * MT, 4>();
+      if constexpr (XCH) {
+        ro_unit<MT, 0, pos(0)>(R, F, X, P, Q);
+        piece<MT, 0, 1>(pend, nh);
+        piece<MT, 1, 1>(pend, nh);
+        piece<MT, 2, 1>(pend, nh);
+        piece<MT, 3, 1>(pend, nh);
+        interleave<4 * MT, 4>();
+        publish<MT>(sm, pend);
+        u4 w[4];
+        take<pos(1)>(R, F, w);  // ring barrier
+        f4 L0, R0, L1, R1;
+        seam_read(sm, 0, L0, R0);
+        seam_read(sm, 1, L1, R1);
+        // (with no update layer pend's G is zero, published and traded as such)
+        piece<MT, 0, 2>(pend, nh, L0, R0);
+        piece<MT, 1, 2>(pend, nh, L0, R0);
+        piece<MT, 2, 2>(pend, nh, L1, R1);
+        piece<MT, 3, 2>(pend, nh, L1, R1);
+        sm.par ^= 1;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
-      ro_unit<MT, 1, 1>(R, F, X, P, Q);
-      interleave<4 * MT, 0>();
+        for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
+        ro_mfma<MT, 1>(w, X, P, Q);
+        interleave<4 * MT, 5>();
+      } else {
+        ro_unit<MT, 0, 0>(R, F, X, P, Q);
+        piece<MT, 0>(pend, nh);
+        piece<MT, 1>(pend, nh);
+        piece<MT, 2>(pend, nh);
+        piece<MT, 3>(pend, nh);
+        interleave<4 * MT, 4>();
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) X.h[mt][3] = nh[mt];
+        ro_unit<MT, 1, 1>(R, F, X, P, Q);
+        interleave<4 * MT, 0>();
+      }
     }
-    // tiles 1..7; an odd tile starts mid-chunk when a chunk holds two tiles
-    constexpr int kOdd = UPC == 4 ? 2 : 0;
+    // tiles 1..7 at ring positions T0, T0+1: readout unit u (of 16) is at pos(u)
+    constexpr int kOdd = XCH ? pos(2) : (UPC == 4 ? 2 : 0);
+    constexpr int kEven = XCH ? pos(0) : 0;
     for (int ot = 1; ot < kNT - 1; ot += 2) {
       ro_tile<MT, kOdd>(R, F, X, S, ot, g4, P, Q, pf, pb);
-      ro_tile<MT, 0>(R, F, X, S, ot + 1, g4, P, Q, pf, pb);
+      ro_tile<MT, kEven>(R, F, X, S, ot + 1, g4, P, Q, pf, pb);
     }
     ro_tile<MT, kOdd>(R, F, X, S, kNT - 1, g4, P, Q, pf, pb);
     {
@@ -432,8 +633,9 @@ struct CoreBF16 {
   }
 
   template <int MT>
-  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &F, float *park,
-                                             const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
+  static __device__ __forceinline__ void gnn_seam(const ChainW &W, const Small &S, R_t &R, Feed &F, float *park,
+                                                  Seam &sm, const float (&feat)[MT], float (&ffwd)[MT],
+                                                  float (&fbwd)[MT]) {
     const int lane = R.lane;
     const int g4 = 4 * (lane >> 4);
     Acts<MT> X;
@@ -461,25 +663,161 @@ struct CoreBF16 {
     if (W.layers > 0) {
       Pair<MT> acc0;
       pair0_first<MT>(R, F, X, S.bl, g4, acc0);
-      pairs_rest<MT>(R, F, X, S.bl, g4, acc0, pend, park, lane);
+      pairs_rest<MT>(R, F, X, S.bl, g4, acc0, pend, park, lane, sm);
     }
     for (int l = 1; l < W.layers; ++l) {
       const float *bias = S.bl + l * kH;
       Pair<MT> acc0;
-      pair0_after<MT>(R, F, X, bias, g4, acc0, pend, park, lane);
-      pairs_rest<MT>(R, F, X, bias, g4, acc0, pend, park, lane);
+      pair0_after<MT>(R, F, X, bias, g4, acc0, pend, park, lane, sm);
+      pairs_rest<MT>(R, F, X, bias, g4, acc0, pend, park, lane, sm);
     }
-    readout<MT>(W, S, R, F, X, pend, park, lane, g4, ffwd, fbwd);
+    readout<MT>(W, S, R, F, X, pend, park, lane, g4, ffwd, fbwd, sm);
+  }
+
+  // The chain_common.h kernels' entry (periodic windows, no seam trade).
+  template <int MT>
+  static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &F, float *park,
+                                             const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
+    static_assert(!XCH, "the super-window core runs in chain_flux_sw_kernel");
+    Seam sm{};
+    gnn_seam<MT>(W, S, R, F, park, sm, feat, ffwd, fbwd);
   }
 };
+
+// ---------------------------------------------------------------------------
+// FluxGNN.forward on B periodic chains of any nx by super-windows
+// (src/flux_gnn.py:40-67).  The B chains are laid end to end as one stream of
+// padded segments: IC b owns stream cells [bP, bP + P), P = nx + 2L + 1, and
+// segment cell p holds IC cell (p - L) mod nx, so face i (cells i, i+1) of
+// IC b sits at segment cells L+i, L+i+1 and its L-layer receptive field
+// [i - L, i + 1 + L] lies inside the segment.  A workgroup's NW waves take
+// 63*NW + 1 consecutive stream cells (64 per wave, overlapping by one) and
+// trade edge G values every layer (CoreBF16 XCH), so only the workgroup's own
+// two ends are wrong after L layers: its faces [L, 63*NW - L) are exact, and
+// consecutive super-windows start 63*NW - 2L cells apart.  Work per IC face:
+// 64*NW / (63*NW - 2L) * P / nx, 1.04 at cfg4 (L = 4, NW = 8, nx = 1024),
+// against 64/55 * 1216/1045 = 1.19 for independent 64-cell windows.
+template <class Core>
+__global__ __launch_bounds__(64 * Core::kNW, 1) void chain_flux_sw_kernel(ChainW W, const float *__restrict__ nf,
+                                                                   const float *__restrict__ state,
+                                                                   int64_t ld_state, const float *__restrict__ x,
+                                                                   int B, int nx, int nsw,
+                                                                   float *__restrict__ fe, float *__restrict__ ff) {
+  constexpr int MT = 4, NW = Core::kNW;
+  constexpr int kRingFloats = Core::kSlots * Core::kChunkFloats;
+  constexpr int kBaseF4 = lds_floats<Core, false>() / 4;
+  __shared__ f4 lds4[kBaseF4 + Core::kSeamF4];
+  float *lds = reinterpret_cast<float *>(lds4);
+  const Small S = stage_small(W, lds + kRingFloats);
+  auto R = make_ring<Core>(W, lds);
+  const int lane = R.lane, j = lane & 15, g = lane >> 4;
+  using Seam = typename Core::Seam;
+  Seam sm{lds4 + kBaseF4 + Seam::slot(R.wave, 0), lds4 + kBaseF4 + Seam::slot((R.wave + NW - 1) % NW, 1),
+          lds4 + kBaseF4 + Seam::slot((R.wave + 1) % NW, 0), 0};
+  __syncthreads();  // small weights staged (no DMA in flight yet)
+  R.prime(R.chunks - 1);  // the pass starts two units before chunk 0 (Core::pos)
+  typename Core::Feed F;
+  Core::begin(R, F);
+  const int L = W.layers;
+  const int P = nx + 2 * L + 1;
+  const int faces = 63 * NW - 2 * L;  // exact faces per super-window
+  const int total = B * P;            // < 2^31 (launch_flux_sw)
+  // Stream cell s0 + c (c < 64) of this wave as (IC b, segment cell p): the
+  // wave-uniform division once, then at most ceil(64 / P) subtractions per lane.
+  auto locate = [&](int s0, int c, int &b, int &p) {
+#ifdef HF_DIAG_NOLOC  // timing diagnostic only: results are wrong (IC = super-window, no index arithmetic)
+    b = (s0 < 0 ? 0 : s0) / 1024 % B;
+    p = c + L;
+    return;
+#endif
+    const int base = s0 < 0 ? 0 : (s0 >= total ? total - 1 : s0);
+    b = base / P;
+    int s = s0 + c;
+    s = s < 0 ? 0 : (s >= total ? total - 1 : s);  // outside the stream: any cell (its faces are discarded)
+    p = s - b * P;
+    while (p >= P) {
+      p -= P;
+      ++b;
+    }
+  };
+  auto first = [&](int k) { return k * faces - L + 63 * R.wave; };  // this wave's first stream cell
+  auto load_feat = [&](int k, float (&feat)[MT]) {
+    const int s0 = __builtin_amdgcn_readfirstlane(first(k));
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      int b, p;
+      locate(s0, cell_of<MT>(mt, j), b, p);
+      int c = p - L;  // IC cell (p - L) mod nx; p - L is in [-L, nx + L]
+      while (c < 0) c += nx;
+      while (c >= nx) c -= nx;
+#ifdef HF_DIAG_NOFEAT  // timing diagnostic only: results are wrong (no feature loads, no flux stores)
+      feat[mt] = 0.01f * (float)(c + g);
+#else
+      feat[mt] = nf ? nf[((int64_t)b * nx + c) * kIn + g]
+                    : (g < 3 ? state[b * ld_state + (int64_t)g * nx + c] : x[c]);
+#endif
+    }
+  };
+#ifdef HF_EXP_PREFETCH
+  float pre[MT];
+  if (blockIdx.x < nsw) load_feat(blockIdx.x, pre);
+#endif
+  for (int k = blockIdx.x; k < nsw; k += gridDim.x) {
+    float feat[MT];
+#ifdef HF_EXP_PREFETCH
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) feat[mt] = pre[mt];
+    if (k + (int)gridDim.x < nsw) load_feat(k + gridDim.x, pre);  // in flight under this forward
+#else
+    load_feat(k, feat);
+#endif
+    float f_fwd[MT], f_bwd[MT];
+    Core::template gnn_seam<MT>(W, S, R, F, park_of<Core, false>(lds, R.wave), sm, feat, f_fwd, f_bwd);
+    const int s0 = __builtin_amdgcn_readfirstlane(first(k));
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int c = cell_of<MT>(mt, j), csw = 63 * R.wave + c;
+      // the wave's last cell is the next wave's first: its face is the next wave's
+      if (c == 63 || csw < L || csw >= L + faces || s0 + c >= total) continue;
+      int b, p;
+      locate(s0, c, b, p);
+      const int i = p - L;  // face i of IC b: cells i, i+1 at segment cells p, p+1
+      if (i < 0 || i >= nx) continue;
+#ifdef HF_DIAG_NOFEAT
+      if (f_fwd[mt] != 12345.f) continue;  // keeps the forward live; never false in practice
+#endif
+      if (fe && g == 0) fe[(int64_t)b * 2 * nx + i] = f_fwd[mt];
+      if (fe && g == 1) fe[(int64_t)b * 2 * nx + nx + i] = f_bwd[mt];
+      if (ff && g == 2) ff[(int64_t)b * nx + i] = face_flux(f_fwd[mt], f_bwd[mt]);
+    }
+  }
+  R.drain();
+}
+
+template <class Core>
+hipError_t launch_flux_sw(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
+                          int B, int nx, float *fe, float *ff, hipStream_t s) {
+  const int64_t total = (int64_t)B * (nx + 2 * w.layers + 1);
+  if (total >= (int64_t(1) << 31) - 64 * Core::kNW) return hipErrorInvalidValue;  // 32-bit stream index
+  const int faces = 63 * Core::kNW - 2 * w.layers;
+  const int nsw = (int)((total + faces - 1) / faces);
+  const int64_t res = resident_groups();
+  const int64_t blocks = nsw < res ? nsw : res;  // persistent: one per CU
+  hipLaunchKernelGGL((chain_flux_sw_kernel<Core>), dim3((unsigned)blocks), dim3(64 * Core::kNW), 0, s, w, nf, state,
+                     ld_state, x, B, nx, nsw, fe, ff);
+  return hipGetLastError();
+}
 
 }  // namespace
 
 hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                   const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
-  // exact kernels (nx = 16..64) and windows of 64 cells (any other nx, e.g.
-  // cfg4's 1024): 8 waves, two per SIMD, 16 KiB chunks in 3 slots
-  return chain::launch_flux_core<CoreBF16<8, 4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  // exact kernels (nx = 16..64, one wave per chain) and super-windows (any
+  // other nx, e.g. cfg4's 1024): 8 waves, two per SIMD, 16 KiB chunks in 3 slots
+  if (B <= 0) return hipSuccess;
+  if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
+    return chain::launch_flux_core<CoreBF16<8, 4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  return launch_flux_sw<CoreBF16<8, 4, 4, false, 3, 1, 0, true>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float *state_final, const float *x,

@@ -227,13 +227,13 @@ struct Ring {
           : "memory");
     }
   }
-  // Start the stream at chunk 0 (positions 0 .. D-1 in flight).
-  __device__ __forceinline__ void prime() {
+  // Start the stream at chunk `first` (chunks first .. first+D-1 in flight).
+  __device__ __forceinline__ void prime(int first = 0) {
     pos = 0;
     rd = 0;
 #pragma unroll
-    for (int i = 0; i < D; ++i) issue(i % chunks, i);
-    ahead = D % chunks;
+    for (int i = 0; i < D; ++i) issue((first + i) % chunks, i);
+    ahead = (first + D) % chunks;
   }
   // Wait for chunk `pos`, keep D chunks in flight, return its slot.
   __device__ __forceinline__ const float *next() {
@@ -293,8 +293,9 @@ __device__ __forceinline__ typename Core::R_t make_ring(const ChainW &W, float *
   typename Core::R_t R;
   // the packed stream is chain_chunks() chunks of chain_chunk_bytes(); a core may move it in larger chunks
   R.chunks = chain_chunks(W.layers, W.prec) * chain_chunk_bytes(W.prec) / (Core::kChunkFloats * 4);
-  R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0,
-                                             R.chunks * Core::kChunkFloats * 4, 0x00020000);
+  R.rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char *>(static_cast<const char *>(W.stream)) + Core::kStreamOffset, 0,
+      R.chunks * Core::kChunkFloats * 4, 0x00020000);
   R.lane_off = (threadIdx.x & 63) * 16;
   R.lds = ring_lds;
   R.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -29,6 +29,7 @@ template <int D = 2, int SLOTS = kRingSlots>
 struct CoreF32T {
   static constexpr int kNW = kWaves;   // waves sharing the weight ring
   static constexpr int kWGPerCU = 1;   // persistent flux kernel: workgroups per CU
+  static constexpr int kStreamOffset = 0;  // bytes of the packed stream before chunk 0
   static constexpr int kSlots = SLOTS;
   static constexpr int kAhead = D;
   static constexpr int kWinMT = 4;     // m-tiles per wave in the windowed flux kernel

@@ -84,6 +84,7 @@ template <int UPC>
 struct CoreF16x3T {
   static constexpr int kNW = kWaves;
   static constexpr int kWGPerCU = 1;
+  static constexpr int kStreamOffset = 0;
   static constexpr int kUPC = UPC;
   static constexpr int kSlots = UPC == 2 ? 3 : 4;
   static constexpr int kAhead = 2;

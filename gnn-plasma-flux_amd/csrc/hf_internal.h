@@ -50,6 +50,8 @@ __host__ __device__ inline int chain_chunks(int layers, int prec) {
   return prec == kPrecF32 ? 16 * layers + 2 * kNT : 8 * layers + kNT;
 }
 __host__ __device__ inline int chain_chunk_bytes(int prec) { return prec == kPrecF16x3 ? 16384 : 8192; }
+// bf16 streams end with a copy of their first kBF16StreamTail bytes (two 4 KiB units)
+constexpr int kBF16StreamTail = 8192;
 
 struct ChainW {
   const void *stream;   // [chain_chunks][chunk]
