@@ -150,7 +150,7 @@ struct CoreBF16 {
   };
   template <int MT>
   static __device__ __forceinline__ void publish(const Seam &sm, const Pair<MT> &P) {
-#ifdef HF_DIAG_NOSEAM  // timing diagnostic only: results are wrong (no seam trade)
+#if defined(HF_DIAG_NOSEAM) || defined(HF_DIAG_NOPUB)  // timing diagnostic only: results are wrong (no seam trade)
     return;
 #endif
     if constexpr (XCH) {
@@ -169,7 +169,7 @@ struct CoreBF16 {
   // After the ring barrier that follows publish(): the neighbours' seam G of
   // tile t (lanes j = 0 use L, lanes j = 15 use R).
   static __device__ __forceinline__ void seam_read(const Seam &sm, int t, f4 &L, f4 &R) {
-#ifdef HF_DIAG_NOSEAM
+#if defined(HF_DIAG_NOSEAM) || defined(HF_DIAG_NORD)
     L = R = f4{0.f, 0.f, 0.f, 0.f};
     return;
 #endif
