@@ -415,7 +415,11 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
     CellCore::gnn_cells(W, S, R, F, feat, ff, fb, X);
     if (!shadow && g == 0) s_F[16 * pos + j] = face_flux(ff[0], fb[0]);
     lds_barrier();  // every wave's face fluxes in s_F
+#ifdef HF_DIAG_NOFV  // timing diagnostic only: results are wrong (no FV, Poisson or outputs per step)
+    if (false) {
+#else
     if (lead) {     // src/hybrid_solver.py:45-63, one cell per lane
+#endif
       float n_new = 0.f, u_new = 0.f;
       if (lane < NX) {
         const int im = lane == 0 ? NX - 1 : lane - 1;
