@@ -210,8 +210,6 @@ hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 bool fused_nx(int nx) { return nx == 16 || nx == 32 || nx == 48 || nx == 64; }
 
-constexpr int kMaxFvNx = 6144;  // LDS bound of fv_poisson.hip (20 B per cell)
-
 int check_device() {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
@@ -563,7 +561,6 @@ int hf_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, i
   if (B < 0 || nx < 1 || ld_n < nx || ld_E < nx) return fail(HF_EINVAL, "hf_poisson: bad shape");
   if (B == 0) return HF_OK;
   if (!n || !E || !pc) return fail(HF_EINVAL, "hf_poisson: NULL pointer");
-  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_poisson: nx too large for the LDS solve");
   HF_CHECK_HIP(hf::launch_poisson(n, ld_n, E, ld_E, pc, B, nx, as_stream(stream)), "hf_poisson");
   return HF_OK;
 }
@@ -623,7 +620,6 @@ int hf_step(hf_model_t m, const float *in, float *out, const float *x, const dou
   if (B == 0) return HF_OK;
   if (!in || !out || !pc) return fail(HF_EINVAL, "hf_step: NULL state or Poisson coefficients");
   if (in == out) return fail(HF_EINVAL, "hf_step: state_in and state_out must not alias");
-  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_step: nx > 6144 (LDS bound of the FV/Poisson kernel)");
   hipStream_t s = as_stream(stream);
   if (!m) {  // BaselineSolver.step
     HF_CHECK_HIP(hf::launch_fv_step(in, 3LL * nx, out, 3LL * nx, nullptr, pc, B, nx, c, dt, nu, dx2, ff,
@@ -657,7 +653,6 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run: need B >= 0, nx >= 1, T >= 0");
   if (B == 0) return HF_OK;
   if (!state0 || !state_final || !pc) return fail(HF_EINVAL, "hf_run: NULL state or Poisson coefficients");
-  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run: nx > 6144 (LDS bound of the FV/Poisson kernel)");
   if (m && !x) return fail(HF_EINVAL, "hf_run: NULL x");
   if (m) {
     if (int rc = chain_usable(m)) return rc;
@@ -729,7 +724,6 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
   if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run_compare: need B >= 0, nx >= 1, T >= 0");
   if (B == 0) return HF_OK;
   if (!state0 || !state_final || !pc || !x || !mse) return fail(HF_EINVAL, "hf_run_compare: NULL pointer");
-  if (nx > kMaxFvNx) return fail(HF_EUNSUPPORTED, "hf_run_compare: nx > 6144 (LDS bound of the FV/Poisson kernel)");
   if (int rc = chain_usable(m)) return rc;
   hipStream_t s = as_stream(stream);
   if (fused_nx(nx)) {

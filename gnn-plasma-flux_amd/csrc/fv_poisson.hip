@@ -98,6 +98,73 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
   if (metrics) block_metrics(m, metrics + b * ld_metrics, nx);
 }
 
+// ------------------------------------------------------------ large nx
+// nx > kFvLdsMaxNx (the chain no longer fits the LDS plan above): the update
+// and the Poisson solve run as separate launches over global memory, a
+// 256-cell block per workgroup (grid: cell blocks x ICs).  The Poisson sum
+// walks j in the order poisson_cell does, the even terms into a0 and the odd
+// ones into a1, with rho and the window of c a tile needs staged in LDS, so
+// E is the LDS kernels' value bit for bit; the metrics come from
+// state_metrics_kernel, which sums in fv_step_kernel's order.
+constexpr int kFvLdsMaxNx = 6144;  // fv_lds_bytes(6144) = 144 KiB of dynamic LDS
+constexpr int kPoissonTileJ = 1024;
+
+template <bool HYBRID>
+__global__ __launch_bounds__(kFvThreads) void fv_update_kernel(const float *__restrict__ in, int64_t ld_in,
+                                                               float *__restrict__ out, int64_t ld_out,
+                                                               const float *__restrict__ face_flux, int nx, float c,
+                                                               float dt, float nu, float dx2,
+                                                               float *__restrict__ flux_out, int64_t ld_flux) {
+  const int64_t b = blockIdx.y;
+  const int i = blockIdx.x * kFvThreads + threadIdx.x;
+  if (i >= nx) return;
+  const float *st = in + b * ld_in;
+  float *so = out + b * ld_out;
+  const int im = i == 0 ? nx - 1 : i - 1;
+  const int ip = i == nx - 1 ? 0 : i + 1;
+  const float u = st[nx + i], um = st[nx + im];
+  const float F = HYBRID ? face_flux[b * nx + i] : __fmul_rn(st[i], u);  // F_n = n*u (:70-71)
+  const float Fm = HYBRID ? face_flux[b * nx + im] : __fmul_rn(st[im], um);
+  const float E = st[2 * nx + i];
+  so[i] = continuity(st[i], F, Fm, c);
+  so[nx + i] = HYBRID ? velocity_hybrid(u, um, E, c, dt)
+                      : velocity_classical(u, um, st[nx + ip], E, c, dt, nu, dx2);
+  if (flux_out) flux_out[b * ld_flux + i] = F;
+}
+
+// E[i] = f32(sum_j c[(i-j) mod nx] (n_j - 1)) for the block's 256 cells.
+__global__ __launch_bounds__(kFvThreads) void poisson_tiled_kernel(const float *__restrict__ n, int64_t ld_n,
+                                                                   float *__restrict__ E, int64_t ld_E,
+                                                                   const double *__restrict__ pc, int nx) {
+  __shared__ float s_rho[kPoissonTileJ];
+  __shared__ double s_c[kPoissonTileJ + kFvThreads];
+  const int64_t b = blockIdx.y;
+  const int i0 = blockIdx.x * kFvThreads, i = i0 + threadIdx.x;
+  double a0 = 0.0, a1 = 0.0;
+  for (int j0 = 0; j0 < nx; j0 += kPoissonTileJ) {
+    const int T = nx - j0 < kPoissonTileJ ? nx - j0 : kPoissonTileJ;
+    __syncthreads();  // the previous tile is consumed
+    for (int k = threadIdx.x; k < T; k += kFvThreads) s_rho[k] = __fsub_rn(n[b * ld_n + j0 + k], 1.0f);
+    // s_c[m] = c[(i0 - j0 - (T-1) + m) mod nx]: term (i, j0 + k) reads m = (i - i0) + T-1 - k
+    const int base = i0 - j0 - (T - 1);
+    for (int m = threadIdx.x; m < T + kFvThreads - 1; m += kFvThreads) {
+      int d = (base + m) % nx;
+      s_c[m] = pc[d < 0 ? d + nx : d];
+    }
+    __syncthreads();
+    if (i < nx) {
+      const double *cc = s_c + threadIdx.x + T - 1;  // cc[-k] = c[(i - j0 - k) mod nx]
+      int k = 0;
+      for (; k + 1 < T; k += 2) {  // j0 is even: k's parity is j's
+        a0 = fma(cc[-k], (double)s_rho[k], a0);
+        a1 = fma(cc[-k - 1], (double)s_rho[k + 1], a1);
+      }
+      if (k < T) a0 = fma(cc[-k], (double)s_rho[k], a0);  // odd nx: the last j is even
+    }
+  }
+  if (i < nx) E[b * ld_E + i] = (float)(a0 + a1);
+}
+
 // ------------------------------------------------------------ FFT sizes
 // One WAVE per pair of ICs (4 waves per workgroup, no workgroup barrier):
 // lane l owns cells l + 64v (v < N/64) of both ICs.  It reads n, u, E (and F
@@ -338,6 +405,20 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
       default: return hipErrorInvalidValue;
     }
   }
+  if (nx > kFvLdsMaxNx) {  // large nx: update, Poisson, metrics as three launches
+    const dim3 grid((unsigned)((nx + kFvThreads - 1) / kFvThreads), (unsigned)B);
+    if (face_flux)
+      hipLaunchKernelGGL(fv_update_kernel<true>, grid, dim3(kFvThreads), 0, s, in, ld_in, out, ld_out, face_flux, nx,
+                         c, dt, nu, dx2, flux_out, ld_flux);
+    else
+      hipLaunchKernelGGL(fv_update_kernel<false>, grid, dim3(kFvThreads), 0, s, in, ld_in, out, ld_out, face_flux,
+                         nx, c, dt, nu, dx2, flux_out, ld_flux);
+    hipLaunchKernelGGL(poisson_tiled_kernel, grid, dim3(kFvThreads), 0, s, out, ld_out, out + 2 * (int64_t)nx, ld_out,
+                       pc, nx);
+    if (metrics)
+      hipLaunchKernelGGL(state_metrics_kernel, dim3(B), dim3(kFvThreads), 0, s, out, ld_out, nx, metrics, ld_metrics);
+    return hipGetLastError();
+  }
   const size_t lds = fv_lds_bytes(nx);
   if (face_flux)
     hipLaunchKernelGGL(fv_step_kernel<true>, dim3(B), dim3(kFvThreads), lds, s, in, ld_in, out,
@@ -374,6 +455,11 @@ hipError_t launch_poisson(const float *n, int ld_n, float *E, int ld_E, const do
     case 1024: return poisson_fft_launch<1024>(n, ld_n, E, ld_E, pc, B, s);
     case 2048: return poisson_fft_launch<2048>(n, ld_n, E, ld_E, pc, B, s);
     default: break;
+  }
+  if (nx > kFvLdsMaxNx) {
+    hipLaunchKernelGGL(poisson_tiled_kernel, dim3((unsigned)((nx + kFvThreads - 1) / kFvThreads), (unsigned)B),
+                       dim3(kFvThreads), 0, s, n, (int64_t)ld_n, E, (int64_t)ld_E, pc, nx);
+    return hipGetLastError();
   }
   const size_t lds = fv_lds_bytes(nx);
   hipLaunchKernelGGL(poisson_kernel, dim3(B), dim3(kFvThreads), lds, s, n, ld_n, E, ld_E, pc, nx);

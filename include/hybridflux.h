@@ -236,7 +236,8 @@ int64_t hf_run_workspace_bytes(int op, int B, int nx, int T);
  * dev_x [nx]: float32 cell centres (node feature x); dev_c: Poisson coeffs.
  * dev_flux_face [B][nx] (may be NULL): the F used this step (F_n classically).
  * dev_metrics [B][HF_NUM_METRICS] (may be NULL) for state_out.
- * nx <= 6144 (LDS bound of the FV/Poisson kernel; larger nx -> HF_EUNSUPPORTED).
+ * Any nx >= 1: nx <= 6144 keeps the chain in LDS; larger nx (not an FFT size)
+ * runs the update and a tiled Poisson sum over global memory, same values.
  */
 int hf_step(hf_model_t model, const float *dev_state_in, float *dev_state_out,
             const float *dev_x, const double *dev_c, int B, int nx,

@@ -283,15 +283,30 @@ def test_aliased_state_buffers(hf, nx):
     assert torch.equal(buf, want["final"])
 
 
-def test_large_nx_is_a_clean_error(hf):
-    """nx > 6144 exceeds the FV/Poisson kernel's LDS plan: a HF_EUNSUPPORTED error,
-    never a launch (the BASELINE configs stop at nx = 1024)."""
-    from hybridflux._lib import HF_EUNSUPPORTED, HybridFluxError
-    solver = hf.BaselineSolver(nx=6160, dt=1e-5, device=DEV)
-    st = torch.ones(2, 3, 6160, device=DEV)
-    with pytest.raises(HybridFluxError) as e:
-        solver.step_batch(st)
-    assert e.value.code == HF_EUNSUPPORTED
+@pytest.mark.parametrize("nx", [6160, 8192])
+def test_large_nx_vs_oracle(hf, nx):
+    """Past the in-LDS kernels' 6144 cells the FV update and the Poisson sum run
+    over global memory (fv_update_kernel, poisson_tiled_kernel): the classical
+    step is the reference's float32 update bit for bit in n and u, E is within
+    the Poisson tolerance, and a hybrid rollout (windowed flux kernel at this nx)
+    follows the oracle (the reference works at any nx)."""
+    G = O.Grid(nx, dt=1e-4)
+    ics = np.stack([O.initial_condition(G, s) for s in (3000, 3001)])
+    s = hf.BaselineSolver(nx, dt=G.dt, device=DEV)
+    out, F, met = s.step_batch(ics, return_flux=True, metrics=True)
+    want, Fn = O.classical_step(G, ics)
+    out = out.cpu().numpy()
+    assert np.array_equal(out[:, :2], want[:, :2])
+    assert np.array_equal(F.cpu().numpy(), Fn)
+    close(out[:, 2], want[:, 2], E_ATOL)
+    E = s.solve_poisson(torch.as_tensor(ics[:, 0], device=DEV)).cpu().numpy()
+    close(E, O.solve_poisson(G, ics[:, 0]), E_ATOL)
+    assert np.isfinite(met.cpu().numpy()).all()
+    w = weights("W1_r1")
+    hs = hf.HybridSolver(w, radius=1, nx=nx, dt=G.dt, device=DEV)
+    got = hs.run_batch(ics, 3)["traj"].cpu().numpy()
+    ref, _ = O.hybrid_run(O.params_from(w), G, ics, 3)
+    close(got, ref, ROLL_ATOL, ROLL_RTOL)
 
 
 def test_zero_steps(hf):
