@@ -808,6 +808,117 @@ hipError_t launch_flux_sw(const ChainW &w, const float *nf, const float *state, 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Cell-split bf16 core for small batches (chain_common.h
+// chain_rollout_cells_kernel / chain_flux_cells_kernel): 16 cells per wave
+// (MT = 1), an IC of nx = 16*WPI cells over WPI waves.  The arithmetic is
+// CoreBF16's MFMA chain for chain and add for add (A = b + W_a h and
+// G = (W_b/2) h accumulated k-block by k-block, z = A + (G(i-1) + G(i+1)), the
+// readout dot summed over tiles 0..7 in order), so a batch gets the
+// IC-per-wave rollout's bits whichever kernel its size selects.  Not
+// pipelined: a layer's four output pairs, then the G values of the wave's
+// edge columns (j = 0, 15) of all 8 tiles traded through LDS around one
+// barrier (CellHalo::exchange), then the epilogue; the readout trades column 0
+// of P and Q the same way (CellHalo::xq).  It shares the weight ring of the
+// bf16 rollout kernel (8 KiB chunks, 4 slots, fragments read a unit ahead).
+struct CellBF16 {
+  using Base = CoreBF16<4, 2, 4, true, 4, 1, -1>;
+  static constexpr int kNW = Base::kNW;
+  static constexpr int kSlots = Base::kSlots;
+  static constexpr int kChunkFloats = Base::kChunkFloats;
+  static constexpr int kStreamOffset = 0;
+  using R_t = Base::R_t;
+  using Feed = Base::Feed;
+  using Acts = Base::Acts<1>;
+  using Pair = Base::Pair<1>;
+  static __device__ __forceinline__ void begin(R_t &R, Feed &F) { Base::begin(R, F); }
+
+  static __device__ __forceinline__ void gnn_cells(const ChainW &W, const Small &S, R_t &R, Feed &F,
+                                                   const float (&feat)[1], float (&ffwd)[1], float (&fbwd)[1],
+                                                   CellHalo &X) {
+    const int lane = R.lane, g4 = 4 * (lane >> 4);
+    Acts A;
+    {
+      f4 h67[1][2];
+      Base::input<1>(S, lane, feat, A, h67);
+    }
+    // message passing (src/flux_gnn.py:53-60)
+    for (int l = 0; l < W.layers; ++l) {
+      const float *bias = S.bl + l * kH;
+      Pair acc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        Base::init<1>(bias, q, g4, acc[q]);
+        Base::unit<1, 0>(R, F, A, acc[q]);
+        interleave<4, 0>();
+        Base::unit<1, 1>(R, F, A, acc[q]);
+        interleave<4, 0>();
+        Base::unit<1, 2>(R, F, A, acc[q]);
+        interleave<4, 0>();
+        Base::unit<1, 3>(R, F, A, acc[q]);
+        interleave<4, 0>();
+      }
+      {
+        f4 G[1][kNT];
+#pragma unroll
+        for (int t = 0; t < kNT; ++t) G[0][t] = acc[t >> 1].g[0][t & 1];
+        X.exchange(G);  // X.l / X.r: G of cell 16*pos - 1 / 16*pos + 16
+      }
+      // z = A + (G(i-1) + G(i+1)), ReLU, bf16 pairs: dword K of k-block q is
+      // tile 2q + (K >> 1), rows 2(K & 1), 2(K & 1) + 1 (CoreBF16::piece)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int K = 0; K < 4; ++K) {
+          const int tt = K >> 1, t = 2 * q + tt, r0 = 2 * (K & 1);
+          float z[2];
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr) {
+            const int r = r0 + rr;
+            const float v = acc[q].g[0][tt][r];
+            const float gl = dpp_over<kRowShr1>(X.l[t][r], v), gr = dpp_over<kRowShl1>(X.r[t][r], v);
+            z[rr] = __fadd_rn(acc[q].a[0][tt][r], __fadd_rn(gl, gr));
+          }
+          A.h[0][q][K] = pk_bf16(relu(z[0]), relu(z[1]));
+        }
+    }
+    // edge readout, P/Q split (src/flux_gnn.py:62-66): all 8 tiles, then column
+    // 0 of P and Q through LDS (P(i+1), Q(i+1) of lane j = 15 live on the right
+    // wave), then the epilogue rows in CoreBF16::readout's order
+    const int j = lane & 15, g = lane >> 4;
+    f4 P[kNT][1], Q[kNT][1];
+#pragma unroll
+    for (int ot = 0; ot < kNT; ++ot) {
+      Base::init_ro<1>(S, ot, g4, P[ot], Q[ot]);
+      Base::ro_unit<1, 0, 0>(R, F, A, P[ot], Q[ot]);
+      interleave<4, 0>();
+      Base::ro_unit<1, 1, 1>(R, F, A, P[ot], Q[ot]);
+      interleave<4, 0>();
+      if (j == 0) {
+        X.xq[((X.wave * kNT + ot) * 2 + 0) * 4 + g] = P[ot][0];
+        X.xq[((X.wave * kNT + ot) * 2 + 1) * 4 + g] = Q[ot][0];
+      }
+    }
+    lds_barrier();
+    float pf = 0.f, pb = 0.f;
+#pragma unroll
+    for (int ot = 0; ot < kNT; ++ot) {
+      const f4 prh = X.xq[((X.rw * kNT + ot) * 2 + 0) * 4 + g];
+      const f4 qrh = X.xq[((X.rw * kNT + ot) * 2 + 1) * 4 + g];
+      const f4 w2 = ldf4(S.w2 + 16 * ot + g4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pv = P[ot][0][r], qv = Q[ot][0][r];
+        const float pr = dpp_over<kRowShl1>(prh[r], pv), qr = dpp_over<kRowShl1>(qrh[r], qv);
+        pf = fmaf(w2[r], relu(__fadd_rn(pv, qr)), pf);
+        pb = fmaf(w2[r], relu(__fadd_rn(pr, qv)), pb);
+      }
+    }
+    float pf1[1] = {pf}, pb1[1] = {pb};
+    readout_finish<1>(pf1, pb1, W.b2, ffwd, fbwd);
+  }
+};
+
 }  // namespace
 
 hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
@@ -815,6 +926,14 @@ hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float 
   // exact kernels (nx = 16..64, one wave per chain) and super-windows (any
   // other nx, e.g. cfg4's 1024): 8 waves, two per SIMD, 16 KiB chunks in 3 slots
   if (B <= 0) return hipSuccess;
+  if (chain_rollout_prefers_cells(w, B, nx)) {  // small batches: each chain over nx/16 waves
+    switch (nx) {
+      case 32: return chain::flux_cells_launch<CellBF16, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 48: return chain::flux_cells_launch<CellBF16, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 64: return chain::flux_cells_launch<CellBF16, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
+      default: break;
+    }
+  }
   if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
     return chain::launch_flux_core<CoreBF16<8, 4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
   return launch_flux_sw<CoreBF16<8, 4, 4, false, 3, 1, 0, true>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
@@ -823,6 +942,15 @@ hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float 
 hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float *state_final, const float *x,
                                      const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                      float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
+  // small batches: each IC over nx/16 waves (cell-split kernel, same bits)
+  if (ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx)) {
+    switch (nx) {
+      case 32: return chain::cells_launch<CellBF16, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 48: return chain::cells_launch<CellBF16, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 64: return chain::cells_launch<CellBF16, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      default: break;
+    }
+  }
   return chain::launch_rollout_core<CoreBF16<4, 2, 4, true, 4, 1, -1>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
                                                              flux_traj, metrics, ex, s);
 }

@@ -326,197 +326,19 @@ struct CoreF32T {
 using CoreF32 = CoreF32T<>;
 
 // ---------------------------------------------------------------------------
-// Cell-split persistent rollout for small batches: an IC of NX = 16*WPI cells
-// on WPI waves (16 consecutive cells each, CoreF32 at MT = 1), 4/WPI ICs per
-// workgroup (WPI = 3: one IC and a shadow wave that keeps the weight ring's
-// lockstep and writes nothing).  B ICs occupy B*WPI/4 CUs' worth of waves
-// instead of B/4, for the same per-cell arithmetic as chain_rollout_kernel:
-// every MFMA chain, neighbour sum, readout partial dot and FV/Poisson
-// expression is evaluated in the same order, so the results are bit-identical
-// to it.  The four waves share the LDS weight ring as in chain_rollout_kernel;
-// per layer they swap boundary columns of h (CellHalo), per step column 0 of
-// the readout accumulators.  The IC's first wave does FV + Poisson + outputs
-// for all its cells, one per lane (src/hybrid_solver.py:45-63).
+// Cell-split small-batch kernels (chain_common.h) on the f32 core at MT = 1.
 #ifndef HF_CELLS_AHEAD
 #define HF_CELLS_AHEAD 4
 #endif
 constexpr int kCellsAhead = HF_CELLS_AHEAD;
 using CellCore = CoreF32T<kCellsAhead, kCellsAhead + 1>;
-constexpr int kXhF4 = 2 * kWaves * 2 * 4 * kNT;  // CellHalo::xh
-constexpr int kXqF4 = kWaves * kNT * 2 * 4;      // CellHalo::xq
-constexpr int kCellsLds =
-    CellCore::kSlots * CellCore::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats + 4 * (kXhF4 + kXqF4);
-
-template <int WPI>
-__global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
-    ChainW W, const float *state0, float *state_final,  // may alias (read whole before written)
-    const float *__restrict__ x,
-    const double *__restrict__ pc, int B, int T, float c, float dt, float *__restrict__ traj,
-    float *__restrict__ flux_traj, float *__restrict__ metrics) {
-  constexpr int NX = 16 * WPI;
-  constexpr int IPW = kWaves / WPI;  // ICs per workgroup
-  constexpr int kRingFloats = CellCore::kSlots * CellCore::kChunkFloats;
-  __shared__ f4 lds4[kCellsLds / 4];
-  float *lds = reinterpret_cast<float *>(lds4);
-  const Small S = stage_small(W, lds + kRingFloats);
-  auto R = make_ring<CellCore>(W, lds);
-  const int wave = R.wave, lane = R.lane, j = lane & 15, g = lane >> 4;
-  const bool shadow = wave >= IPW * WPI;
-  const int slot = shadow ? 0 : wave / WPI;  // IC of this wave within the workgroup
-  const int pos = shadow ? 0 : wave % WPI;   // cells 16*pos .. 16*pos + 15 of it
-  const bool lead = !shadow && pos == 0;
-  CellHalo X;
-  X.xh = reinterpret_cast<f4 *>(lds + kRingFloats + kSmallFloats + kWaves * kWaveScratchFloats);
-  X.xq = X.xh + kXhF4;
-  X.wave = wave;
-  X.lane = lane;
-  X.par = 0;
-  X.lw = shadow ? wave : slot * WPI + (pos + WPI - 1) % WPI;  // periodic chain
-  X.rw = shadow ? wave : slot * WPI + (pos + 1) % WPI;
-  float *scratch = lds + kRingFloats + kSmallFloats + slot * kWaveScratchFloats;
-  float *s_st = scratch;  // n | u | E | x   (4 x 64)
-  float *s_F = scratch + 4 * 64;
-  float *s_rho = scratch + 5 * 64;
-  double *s_c = reinterpret_cast<double *>(scratch + 6 * 64);
-  const int b_raw = blockIdx.x * IPW + slot;
-  const bool live = b_raw < B;
-  const int64_t b = live ? b_raw : B - 1;  // a missing IC mirrors the last one and writes nothing
-  if (lead) {
-    const float *st0 = state0 + b * 3 * NX;
-    for (int i = lane; i < 3 * NX; i += 64) s_st[(i / NX) * 64 + i % NX] = st0[i];
-    if (lane < NX) {
-      s_st[3 * 64 + lane] = x[lane];
-      s_c[lane] = pc[lane];
-    }
-  }
-  __syncthreads();  // small weights + IC state visible (no DMA in flight yet)
-  const bool out = lead && live;
-  float *tj = (traj && out) ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
-  float *mt_out = (metrics && out) ? metrics + b * (int64_t)(T + 1) * HF_NUM_METRICS : nullptr;
-  float *ftj = (flux_traj && out) ? flux_traj + b * (int64_t)T * NX : nullptr;
-  auto emit = [&](int t) {  // lead wave
-    if (tj)
-      for (int i = lane; i < 3 * NX; i += 64) tj[(int64_t)t * 3 * NX + i] = s_st[(i / NX) * 64 + i % NX];
-    if (mt_out) {
-      MetricAcc m;
-      m.init();
-      if (lane < NX) m.add(s_st[lane], s_st[64 + lane], s_st[128 + lane]);
-      m.wave_reduce();
-      if (lane == 0) m.store(mt_out + t * HF_NUM_METRICS, NX);
-    }
-  };
-  if (lead) emit(0);
-  R.prime();
-  CellCore::Feed F;
-  CellCore::begin(R, F);
-  for (int t = 0; t < T; ++t) {
-    const float feat[1] = {s_st[g * 64 + 16 * pos + j]};
-    float ff[1], fb[1];
-    CellCore::gnn_cells(W, S, R, F, feat, ff, fb, X);
-    if (!shadow && g == 0) s_F[16 * pos + j] = face_flux(ff[0], fb[0]);
-    lds_barrier();  // every wave's face fluxes in s_F
-#ifdef HF_DIAG_NOFV  // timing diagnostic only: results are wrong (no FV, Poisson or outputs per step)
-    if (false) {
-#else
-    if (lead) {     // src/hybrid_solver.py:45-63, one cell per lane
-#endif
-      float n_new = 0.f, u_new = 0.f;
-      if (lane < NX) {
-        const int im = lane == 0 ? NX - 1 : lane - 1;
-        const float Fv = s_F[lane];
-        n_new = continuity(s_st[lane], Fv, s_F[im], c);
-        u_new = velocity_hybrid(s_st[64 + lane], s_st[64 + im], s_st[128 + lane], c, dt);
-        s_rho[lane] = __fsub_rn(n_new, 1.0f);
-        if (ftj) ftj[(int64_t)t * NX + lane] = Fv;
-      }
-      wave_lds_sync();
-      if (lane < NX) {
-        const float E_new = poisson_cell(s_rho, s_c, lane, NX);
-        s_st[lane] = n_new;
-        s_st[64 + lane] = u_new;
-        s_st[128 + lane] = E_new;
-      }
-      wave_lds_sync();
-      emit(t + 1);
-    }
-    lds_barrier();  // new state visible to every wave
-  }
-  R.drain();
-  if (!out) return;
-  float *dst = state_final + b * 3 * NX;
-  for (int i = lane; i < 3 * NX; i += 64) dst[i] = s_st[(i / NX) * 64 + i % NX];
-}
-
-// FluxGNN.forward on B chains of 16*WPI cells, cell-split as above (the
-// small-batch counterpart of chain_flux_kernel<CoreF32, MT, true>, bit-identical to it).
-template <int WPI>
-__global__ __launch_bounds__(256, 1) void chain_flux_cells_kernel(ChainW W, const float *__restrict__ nf,
-                                                                  const float *__restrict__ state, int64_t ld_state,
-                                                                  const float *__restrict__ x, int B,
-                                                                  float *__restrict__ fe, float *__restrict__ ff) {
-  constexpr int NX = 16 * WPI;
-  constexpr int IPW = kWaves / WPI;
-  constexpr int kRingFloats = CellCore::kSlots * CellCore::kChunkFloats;
-  __shared__ f4 lds4[kCellsLds / 4];
-  float *lds = reinterpret_cast<float *>(lds4);
-  const Small S = stage_small(W, lds + kRingFloats);
-  auto R = make_ring<CellCore>(W, lds);
-  const int wave = R.wave, lane = R.lane, j = lane & 15, g = lane >> 4;
-  const bool shadow = wave >= IPW * WPI;
-  const int slot = shadow ? 0 : wave / WPI, pos = shadow ? 0 : wave % WPI;
-  CellHalo X;
-  X.xh = reinterpret_cast<f4 *>(lds + kRingFloats + kSmallFloats + kWaves * kWaveScratchFloats);
-  X.xq = X.xh + kXhF4;
-  X.wave = wave;
-  X.lane = lane;
-  X.par = 0;
-  X.lw = shadow ? wave : slot * WPI + (pos + WPI - 1) % WPI;
-  X.rw = shadow ? wave : slot * WPI + (pos + 1) % WPI;
-  const int b_raw = blockIdx.x * IPW + slot;
-  const bool out = !shadow && b_raw < B;
-  const int64_t b = b_raw < B ? b_raw : B - 1;
-  const int cell = 16 * pos + j;
-  const float feat[1] = {nf ? nf[(b * NX + cell) * kIn + g]
-                            : (g < 3 ? state[b * ld_state + (int64_t)g * NX + cell] : x[cell])};
-  __syncthreads();  // small weights staged (no DMA in flight yet)
-  R.prime();
-  CellCore::Feed F;
-  CellCore::begin(R, F);
-  float f_fwd[1], f_bwd[1];
-  CellCore::gnn_cells(W, S, R, F, feat, f_fwd, f_bwd, X);
-  R.drain();
-  if (!out) return;
-  if (fe && g == 0) fe[b * 2 * NX + cell] = f_fwd[0];
-  if (fe && g == 1) fe[b * 2 * NX + NX + cell] = f_bwd[0];
-  if (ff && g == 2) ff[b * NX + cell] = face_flux(f_fwd[0], f_bwd[0]);
-}
-
-template <int WPI>
-hipError_t flux_cells_launch(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
-                             int B, float *fe, float *ff, hipStream_t s) {
-  constexpr int IPW = kWaves / WPI;
-  hipLaunchKernelGGL((chain_flux_cells_kernel<WPI>), dim3((B + IPW - 1) / IPW), dim3(64 * kWaves), 0, s, w, nf,
-                     state, ld_state, x, B, fe, ff);
-  return hipGetLastError();
-}
-
-template <int WPI>
-hipError_t cells_launch(const ChainW &w, const float *state0, float *state_final, const float *x, const double *pc,
-                        int B, int T, float c, float dt, float *traj, float *flux_traj, float *metrics,
-                        hipStream_t s) {
-  constexpr int IPW = kWaves / WPI;
-  hipLaunchKernelGGL((chain_rollout_cells_kernel<WPI>), dim3((B + IPW - 1) / IPW), dim3(64 * kWaves), 0, s, w,
-                     state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics);
-  return hipGetLastError();
-}
-
 }  // namespace
 
 // Whether the cell-split kernel beats the IC-per-wave kernel for B ICs of nx
 // cells: its workgroups carry 4/WPI ICs at about 1/WPI of the IC-per-wave
 // kernel's time per step (plus the exchanges), against 4 ICs per workgroup.
 bool chain_rollout_prefers_cells(const ChainW &w, int B, int nx) {
-  if (w.prec != kPrecF32 || B <= 0 || (nx != 32 && nx != 48 && nx != 64)) return false;
+  if ((w.prec != kPrecF32 && w.prec != kPrecBF16) || B <= 0 || (nx != 32 && nx != 48 && nx != 64)) return false;
   const int wpi = nx / 16, ipw = kWaves / wpi;
   const int64_t cus = chain::resident_groups();
   const int64_t wave_rounds = ((int64_t)B + 4 * cus - 1) / (4 * cus);
@@ -529,9 +351,9 @@ hipError_t launch_chain_rollout_cells(const ChainW &w, const float *state0, floa
                                       float *flux_traj, float *metrics, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (nx) {
-    case 32: return cells_launch<2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 48: return cells_launch<3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 64: return cells_launch<4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 32: return cells_launch<CellCore, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 48: return cells_launch<CellCore, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 64: return cells_launch<CellCore, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -541,9 +363,9 @@ hipError_t launch_chain_flux_f32(const ChainW &w, const float *nf, const float *
   // small batches: each chain spread over nx/16 waves, as the rollout
   if (chain_rollout_prefers_cells(w, B, nx)) {
     switch (nx) {
-      case 32: return flux_cells_launch<2>(w, nf, state, ld_state, x, B, fe, ff, s);
-      case 48: return flux_cells_launch<3>(w, nf, state, ld_state, x, B, fe, ff, s);
-      case 64: return flux_cells_launch<4>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 32: return flux_cells_launch<CellCore, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 48: return flux_cells_launch<CellCore, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 64: return flux_cells_launch<CellCore, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
       default: break;
     }
   }
