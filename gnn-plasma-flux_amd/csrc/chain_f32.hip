@@ -338,7 +338,7 @@ using CellCore = CoreF32T<kCellsAhead, kCellsAhead + 1>;
 // cells: its workgroups carry 4/WPI ICs at about 1/WPI of the IC-per-wave
 // kernel's time per step (plus the exchanges), against 4 ICs per workgroup.
 bool chain_rollout_prefers_cells(const ChainW &w, int B, int nx) {
-  if ((w.prec != kPrecF32 && w.prec != kPrecBF16) || B <= 0 || (nx != 32 && nx != 48 && nx != 64)) return false;
+  if (B <= 0 || (nx != 32 && nx != 48 && nx != 64)) return false;  // every precision has a cell-split core
   const int wpi = nx / 16, ipw = kWaves / wpi;
   const int64_t cus = chain::resident_groups();
   const int64_t wave_rounds = ((int64_t)B + 4 * cus - 1) / (4 * cus);

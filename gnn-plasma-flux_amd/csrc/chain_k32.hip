@@ -423,11 +423,128 @@ struct CoreF16x3T {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Cell-split f16x3 core for small batches (chain_common.h
+// chain_rollout_cells_kernel / chain_flux_cells_kernel): 16 cells per wave,
+// an IC over nx/16 waves, CoreF16x3T's arithmetic MFMA chain for chain (so a
+// batch gets the IC-per-wave kernels' bits whichever kernel its size
+// selects), laid out like chain_bf16.hip's CellBF16: a layer's four output
+// pairs, then the G values of the edge columns traded through LDS around one
+// barrier, then the epilogue; the readout trades column 0 of P and Q.
+struct CellF16x3 {
+  using Base = CoreF16x3T<1>;  // the rollout's ring: 8 KiB chunks (one unit), 4 slots
+  static constexpr int kNW = Base::kNW;
+  static constexpr int kSlots = Base::kSlots;
+  static constexpr int kChunkFloats = Base::kChunkFloats;
+  static constexpr int kStreamOffset = 0;
+  using R_t = Base::R_t;
+  using Feed = Base::Feed;
+  static __device__ __forceinline__ void begin(R_t &R, Feed &F) { Base::begin(R, F); }
+
+  static __device__ __forceinline__ void gnn_cells(const ChainW &W, const Small &S, R_t &R, Feed &F,
+                                                   const float (&feat)[1], float (&ffwd)[1], float (&fbwd)[1],
+                                                   CellHalo &X) {
+    const int lane = R.lane, g4 = 4 * (lane >> 4), g = lane >> 4, j = lane & 15;
+    Base::Acts<1> A;
+    {
+      f4 h[1][kNT];
+      input_layer<1>(S, lane, feat, h);  // f32 MFMA, ReLU applied
+#pragma unroll
+      for (int kb = 0; kb < Base::kKB; ++kb)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int t = k >> 1, r = 2 * (k & 1);
+          const Split sp = split_pair(h[0][2 * kb + t][r], h[0][2 * kb + t][r + 1]);
+          A.h[0][kb].v[0][k] = sp.hi;
+          A.h[0][kb].v[1][k] = sp.lo;
+        }
+    }
+    // message passing (src/flux_gnn.py:53-60)
+    for (int l = 0; l < W.layers; ++l) {
+      const float *bias = S.bl + l * kH;
+      Base::PairAcc<1> acc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        Base::init_pair<1>(bias, q, g4, acc[q]);
+        Base::unit<1, 0, 0>(R, F, A, acc[q]);
+        interleave<12, 0>();
+        Base::unit<1, 1, 0>(R, F, A, acc[q]);
+        interleave<12, 0>();
+        Base::unit<1, 2, 0>(R, F, A, acc[q]);
+        interleave<12, 0>();
+        Base::unit<1, 3, 0>(R, F, A, acc[q]);
+        interleave<12, 0>();
+      }
+      {
+        f4 G[1][kNT];
+#pragma unroll
+        for (int t = 0; t < kNT; ++t) G[0][t] = acc[t >> 1].g[0][t & 1];
+        X.exchange(G);  // X.l / X.r: G of cell 16*pos - 1 / 16*pos + 16
+      }
+      // h = ReLU(acc + 0.5*(G[i-1] + G[i+1])), split into fp16 hi/lo (Base::piece)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int K = 0; K < 4; ++K) {
+          const int tt = K >> 1, t = 2 * q + tt, r0 = 2 * (K & 1);
+          float v[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int r = r0 + e;
+            const float gv = acc[q].g[0][tt][r];
+            const float gl = dpp_over<kRowShr1>(X.l[t][r], gv), gr = dpp_over<kRowShl1>(X.r[t][r], gv);
+            v[e] = relu(fmaf(__fadd_rn(gl, gr), 0.5f, acc[q].a[0][tt][r]));
+          }
+          const Split sp = split_pair(v[0], v[1]);
+          A.h[0][q].v[0][K] = sp.hi;
+          A.h[0][q].v[1][K] = sp.lo;
+        }
+    }
+    // edge readout, P/Q split (src/flux_gnn.py:62-66): all 8 tiles, column 0
+    // of P and Q through LDS, then the epilogue rows in Base::readout's order
+    f4 P[kNT][1], Q[kNT][1];
+#pragma unroll
+    for (int ot = 0; ot < kNT; ++ot) {
+      Base::init_ro<1>(S, ot, g4, P[ot], Q[ot]);
+      Base::ro_unit<1, 0, 0>(R, F, A, P[ot], Q[ot]);
+      interleave<12, 0>();
+      Base::ro_unit<1, 1, 0>(R, F, A, P[ot], Q[ot]);
+      interleave<12, 0>();
+      if (j == 0) {
+        X.xq[((X.wave * kNT + ot) * 2 + 0) * 4 + g] = P[ot][0];
+        X.xq[((X.wave * kNT + ot) * 2 + 1) * 4 + g] = Q[ot][0];
+      }
+    }
+    lds_barrier();
+    float pf = 0.f, pb = 0.f;
+#pragma unroll
+    for (int ot = 0; ot < kNT; ++ot) {
+      const f4 prh = X.xq[((X.rw * kNT + ot) * 2 + 0) * 4 + g];
+      const f4 qrh = X.xq[((X.rw * kNT + ot) * 2 + 1) * 4 + g];
+      const f4 w2 = ldf4(S.w2 + 16 * ot + g4);
+      readout_row_halo<0>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
+      readout_row_halo<1>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
+      readout_row_halo<2>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
+      readout_row_halo<3>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
+    }
+    float pf1[1] = {pf}, pb1[1] = {pb};
+    readout_finish<1>(pf1, pb1, W.b2, ffwd, fbwd);
+  }
+};
+
 }  // namespace
 
 hipError_t launch_chain_flux_k32(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                  const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
   if (w.prec != kPrecF16x3) return launch_chain_flux_bf16(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  if (chain_rollout_prefers_cells(w, B, nx)) {  // small batches: each chain over nx/16 waves
+    switch (nx) {
+      case 32: return chain::flux_cells_launch<CellF16x3, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 48: return chain::flux_cells_launch<CellF16x3, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 64: return chain::flux_cells_launch<CellF16x3, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
+      default: break;
+    }
+  }
   if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
     return chain::launch_flux_core<CoreF16x3T<1>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
   return chain::launch_flux_windowed<CoreF16x3T<2>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
@@ -436,6 +553,14 @@ hipError_t launch_chain_flux_k32(const ChainW &w, const float *nf, const float *
 hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float *state_final, const float *x,
                                     const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                     float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
+  if (w.prec == kPrecF16x3 && ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx)) {
+    switch (nx) {  // small batches: each IC over nx/16 waves (cell-split kernel, same bits)
+      case 32: return chain::cells_launch<CellF16x3, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 48: return chain::cells_launch<CellF16x3, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 64: return chain::cells_launch<CellF16x3, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      default: break;
+    }
+  }
   if (w.prec == kPrecF16x3)
     return chain::launch_rollout_core<CoreF16x3T<1>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
                                                      flux_traj, metrics, ex, s);

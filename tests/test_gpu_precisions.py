@@ -191,16 +191,18 @@ def test_bf16_rollout_nx64_vs_oracles(hf, record):
     close(traj, wbf, BF16_STATE_WBF16)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "f16x3"])
 @pytest.mark.parametrize("nx", [32, 48, 64])
-def test_bf16_cell_split_kernel_bitwise(hf, nx):
-    """bf16 small batches run the cell-split kernel (CellBF16: an IC over nx/16
-    waves, the G edge columns and readout column 0 traded through LDS), large
-    ones the IC-per-wave kernels: every output, every step, bit-identical.  B=5
-    leaves a workgroup half empty at nx=32 and runs the shadow wave at nx=48.
-    The small-batch rollout and flux also follow the emulating oracle."""
+def test_k32_cell_split_kernel_bitwise(hf, nx, precision):
+    """bf16 / f16x3 small batches run the cell-split kernels (CellBF16,
+    CellF16x3: an IC over nx/16 waves, the G edge columns and readout column 0
+    traded through LDS), large ones the IC-per-wave kernels: every output,
+    every step, bit-identical.  B=5 leaves a workgroup half empty at nx=32 and
+    runs the shadow wave at nx=48.  The small-batch rollout and flux also
+    follow the oracles (bf16: the emulating oracle; f16x3: float32)."""
     w = weights("W1_r2")
     G = O.Grid(nx, dt=5e-3 * min(1.0, nx / 64.0))
-    solver = hf.HybridSolver(w, radius=2, nx=nx, dt=G.dt, device=DEV, precision="bf16")
+    solver = hf.HybridSolver(w, radius=2, nx=nx, dt=G.dt, device=DEV, precision=precision)
     big = solver.baseline.initial_conditions(list(range(2000, 2000 + 3072)), as_tensor=True)
     ref = solver.run_batch(big, 12, traj=True, flux=True, metrics=True)
     for sub in ([0, 1, 2, 3, 4], list(range(100, 356))):
@@ -208,15 +210,23 @@ def test_bf16_cell_split_kernel_bitwise(hf, nx):
         for k in ("final", "traj", "flux", "metrics"):
             assert torch.equal(got[k], ref[k][sub]), (nx, len(sub), k)
     ics = big.cpu().numpy()
-    emul, _ = O.hybrid_run(O.params_from(w), G, ics[:5], 12, flux_fn=O.hybrid_flux_edge_bf16)
-    close(ref["traj"][:5].cpu().numpy(), emul, BF16_STATE_EMUL)
+    p = O.params_from(w)
+    if precision == "bf16":
+        want, _ = O.hybrid_run(p, G, ics[:5], 12, flux_fn=O.hybrid_flux_edge_bf16)
+        close(ref["traj"][:5].cpu().numpy(), want, BF16_STATE_EMUL)
+    else:
+        want, _ = O.hybrid_run(p, G, ics[:5], 12)
+        close(ref["traj"][:5].cpu().numpy(), want, 1e-5, 1e-5)
     with torch.no_grad():
         nf, ei = hf.build_chain_graph_batch(ics, G.x, DEV)
         fe_big = solver.model(nf, ei).reshape(len(ics), 2 * nx)
         nf, ei = hf.build_chain_graph_batch(ics[:5], G.x, DEV)
         fe_small = solver.model(nf, ei).reshape(5, 2 * nx)
     assert torch.equal(fe_small, fe_big[:5])
-    close(fe_small.cpu().numpy(), O.hybrid_flux_edge_bf16(O.params_from(w), G, ics[:5]), BF16_FLUX_EMUL)
+    if precision == "bf16":
+        close(fe_small.cpu().numpy(), O.hybrid_flux_edge_bf16(p, G, ics[:5]), BF16_FLUX_EMUL)
+    else:
+        close(fe_small.cpu().numpy(), O.hybrid_flux_edge(p, G, ics[:5]), 2e-6)
 
 
 def test_bf16_full_size_cfg4_properties(hf, record):
