@@ -61,14 +61,15 @@ def pinned(n):
     return set(avail[:n])
 
 
-def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=None):
+def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=None, also=None):
     """Time one more BASELINE.json single-GPU config the same way as the
     headline (preallocated outputs and workspace, HIP events on the launch
     stream, wall clock around the launches).  Reported next to the headline,
     never as it.  W untimed warmup steps run first as one rollout (cfg4: as
-    many as it times, ~40 ms, so the timed rollout runs at the sustained clock
-    rather than in the clock ramp after the host-side setup; the headline keeps
-    the driver's --warmup).  fixture: {label: states [n, K+1, 3, nx]} of the batch's first
+    many as it times (cfg4 ~40 ms), so the timed rollout runs at the sustained
+    clock rather than in the clock ramp after the host-side setup; the headline
+    keeps the driver's --warmup).  also: the same workload in another precision,
+    timed the same way and reported under alt_<precision>.  fixture: {label: states [n, K+1, 3, nx]} of the batch's first
     n ICs (committed test vectors); the final states' max |error| against each
     is reported."""
     from hybridflux import HybridSolver, engine
@@ -97,6 +98,20 @@ def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=Non
            "value": round(B * K / wall, 1), "unit": "IC-steps/s", "ms_per_step": round(wall / K * 1e3, 4),
            "kernel_ms": round(kms, 3), "mfma_frac": round(flop / (kms * 1e-3) / 1e12 / peak, 4),
            "finite_fraction": float(met[:, -1, 2].float().mean().item())}
+    if also:  # the same workload in another precision (reported beside, not instead)
+        s2 = HybridSolver(weights, radius=radius, nx=nx, dt=dt, device=dev, precision=also)
+        s2.run_batch(ics, max(W, 1), traj=False, ws=ws)
+        final2 = torch.empty_like(ics)
+        torch.cuda.synchronize(dev)
+        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ta = time.perf_counter()
+        a0.record(stream)
+        s2.run_batch(ics, K, traj=False, metrics=met, out=final2, ws=ws)
+        a1.record(stream)
+        torch.cuda.synchronize(dev)
+        wall2 = time.perf_counter() - ta
+        out[f"alt_{also}"] = {"value": round(B * K / wall2, 1), "kernel_ms": round(a0.elapsed_time(a1), 3),
+                              "max_abs_diff_vs_f32_final_state": float((final2 - final).abs().max().item())}
     for label, want in (fixture or {}).items():
         n = want.shape[0]
         if want.shape[1] == K + 1:
@@ -235,7 +250,9 @@ def main():
               "reference_f32": ref["states"]}
         w_r1 = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r1.npz"), allow_pickle=False))
         w_r2 = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r2.npz"), allow_pickle=False))
-        others = [other_config(w_r1, dev, "cfg2: 64-cell chain, 256-IC batch, r=1, f32", 256, 64, "f32", K, W, 1),
+        # both at BASELINE's T = 30, warmed for as many steps as they time
+        others = [other_config(w_r1, dev, "cfg2: 64-cell chain, 256-IC batch, r=1, f32", 256, 64, "f32", 30, 30, 1,
+                               also="f16x3"),
                   other_config(w_r2, dev, "cfg4: 1024-cell chain, 4096-IC batch, r=2, bf16 MLP weights, dt=3.125e-4",
                                4096, 1024, "bf16", 30, 30, 2, fixture=fx)]
 
