@@ -134,9 +134,8 @@ struct CellHalo {
   f4 *xh;             // [parity 2][wave 4][side 2][g 4][nt 8]: boundary columns of h
   f4 *xq;             // [wave 4][ot 8][P|Q 2][g 4]: column j=0 of the readout accumulators
   int wave, lw, rw, lane, par;
-  // Publish this wave's boundary columns of h (j = 0: side 0, j = 15: side 1),
-  // then read the left wave's side 1 and the right wave's side 0.
-  __device__ __forceinline__ void exchange(const f4 (&h)[1][kNT]) {
+  // Publish this wave's boundary columns of h (j = 0: side 0, j = 15: side 1).
+  __device__ __forceinline__ void publish(const f4 (&h)[1][kNT]) {
     f4 *b = xh + par * (kWaves * 2 * 4 * kNT);
     const int j = lane & 15, g = lane >> 4;
     if (j == 0 || j == 15) {
@@ -144,13 +143,24 @@ struct CellHalo {
 #pragma unroll
       for (int nt = 0; nt < kNT; ++nt) b[((wave * 2 + side) * 4 + g) * kNT + nt] = h[0][nt];
     }
-    lds_barrier();
+  }
+  // After a workgroup barrier that follows every wave's publish(): the left
+  // wave's side 1 and the right wave's side 0.  (The buffer alternates by
+  // parity, so the next publish never overwrites columns still being read.)
+  __device__ __forceinline__ void read() {
+    const f4 *b = xh + par * (kWaves * 2 * 4 * kNT);
+    const int g = lane >> 4;
 #pragma unroll
     for (int nt = 0; nt < kNT; ++nt) {
       l[nt] = b[((lw * 2 + 1) * 4 + g) * kNT + nt];
       r[nt] = b[((rw * 2 + 0) * 4 + g) * kNT + nt];
     }
     par ^= 1;
+  }
+  __device__ __forceinline__ void exchange(const f4 (&h)[1][kNT]) {
+    publish(h);
+    lds_barrier();
+    read();
   }
 };
 

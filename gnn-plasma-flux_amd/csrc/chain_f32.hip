@@ -99,9 +99,10 @@ struct CoreF32T {
   // matrix pipe between m-tiles.
   template <int MT, int KS, class H>
   static __device__ __forceinline__ void layer_step(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
-                                                    f4 (&acc)[MT][kNT], const H &X) {
+                                                    f4 (&acc)[MT][kNT], H &X) {
     f4 a[2];
     take<KS % kUPC>(R, F, a);
+    if constexpr (H::kOn && KS == kUPC) X.read();  // the ring barrier of take<kUPC-1> follows every publish
     float bn[MT];
     if constexpr (KS + 1 < 2 * kKS) b_operand<MT, KS + 1>(h, bn, X);
 #pragma unroll
@@ -127,7 +128,7 @@ struct CoreF32T {
   }
   template <int MT, int KS0, class H>
   static __device__ __forceinline__ void layer_chunk(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
-                                                     f4 (&acc)[MT][kNT], const H &X) {
+                                                     f4 (&acc)[MT][kNT], H &X) {
     layer_step<MT, KS0 + 0>(R, F, h, b, acc, X);
     layer_step<MT, KS0 + 1>(R, F, h, b, acc, X);
     layer_step<MT, KS0 + 2>(R, F, h, b, acc, X);
@@ -166,47 +167,54 @@ struct CoreF32T {
     readout_unit<MT, HH, 3>(R, F, h, P, Q);
   }
 
-  // Edge readout of a cell-split wave (MT = 1): all 8 output tiles' P and Q
-  // first, then column j = 0 of each through LDS (P(i+1), Q(i+1) of lane 15
-  // live on the right wave), then the epilogues and partial dots in the same
-  // order as gnn_impl's readout, so the fluxes are bit-identical to it.
+  // Edge readout of a cell-split wave (MT = 1), pipelined tile by tile: tile
+  // ot's column j = 0 of P and Q is published through LDS after its MFMAs
+  // (P(i+1), Q(i+1) of lane 15 live on the right wave), read after the ring
+  // barrier that ends tile ot+1's first chunk, and tile ot's epilogue runs
+  // under tile ot+1's second chunk; only the last tile needs a barrier of its
+  // own.  Epilogues and partial dots run in gnn_impl's readout order, so the
+  // fluxes are bit-identical to it.
   static __device__ __forceinline__ void readout_cells(const ChainW &W, const Small &S, R_t &R, Feed &F,
                                                        const f4 (&h)[1][kNT], float (&ffwd)[1], float (&fbwd)[1],
                                                        CellHalo &X) {
     const int lane = R.lane, j = lane & 15, g = lane >> 4, g4 = 4 * g;
-    f4 P[kNT][1], Q[kNT][1];
+    float pf = 0.f, pb = 0.f, sf = 0.f, sb = 0.f;
+    // epilogue of tile ot (after the barrier that follows its publish); a tile
+    // pair's partial dots are summed across the lane groups after its second tile
+    auto epilogue = [&](int ot, const f4 &P, const f4 &Q) {
+      const f4 prh = X.xq[((X.rw * kNT + ot) * 2 + 0) * 4 + g];
+      const f4 qrh = X.xq[((X.rw * kNT + ot) * 2 + 1) * 4 + g];
+      const f4 w2 = ldf4(S.w2 + 16 * ot + g4);
+      readout_row_halo<0>(P, Q, prh, qrh, w2, pf, pb);
+      readout_row_halo<1>(P, Q, prh, qrh, w2, pf, pb);
+      readout_row_halo<2>(P, Q, prh, qrh, w2, pf, pb);
+      readout_row_halo<3>(P, Q, prh, qrh, w2, pf, pb);
+      if (ot & 1) {
+        float pf1[1] = {pf}, pb1[1] = {pb}, ff[1], fb[1];
+        readout_finish<1>(pf1, pb1, 0.f, ff, fb);
+        sf = __fadd_rn(sf, ff[0]);
+        sb = __fadd_rn(sb, fb[0]);
+        pf = pb = 0.f;
+      }
+    };
+    f4 Pp, Qp;  // the previous tile's accumulators
 #pragma unroll
     for (int ot = 0; ot < kNT; ++ot) {
-      P[ot][0] = ldf4(S.be + 16 * ot + g4);  // b_e as P's initial accumulator
-      Q[ot][0] = f4{0.f, 0.f, 0.f, 0.f};
-      readout_chunk<1, 0>(R, F, h, P[ot], Q[ot]);
-      readout_chunk<1, 1>(R, F, h, P[ot], Q[ot]);
+      f4 P[1], Q[1];
+      P[0] = ldf4(S.be + 16 * ot + g4);  // b_e as P's initial accumulator
+      Q[0] = f4{0.f, 0.f, 0.f, 0.f};
+      readout_chunk<1, 0>(R, F, h, P, Q);  // ends with the ring barrier
+      if (ot > 0) epilogue(ot - 1, Pp, Qp);
+      readout_chunk<1, 1>(R, F, h, P, Q);
       if (j == 0) {
-        X.xq[((X.wave * kNT + ot) * 2 + 0) * 4 + g] = P[ot][0];
-        X.xq[((X.wave * kNT + ot) * 2 + 1) * 4 + g] = Q[ot][0];
+        X.xq[((X.wave * kNT + ot) * 2 + 0) * 4 + g] = P[0];
+        X.xq[((X.wave * kNT + ot) * 2 + 1) * 4 + g] = Q[0];
       }
+      Pp = P[0];
+      Qp = Q[0];
     }
     lds_barrier();
-    float sf = 0.f, sb = 0.f;
-#pragma unroll
-    for (int w = 0; w < kNT / 2; ++w) {
-      float pf = 0.f, pb = 0.f;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int ot = 2 * w + t;
-        const f4 prh = X.xq[((X.rw * kNT + ot) * 2 + 0) * 4 + g];
-        const f4 qrh = X.xq[((X.rw * kNT + ot) * 2 + 1) * 4 + g];
-        const f4 w2 = ldf4(S.w2 + 16 * ot + g4);
-        readout_row_halo<0>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
-        readout_row_halo<1>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
-        readout_row_halo<2>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
-        readout_row_halo<3>(P[ot][0], Q[ot][0], prh, qrh, w2, pf, pb);
-      }
-      float pf1[1] = {pf}, pb1[1] = {pb}, ff[1], fb[1];
-      readout_finish<1>(pf1, pb1, 0.f, ff, fb);
-      sf = __fadd_rn(sf, ff[0]);
-      sb = __fadd_rn(sb, fb[0]);
-    }
+    epilogue(kNT - 1, Pp, Qp);
     ffwd[0] = __fadd_rn(sf, W.b2);
     fbwd[0] = __fadd_rn(sb, W.b2);
   }
@@ -237,7 +245,10 @@ struct CoreF32T {
     const int g4 = 4 * (lane >> 4);
     f4 h[MT][kNT];
     input_layer<MT>(S, lane, feat, h);
-    if constexpr (H::kOn) X.exchange(h);
+    // cell-split waves: the boundary columns are published here and read
+    // after the ring barrier that ends the next layer's first chunk
+    // (layer_step<4>), long before the first neighbour-sum k-step (32)
+    if constexpr (H::kOn) X.publish(h);
 
     // message passing: h = ReLU(W_l [h ; (h[i+1]+h[i-1])/2] + b_l)        (src/flux_gnn.py:53-60)
     for (int l = 0; l < W.layers; ++l) {
@@ -273,7 +284,7 @@ struct CoreF32T {
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) h[mt][nt] = relu4(acc[mt][nt]);
       if constexpr (H::kOn) {
-        if (l + 1 < W.layers) X.exchange(h);
+        if (l + 1 < W.layers) X.publish(h);
       }
     }
     if constexpr (H::kOn) {
