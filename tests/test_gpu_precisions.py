@@ -229,6 +229,26 @@ def test_k32_cell_split_kernel_bitwise(hf, nx, precision):
         close(fe_small.cpu().numpy(), O.hybrid_flux_edge(p, G, ics[:5]), 2e-6)
 
 
+@pytest.mark.parametrize("precision", ["f32", "bf16", "f16x3"])
+@pytest.mark.parametrize("layers", [0, 2, 7])
+def test_cell_split_rollout_any_layer_count(hf, layers, precision):
+    """The cell-split rollouts (every precision) against the IC-per-wave
+    kernels at other layer counts (FluxGNN(4,128,L), random weights, nx=48 with
+    its shadow wave): 5 ICs alone (cell-split) == the same ICs inside 2048
+    (IC-per-wave), bitwise, trajectory, face flux and metrics."""
+    from hybridflux import engine
+    dev = torch.device(DEV)
+    grid = engine.Grid(48, dt=3.75e-3)
+    m = engine.DeviceModel(rand_sd(layers, 90 + layers), dev, precision)
+    G = O.Grid(48, dt=3.75e-3)
+    ics = torch.as_tensor(np.stack([O.initial_condition(G, s) for s in range(3000, 3000 + 2048)]), device=dev)
+    big = engine.run(m, grid, ics, 6, traj=True, flux=True, metrics=True)
+    small = engine.run(m, grid, ics[:5].contiguous(), 6, traj=True, flux=True, metrics=True)
+    for k in ("final", "traj", "flux", "metrics"):
+        assert torch.equal(small[k], big[k][:5]), k
+    assert torch.isfinite(small["traj"]).all()
+
+
 def test_bf16_full_size_cfg4_properties(hf, record):
     """BASELINE config 4 at full size (4096 ICs x 1024 cells, 30 steps, bf16):
     deterministic, batch-invariant (the first 256 ICs alone == inside the batch,
