@@ -243,6 +243,27 @@ def main():
                      "max_abs_diff_vs_headline_final_state": dev_err}
         del s2, r2
 
+    # cfg3 names "all ablation radii": the other two checkpoints (W1_r1, W1_r2)
+    # on the same ICs, timed the same way (the radius only selects the weights)
+    radii = None
+    if world == 1 and not args.no_other_configs and nx == 64 and args.precision == "f32":
+        radii = {}
+        for r in (1, 2):
+            wr = dict(np.load(os.path.join(ROOT, "tests", "golden", f"weights_W1_r{r}.npz"), allow_pickle=False))
+            s2 = HybridSolver(wr, radius=r, nx=nx, dt=dt, device=dev, precision=args.precision)
+            s2.run_batch(ics, max(W, 1), traj=not args.no_traj)
+            torch.cuda.synchronize(dev)
+            a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ta = time.perf_counter()
+            a0.record(stream)
+            s2.run_batch(ics, K, traj=traj_buf if traj_buf is not None else False, metrics=met_buf,
+                         out=torch.empty_like(ics))
+            a1.record(stream)
+            torch.cuda.synchronize(dev)
+            wall2 = time.perf_counter() - ta
+            radii[f"W1_r{r}"] = {"value": round(B * K / wall2, 1), "kernel_ms": round(a0.elapsed_time(a1), 3)}
+            del s2
+
     others = None
     if world == 1 and not args.no_other_configs:
         # cfg4's first ICs (seeds 1000..1003) against committed vectors: the bf16
@@ -328,6 +349,7 @@ def main():
             # SURVEY.md 8(d) secondary rates: batch-steps/s = T / wall, cell-steps/s = IC-steps/s * nx
             "also": {"batch_steps_per_s": round(K / wall_max, 1), "cell_steps_per_s": round(value * nx, 1)},
             "alt": alt or None,
+            "radii": radii,
             "other_configs": others,
         }
         print(json.dumps(line), flush=True)
