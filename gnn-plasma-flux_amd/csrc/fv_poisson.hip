@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
 // ------------------------------------------------------------ large nx
 // nx > kFvLdsMaxNx (the chain no longer fits the LDS plan above): the update
 // and the Poisson solve run as separate launches over global memory, a
-// 256-cell block per workgroup (grid: cell blocks x ICs).  The Poisson sum
+// 256-cell block per workgroup (grid: ICs x cell blocks).  The Poisson sum
 // walks j in the order poisson_cell does, the even terms into a0 and the odd
 // ones into a1, with rho and the window of c a tile needs staged in LDS, so
 // E is the LDS kernels' value bit for bit; the metrics come from
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(kFvThreads) void fv_update_kernel(const float *__re
                                                                const float *__restrict__ face_flux, int nx, float c,
                                                                float dt, float nu, float dx2,
                                                                float *__restrict__ flux_out, int64_t ld_flux) {
-  const int64_t b = blockIdx.y;
-  const int i = blockIdx.x * kFvThreads + threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int i = blockIdx.y * kFvThreads + threadIdx.x;
   if (i >= nx) return;
   const float *st = in + b * ld_in;
   float *so = out + b * ld_out;
@@ -138,8 +138,8 @@ __global__ __launch_bounds__(kFvThreads) void poisson_tiled_kernel(const float *
                                                                    const double *__restrict__ pc, int nx) {
   __shared__ float s_rho[kPoissonTileJ];
   __shared__ double s_c[kPoissonTileJ + kFvThreads];
-  const int64_t b = blockIdx.y;
-  const int i0 = blockIdx.x * kFvThreads, i = i0 + threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int i0 = blockIdx.y * kFvThreads, i = i0 + threadIdx.x;
   double a0 = 0.0, a1 = 0.0;
   for (int j0 = 0; j0 < nx; j0 += kPoissonTileJ) {
     const int T = nx - j0 < kPoissonTileJ ? nx - j0 : kPoissonTileJ;
@@ -406,7 +406,7 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
     }
   }
   if (nx > kFvLdsMaxNx) {  // large nx: update, Poisson, metrics as three launches
-    const dim3 grid((unsigned)((nx + kFvThreads - 1) / kFvThreads), (unsigned)B);
+    const dim3 grid((unsigned)B, (unsigned)((nx + kFvThreads - 1) / kFvThreads));  // ICs on x (no 65535 cap)
     if (face_flux)
       hipLaunchKernelGGL(fv_update_kernel<true>, grid, dim3(kFvThreads), 0, s, in, ld_in, out, ld_out, face_flux, nx,
                          c, dt, nu, dx2, flux_out, ld_flux);
@@ -457,7 +457,7 @@ hipError_t launch_poisson(const float *n, int ld_n, float *E, int ld_E, const do
     default: break;
   }
   if (nx > kFvLdsMaxNx) {
-    hipLaunchKernelGGL(poisson_tiled_kernel, dim3((unsigned)((nx + kFvThreads - 1) / kFvThreads), (unsigned)B),
+    hipLaunchKernelGGL(poisson_tiled_kernel, dim3((unsigned)B, (unsigned)((nx + kFvThreads - 1) / kFvThreads)),
                        dim3(kFvThreads), 0, s, n, (int64_t)ld_n, E, (int64_t)ld_E, pc, nx);
     return hipGetLastError();
   }
