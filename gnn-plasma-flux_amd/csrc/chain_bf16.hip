@@ -936,7 +936,11 @@ hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float 
   }
   if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
     return chain::launch_flux_core<CoreBF16<8, 4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
-  return launch_flux_sw<CoreBF16<8, 4, 4, false, 3, 1, 0, true>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+// ring position of the deferred DMA: 0 (pair unit 2) measured best; 1, 2, 3: +3-10 % (profiles/r02_cfg4_diag.jsonl, run D)
+#ifndef HF_SW_DMAU
+#define HF_SW_DMAU 0
+#endif
+  return launch_flux_sw<CoreBF16<8, 4, 4, false, 3, 1, HF_SW_DMAU, true>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float *state_final, const float *x,
