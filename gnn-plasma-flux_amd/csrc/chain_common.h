@@ -655,15 +655,15 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
 // ---------------------------------------------------------------------------
 // Cell-split persistent rollout for small batches: an IC of NX = 16*WPI cells
 // on WPI waves (16 consecutive cells each; cell core CC: CoreF32 at MT = 1 in
-// chain_f32.hip, CellBF16 in chain_bf16.hip), 4/WPI ICs per
+// chain_f32.hip, CellBF16 in chain_bf16.hip, CellF16x3 in chain_k32.hip), 4/WPI ICs per
 // workgroup (WPI = 3: one IC and a shadow wave that keeps the weight ring's
 // lockstep and writes nothing).  B ICs occupy B*WPI/4 CUs' worth of waves
 // instead of B/4, for the same per-cell arithmetic as chain_rollout_kernel:
 // every MFMA chain, neighbour sum, readout partial dot and FV/Poisson
 // expression is evaluated in the same order, so the results are bit-identical
 // to it.  The four waves share the LDS weight ring as in chain_rollout_kernel;
-// per layer they swap boundary columns of h (CellHalo), per step column 0 of
-// the readout accumulators.  The IC's first wave does FV + Poisson + outputs
+// per layer they swap boundary columns of h (f32) or G (bf16, f16x3) through
+// CellHalo, per step column 0 of the readout accumulators.  The IC's first wave does FV + Poisson + outputs
 // for all its cells, one per lane (src/hybrid_solver.py:45-63).
 constexpr int kXhF4 = 2 * kWaves * 2 * 4 * kNT;  // CellHalo::xh
 constexpr int kXqF4 = kWaves * kNT * 2 * 4;      // CellHalo::xq
