@@ -196,8 +196,11 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ws, _ = engine.workspace(HF_OP_RUN, B, nx, K, dev)
 
-    # warmup: one rollout of W steps (compiles nothing; faults the code objects in)
-    solver.run_batch(ics, max(W, 1), traj=not args.no_traj, metrics=True, ws=ws)
+    # warmup: one rollout of W steps (compiles nothing; faults the code objects
+    # in) and its metric exchange (RCCL sets up its channels on first use)
+    warm = solver.run_batch(ics, max(W, 1), traj=not args.no_traj, metrics=True, ws=ws)
+    gather_rollout(warm, n_total)
+    del warm
     torch.cuda.synchronize(dev)
 
     # preallocate outputs so the timed region is launches + the metric exchange
