@@ -761,10 +761,11 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
         s_st[64 + lane] = u_new;
         s_st[128 + lane] = E_new;
       }
-      wave_lds_sync();
-      emit(t + 1);
     }
     lds_barrier();  // new state visible to every wave
+    // the lead's outputs of the new state overlap the other waves' next
+    // forward (nothing writes the state again before this step's FV)
+    if (lead) emit(t + 1);
   }
   R.drain();
   if (!out) return;
