@@ -5,7 +5,9 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -611,6 +613,79 @@ struct Scratch {
   }
 };
 
+// The per-step sequencing of the generic path for one slice of the batch:
+// [chain flux ->] FV + Poisson per step, ping-ponging through buf0/buf1 (or
+// the trajectory).  ldT / ldM / ldFT are the per-IC strides of traj, metrics
+// and flux_traj, so a slice is the same call on offset pointers.
+hipError_t run_steps(const hf_model *m, const float *state0, float *state_final, const float *x, const double *pc,
+                     int B, int nx, int T, float c, float dt, float nu, float dx2, float *traj, float *flux_traj,
+                     float *metrics, float *buf0, float *buf1, float *F, hipStream_t s) {
+  const int64_t S = 3LL * nx, ldT = (T + 1) * S, ldM = (int64_t)(T + 1) * HF_NUM_METRICS;
+  float *buf[2] = {buf0, buf1};
+  hipError_t e = hipSuccess;
+  const float *cur = state0;
+  int64_t ld_cur = S;
+  for (int t = 0; t < T && e == hipSuccess; ++t) {
+    float *dst;
+    int64_t ld_dst;
+    if (traj) {
+      dst = traj + (int64_t)(t + 1) * S;
+      ld_dst = ldT;
+    } else if (t == T - 1 && state_final != state0) {
+      dst = state_final;
+      ld_dst = S;
+    } else {
+      dst = buf[t & 1];
+      ld_dst = S;
+    }
+    if (m) e = hf::launch_chain_flux(m->chain, nullptr, cur, ld_cur, x, B, nx, nullptr, F, s);
+    if (e == hipSuccess)
+      e = hf::launch_fv_step(cur, ld_cur, dst, ld_dst, F, pc, B, nx, c, dt, nu, dx2,
+                             flux_traj ? flux_traj + (int64_t)t * nx : nullptr, (int64_t)T * nx,
+                             metrics ? metrics + (int64_t)(t + 1) * HF_NUM_METRICS : nullptr, ldM, s);
+    cur = dst;
+    ld_cur = ld_dst;
+  }
+  if (e == hipSuccess && cur != state_final)
+    e = hipMemcpy2DAsync(state_final, sizeof(float) * S, cur, sizeof(float) * ld_cur, sizeof(float) * S, B,
+                         hipMemcpyDeviceToDevice, s);
+  return e;
+}
+
+// Lanes of the generic hybrid rollout.  Its steps are a persistent flux kernel
+// that fills every CU (one workgroup each, LDS-bound) and then the short
+// FV/Poisson kernel; inside one stream the flux kernel's last round of windows
+// and the whole FV kernel leave most CUs idle.  With two lanes the two halves
+// of the batch step independently on the caller's stream and a second stream
+// (forked and joined with events), so one half's flux windows fill the CUs
+// the other half's tail and FV leave idle.  Every IC's arithmetic is the same
+// in either form.  HF_RUN_LANES=1 forces one lane (A/B timing).
+constexpr int64_t kLaneMinCells = 1 << 20;  // each half still fills the chip for several rounds
+
+int run_lanes() {
+  static const int lanes = [] {
+    const char *v = std::getenv("HF_RUN_LANES");
+    return (v && std::atoi(v) == 1) ? 1 : 2;
+  }();
+  return lanes;
+}
+
+hipError_t lane_stream(hipStream_t *out) {
+  static std::mutex mu;
+  static hipStream_t streams[64] = {};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!streams[dev]) {
+    e = hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+  }
+  *out = streams[dev];
+  return hipSuccess;
+}
+
 }  // namespace
 
 int hf_step(hf_model_t m, const float *in, float *out, const float *x, const double *pc, int B, int nx,
@@ -683,36 +758,41 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   const int64_t sbytes = (sizeof(float) * B * S + 255) / 256 * 256, fbytes = (sizeof(float) * B * nx + 255) / 256 * 256;
   Scratch sc;
   if (int rc = sc.init(ws, ws_bytes, (traj ? 0 : 2 * sbytes) + (m ? fbytes : 0), s, "hf_run")) return rc;
-  float *buf[2] = {nullptr, nullptr};
-  if (!traj) buf[0] = sc.take(sbytes), buf[1] = sc.take(sbytes);
+  float *buf0 = nullptr, *buf1 = nullptr;
+  if (!traj) buf0 = sc.take(sbytes), buf1 = sc.take(sbytes);
   float *F = m ? sc.take(fbytes) : nullptr;
-  hipError_t e = hipSuccess;
-  const float *cur = state0;
-  int64_t ld_cur = S;
-  for (int t = 0; t < T && e == hipSuccess; ++t) {
-    float *dst;
-    int64_t ld_dst;
-    if (traj) {
-      dst = traj + (int64_t)(t + 1) * S;
-      ld_dst = ldT;
-    } else if (t == T - 1 && state_final != state0) {
-      dst = state_final;
-      ld_dst = S;
-    } else {
-      dst = buf[t & 1];
-      ld_dst = S;
-    }
-    if (m) e = hf::launch_chain_flux(m->chain, nullptr, cur, ld_cur, x, B, nx, nullptr, F, s);
-    if (e == hipSuccess)
-      e = hf::launch_fv_step(cur, ld_cur, dst, ld_dst, F, pc, B, nx, c, dt, nu, dx2,
-                             flux_traj ? flux_traj + (int64_t)t * nx : nullptr, (int64_t)T * nx,
-                             metrics ? metrics + (int64_t)(t + 1) * HF_NUM_METRICS : nullptr, ldM, s);
-    cur = dst;
-    ld_cur = ld_dst;
+  if (!m || B < 2 || (int64_t)B * nx < 2 * kLaneMinCells || run_lanes() == 1) {
+    HF_CHECK_HIP(run_steps(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics, buf0,
+                           buf1, F, s),
+                 "hf_run");
+    return HF_OK;
   }
-  if (e == hipSuccess && cur != state_final)
-    e = hipMemcpy2DAsync(state_final, sizeof(float) * S, cur, sizeof(float) * ld_cur, sizeof(float) * S, B,
-                         hipMemcpyDeviceToDevice, s);
+  // two lanes: ICs [0, B0) on the caller's stream, [B0, B) on the lane stream
+  const int B0 = B / 2;
+  const int64_t o = B0;
+  hipStream_t s2;
+  HF_CHECK_HIP(lane_stream(&s2), "hf_run lane stream");
+  hipEvent_t fork, join;
+  HF_CHECK_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "hf_run lane event");
+  hipError_t e = hipEventCreateWithFlags(&join, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    (void)hipEventDestroy(fork);
+    return fail_hip(e, "hf_run lane event");
+  }
+  e = hipEventRecord(fork, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s2, fork, 0);
+  if (e == hipSuccess)
+    e = run_steps(m, state0 + o * S, state_final + o * S, x, pc, B - B0, nx, T, c, dt, nu, dx2,
+                  traj ? traj + o * ldT : nullptr, flux_traj ? flux_traj + o * T * nx : nullptr,
+                  metrics ? metrics + o * ldM : nullptr, buf0 ? buf0 + o * S : nullptr,
+                  buf1 ? buf1 + o * S : nullptr, F + o * nx, s2);
+  if (e == hipSuccess)
+    e = run_steps(m, state0, state_final, x, pc, B0, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics, buf0, buf1, F,
+                  s);
+  if (e == hipSuccess) e = hipEventRecord(join, s2);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+  (void)hipEventDestroy(fork);
+  (void)hipEventDestroy(join);
   HF_CHECK_HIP(e, "hf_run");
   return HF_OK;
 }
