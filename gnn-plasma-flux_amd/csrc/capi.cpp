@@ -655,34 +655,38 @@ hipError_t run_steps(const hf_model *m, const float *state0, float *state_final,
 // Lanes of the generic hybrid rollout.  Its steps are a persistent flux kernel
 // that fills every CU (one workgroup each, LDS-bound) and then the short
 // FV/Poisson kernel; inside one stream the flux kernel's last round of windows
-// and the whole FV kernel leave most CUs idle.  With two lanes the two halves
-// of the batch step independently on the caller's stream and a second stream
-// (forked and joined with events), so one half's flux windows fill the CUs
-// the other half's tail and FV leave idle.  Every IC's arithmetic is the same
-// in either form.  HF_RUN_LANES=1 forces one lane (A/B timing).
-constexpr int64_t kLaneMinCells = 1 << 20;  // each half still fills the chip for several rounds
+// and the whole FV kernel leave most CUs idle.  With lanes, slices of the
+// batch step independently on the caller's stream and on lane streams (forked
+// and joined with events), so one slice's flux windows fill the CUs another
+// slice's tail and FV leave idle.  Every IC's arithmetic is the same in either
+// form.  HF_RUN_LANES=n (1..kMaxLanes) overrides the default (A/B timing).
+constexpr int kMaxLanes = 4;
+constexpr int kDefaultLanes = 3;  // profiles/r02_lanes_ab.json: 1 / 2 / 3 / 4 lanes = 1.141 / 1.129 / 1.119 / 1.118 ms per cfg4 step
+constexpr int64_t kLaneMinCells = 1 << 20;  // each slice still fills the chip for several rounds
 
 int run_lanes() {
   static const int lanes = [] {
     const char *v = std::getenv("HF_RUN_LANES");
-    return (v && std::atoi(v) == 1) ? 1 : 2;
+    const int n = v ? std::atoi(v) : kDefaultLanes;
+    return n < 1 ? 1 : n > kMaxLanes ? kMaxLanes : n;
   }();
   return lanes;
 }
 
-hipError_t lane_stream(hipStream_t *out) {
+// lane stream i (1..kMaxLanes-1) of the current device, created on first use
+hipError_t lane_stream(int i, hipStream_t *out) {
   static std::mutex mu;
-  static hipStream_t streams[64] = {};
+  static hipStream_t streams[64][kMaxLanes] = {};
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lock(mu);
-  if (!streams[dev]) {
-    e = hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking);
+  if (!streams[dev][i]) {
+    e = hipStreamCreateWithFlags(&streams[dev][i], hipStreamNonBlocking);
     if (e != hipSuccess) return e;
   }
-  *out = streams[dev];
+  *out = streams[dev][i];
   return hipSuccess;
 }
 
@@ -761,38 +765,38 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   float *buf0 = nullptr, *buf1 = nullptr;
   if (!traj) buf0 = sc.take(sbytes), buf1 = sc.take(sbytes);
   float *F = m ? sc.take(fbytes) : nullptr;
-  if (!m || B < 2 || (int64_t)B * nx < 2 * kLaneMinCells || run_lanes() == 1) {
+  int lanes = run_lanes();
+  while (lanes > 1 && (int64_t)B * nx < lanes * kLaneMinCells) --lanes;
+  if (!m || B < lanes) lanes = 1;
+  if (lanes == 1) {
     HF_CHECK_HIP(run_steps(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics, buf0,
                            buf1, F, s),
                  "hf_run");
     return HF_OK;
   }
-  // two lanes: ICs [0, B0) on the caller's stream, [B0, B) on the lane stream
-  const int B0 = B / 2;
-  const int64_t o = B0;
-  hipStream_t s2;
-  HF_CHECK_HIP(lane_stream(&s2), "hf_run lane stream");
-  hipEvent_t fork, join;
+  // lane i steps ICs [B*i/lanes, B*(i+1)/lanes); lane 0 on the caller's stream
+  hipStream_t ls[kMaxLanes] = {s};
+  for (int i = 1; i < lanes; ++i) HF_CHECK_HIP(lane_stream(i, &ls[i]), "hf_run lane stream");
+  hipEvent_t fork, join[kMaxLanes] = {};
   HF_CHECK_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "hf_run lane event");
-  hipError_t e = hipEventCreateWithFlags(&join, hipEventDisableTiming);
-  if (e != hipSuccess) {
-    (void)hipEventDestroy(fork);
-    return fail_hip(e, "hf_run lane event");
+  hipError_t e = hipEventRecord(fork, s);
+  for (int i = lanes - 1; i >= 0 && e == hipSuccess; --i) {
+    const int64_t o = (int64_t)B * i / lanes, n = (int64_t)B * (i + 1) / lanes - o;
+    if (i > 0) {
+      e = hipStreamWaitEvent(ls[i], fork, 0);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
+    }
+    if (e == hipSuccess)
+      e = run_steps(m, state0 + o * S, state_final + o * S, x, pc, (int)n, nx, T, c, dt, nu, dx2,
+                    traj ? traj + o * ldT : nullptr, flux_traj ? flux_traj + o * T * nx : nullptr,
+                    metrics ? metrics + o * ldM : nullptr, buf0 ? buf0 + o * S : nullptr,
+                    buf1 ? buf1 + o * S : nullptr, F + o * nx, ls[i]);
+    if (i > 0 && e == hipSuccess) e = hipEventRecord(join[i], ls[i]);
   }
-  e = hipEventRecord(fork, s);
-  if (e == hipSuccess) e = hipStreamWaitEvent(s2, fork, 0);
-  if (e == hipSuccess)
-    e = run_steps(m, state0 + o * S, state_final + o * S, x, pc, B - B0, nx, T, c, dt, nu, dx2,
-                  traj ? traj + o * ldT : nullptr, flux_traj ? flux_traj + o * T * nx : nullptr,
-                  metrics ? metrics + o * ldM : nullptr, buf0 ? buf0 + o * S : nullptr,
-                  buf1 ? buf1 + o * S : nullptr, F + o * nx, s2);
-  if (e == hipSuccess)
-    e = run_steps(m, state0, state_final, x, pc, B0, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics, buf0, buf1, F,
-                  s);
-  if (e == hipSuccess) e = hipEventRecord(join, s2);
-  if (e == hipSuccess) e = hipStreamWaitEvent(s, join, 0);
+  for (int i = 1; i < lanes && e == hipSuccess; ++i) e = hipStreamWaitEvent(s, join[i], 0);
   (void)hipEventDestroy(fork);
-  (void)hipEventDestroy(join);
+  for (int i = 1; i < lanes; ++i)
+    if (join[i]) (void)hipEventDestroy(join[i]);
   HF_CHECK_HIP(e, "hf_run");
   return HF_OK;
 }

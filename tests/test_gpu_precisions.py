@@ -261,7 +261,7 @@ def test_bf16_full_size_cfg4_properties(hf, record):
     assert torch.equal(a["final"], b["final"]) and torch.equal(a["metrics"], b["metrics"])
     sub = solver.run_batch(ics[:256], 30, traj=False, metrics=True)
     assert torch.equal(sub["final"], a["final"][:256]) and torch.equal(sub["metrics"], a["metrics"][:256])
-    # ICs 2048.. step on hf_run's second lane (capi.cpp run_lanes) in the full batch
+    # ICs 2048.. step on one of hf_run's lane streams (capi.cpp run_lanes) in the full batch
     sub = solver.run_batch(ics[2048:2304], 30, traj=False, metrics=True)
     assert torch.equal(sub["final"], a["final"][2048:2304]) and torch.equal(sub["metrics"], a["metrics"][2048:2304])
     assert bool(torch.isfinite(a["final"]).all()) and bool((a["metrics"][..., 2] == 1).all())

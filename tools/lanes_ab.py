@@ -29,7 +29,7 @@ def main():
     dev = torch.device("cuda", 0)
     w = os.path.join(ROOT, "tests", "golden", "weights_W1_r2.npz")
     res = {"lanes": os.environ.get("HF_RUN_LANES", "default")}
-    for prec in ("bf16", "f32", "f16x3"):
+    for prec in os.environ.get("LANES_AB_PREC", "bf16,f32,f16x3").split(","):
         solver = HybridSolver(w, radius=2, nx=nx, dt=dt, device=dev, precision=prec)
         ics = solver.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True)
         ws, _ = engine.workspace(HF_OP_RUN, B, nx, T, dev)
