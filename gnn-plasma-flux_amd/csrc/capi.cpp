@@ -768,6 +768,11 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   int lanes = run_lanes();
   while (lanes > 1 && (int64_t)B * nx < lanes * kLaneMinCells) --lanes;
   if (!m || B < lanes) lanes = 1;
+  if (lanes > 1 && s) {  // lane streams live on the current device: a stream of another device runs one lane
+    int cur = 0;
+    hipDevice_t sdev = 0;
+    if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice(s, &sdev) != hipSuccess || sdev != cur) lanes = 1;
+  }
   if (lanes == 1) {
     HF_CHECK_HIP(run_steps(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics, buf0,
                            buf1, F, s),
