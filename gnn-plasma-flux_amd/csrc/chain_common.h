@@ -200,10 +200,19 @@ __device__ __forceinline__ Small stage_small(const ChainW &W, float *s) {
 // arithmetic a mask).
 // DEFER: next() only waits and barriers; the DMA it owes (chunk pos+D into the
 // slot just released) is issued by issue_pending() at a point the core picks.
-template <int CF, int NW = kWaves, int SLOTS = kRingSlots, int D = 2, bool DEFER = false>
+// LOADER: the NW waves only consume; one extra wave of the workgroup (wave NW)
+// issues every piece of every chunk (loader_prime / loader_next), so the
+// compute waves' instruction streams carry no DMA issue (~60 cycles per 1 KiB
+// piece beside the MFMAs, MI355X_MICROARCH.md).  A consumer's next() is then
+// only its LDS wait + the barrier; the loader waits for its own DMA of the
+// chunk before the same barrier.
+template <int CF, int NW = kWaves, int SLOTS = kRingSlots, int D = 2, bool DEFER = false, bool LOADER = false>
 struct Ring {
   static_assert(SLOTS >= D + 1 && D >= 2 && D <= 6, "ring slots / prefetch distance");
+  static_assert(!(LOADER && DEFER), "a loader ring issues at its own barrier");
+  static constexpr bool kLoader = LOADER;
   static constexpr int kPerWave = CF / (NW * 256);  // 1 KiB DMA instructions per wave per chunk
+  static constexpr int kPieces = CF / 256;          // 1 KiB DMA instructions per chunk (the loader's share)
   static_assert(kPerWave == 1 || kPerWave == 2 || kPerWave == 4, "ring chunk split over the waves");
   __amdgpu_buffer_rsrc_t rsrc;  // packed weight stream (global)
   int lane_off;                 // lane * 16 bytes (the only per-lane address term)
@@ -221,11 +230,11 @@ struct Ring {
   // ring's own counted vmcnt + barrier in next() order the DMA for readers.
   // buffer_load ... lds: the chunk offset is an SGPR (soffset), the lane
   // offset a fixed VGPR, so an issue costs no VALU address arithmetic.
-  __device__ __forceinline__ void issue(int chunk, int slot, int j0 = 0, int j1 = kPerWave) const {
+  __device__ __forceinline__ void issue(int chunk, int slot, int j0 = 0, int j1 = kPerWave, bool all = false) const {
     const unsigned d = (unsigned)(uintptr_t)(lds_void *)(lds + slot * CF);
 #pragma unroll
     for (int jj = j0; jj < j1; ++jj) {
-      const int j = kPerWave * wave + jj;  // this wave's share of the chunk
+      const int j = all ? jj : kPerWave * wave + jj;  // this wave's share of the chunk (the loader: all of it)
       const unsigned dst = __builtin_amdgcn_readfirstlane(d + j * 1024);
       const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(chunk * CF + j * 256) * 4u);
       unsigned keep;
@@ -241,9 +250,38 @@ struct Ring {
   __device__ __forceinline__ void prime(int first = 0) {
     pos = 0;
     rd = 0;
+    if constexpr (!LOADER) {
 #pragma unroll
-    for (int i = 0; i < D; ++i) issue((first + i) % chunks, i);
+      for (int i = 0; i < D; ++i) issue((first + i) % chunks, i);
+    }
     ahead = (first + D) % chunks;
+  }
+  // LOADER: the loader wave's counterparts of prime() and next(), one call per
+  // consumer call, in the same order (and one lds_barrier() per consumer
+  // barrier outside the ring).
+  __device__ __forceinline__ void loader_prime(int first = 0) {
+    static_assert(LOADER, "loader ring only");
+    pos = 0;
+    rd = 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) issue((first + i) % chunks, i, 0, kPieces, true);
+    ahead = (first + D) % chunks;
+  }
+  __device__ __forceinline__ void loader_next() {
+    static_assert(LOADER, "loader ring only");
+    constexpr int kVm = kPieces * (D - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (kVm == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 24) asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 32) asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 40) asm volatile("s_waitcnt vmcnt(40)\n\ts_barrier" ::: "memory");
+    else static_assert(kVm == 8, "vmcnt of the loader ring");
+    __builtin_amdgcn_sched_barrier(0);
+    issue(ahead, rd + D >= SLOTS ? rd + D - SLOTS : rd + D, 0, kPieces, true);
+    ahead = ahead + 1 == chunks ? 0 : ahead + 1;
+    rd = rd + 1 == SLOTS ? 0 : rd + 1;
+    ++pos;
   }
   // Wait for chunk `pos`, keep D chunks in flight, return its slot.
   __device__ __forceinline__ const float *next() {
@@ -260,7 +298,8 @@ struct Ring {
     asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
 #else
     constexpr int kVm = kPerWave * (D - 1);
-    if constexpr (kVm == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (LOADER) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (kVm == 1) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else if constexpr (kVm == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else if constexpr (kVm == 3) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else if constexpr (kVm == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -276,7 +315,8 @@ struct Ring {
 #endif
     __builtin_amdgcn_sched_barrier(0);
 #if !defined(HF_DIAG_NODMA) && !defined(HF_DIAG_NOSYNC)  // timing diagnostics only
-    if constexpr (DEFER) {
+    if constexpr (LOADER) {
+    } else if constexpr (DEFER) {
       pend_chunk = ahead;
       pend_slot = rd + D >= SLOTS ? rd + D - SLOTS : rd + D;
     } else {
@@ -672,8 +712,14 @@ constexpr int cells_lds_floats() {
   return CC::kSlots * CC::kChunkFloats + kSmallFloats + kWaves * kWaveScratchFloats + 4 * (kXhF4 + kXqF4);
 }
 
+// threads of a cell-split rollout workgroup: 4 compute waves (+ the loader wave)
+template <class CC>
+constexpr int cells_threads() {
+  return 64 * (kWaves + (CC::R_t::kLoader ? 1 : 0));
+}
+
 template <class CC, int WPI>
-__global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
+__global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_kernel(
     ChainW W, const float *state0, float *state_final,  // may alias (read whole before written)
     const float *__restrict__ x,
     const double *__restrict__ pc, int B, int T, float c, float dt, float *__restrict__ traj,
@@ -686,10 +732,13 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
   const Small S = stage_small(W, lds + kRingFloats);
   auto R = make_ring<CC>(W, lds);
   const int wave = R.wave, lane = R.lane, j = lane & 15, g = lane >> 4;
-  const bool shadow = wave >= IPW * WPI;
+  constexpr bool kLd = CC::R_t::kLoader;
+  const bool shadow = wave >= IPW * WPI;     // (the loader wave, wave kWaves, too)
   const int slot = shadow ? 0 : wave / WPI;  // IC of this wave within the workgroup
   const int pos = shadow ? 0 : wave % WPI;   // cells 16*pos .. 16*pos + 15 of it
-  const bool lead = !shadow && pos == 0;
+  // the lead (FV + Poisson + outputs) is the IC's wave 1 beside a loader
+  // wave: the loader shares SIMD 0 with wave 0
+  const bool lead = !shadow && pos == (kLd ? 1 : 0);
   CellHalo X;
   X.xh = reinterpret_cast<f4 *>(lds + kRingFloats + kSmallFloats + kWaves * kWaveScratchFloats);
   X.xq = X.xh + kXhF4;
@@ -715,6 +764,20 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_cells_kernel(
     }
   }
   __syncthreads();  // small weights + IC state visible (no DMA in flight yet)
+  if constexpr (kLd) {
+    if (wave == kWaves) {  // the loader: the compute waves' ring barriers and step barriers, in order
+      R.loader_prime();
+      R.loader_next();  // CC::begin
+      for (int t = 0; t < T; ++t) {
+        for (int k = 0; k < R.chunks; ++k) R.loader_next();  // one forward pass
+        lds_barrier();  // readout_cells' last tile
+        lds_barrier();  // face fluxes
+        lds_barrier();  // new state
+      }
+      R.drain();
+      return;
+    }
+  }
   const bool out = lead && live;
   float *tj = (traj && out) ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
   float *mt_out = (metrics && out) ? metrics + b * (int64_t)(T + 1) * HF_NUM_METRICS : nullptr;
@@ -831,7 +894,7 @@ hipError_t cells_launch(const ChainW &w, const float *state0, float *state_final
                         int B, int T, float c, float dt, float *traj, float *flux_traj, float *metrics,
                         hipStream_t s) {
   constexpr int IPW = kWaves / WPI;
-  hipLaunchKernelGGL((chain_rollout_cells_kernel<CC, WPI>), dim3((B + IPW - 1) / IPW), dim3(64 * kWaves), 0, s, w,
+  hipLaunchKernelGGL((chain_rollout_cells_kernel<CC, WPI>), dim3((B + IPW - 1) / IPW), dim3(cells_threads<CC>()), 0, s, w,
                      state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics);
   return hipGetLastError();
 }

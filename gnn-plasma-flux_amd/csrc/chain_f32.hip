@@ -25,7 +25,7 @@ using namespace chain;
 // (chain_common.h Ring): 2 in 4 for the IC-per-wave kernels; the cell-split
 // kernels consume a chunk in a quarter of the time (16 cells per wave) and run
 // deeper (kCellsAhead).
-template <int D = 2, int SLOTS = kRingSlots>
+template <int D = 2, int SLOTS = kRingSlots, bool LDR = false>
 struct CoreF32T {
   static constexpr int kNW = kWaves;   // waves sharing the weight ring
   static constexpr int kWGPerCU = 1;   // persistent flux kernel: workgroups per CU
@@ -38,7 +38,7 @@ struct CoreF32T {
   static constexpr int kUPC = 4;
   static constexpr int kChunkFloats = 512 * kUPC;  // 4 units of 2 KiB (2 ds_read_b128 per lane)
   static constexpr int kParkFloats = 0;
-  using R_t = Ring<kChunkFloats, kNW, kSlots, kAhead>;
+  using R_t = Ring<kChunkFloats, kNW, kSlots, kAhead, false, LDR>;  // LDR: a loader wave issues the ring DMA
 
   // Register-prefetched weight feed.  A chunk is 4 units; unit u is the lane's
   // fragments 2u, 2u+1 and feeds 32 MFMAs (one update k-step, or four readout
@@ -343,6 +343,13 @@ using CoreF32 = CoreF32T<>;
 #endif
 constexpr int kCellsAhead = HF_CELLS_AHEAD;
 using CellCore = CoreF32T<kCellsAhead, kCellsAhead + 1>;
+// The cell-split rollout's core: a fifth (loader) wave issues the weight
+// ring's DMA, so the four compute waves carry none (chain_common.h Ring
+// LOADER).  HF_CELLS_LOADER=0 builds the four-wave form (A/B).
+#ifndef HF_CELLS_LOADER
+#define HF_CELLS_LOADER 1
+#endif
+using CellRollCore = CoreF32T<kCellsAhead, kCellsAhead + 1, HF_CELLS_LOADER != 0>;
 }  // namespace
 
 // Whether the cell-split kernel beats the IC-per-wave kernel for B ICs of nx
@@ -362,9 +369,9 @@ hipError_t launch_chain_rollout_cells(const ChainW &w, const float *state0, floa
                                       float *flux_traj, float *metrics, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (nx) {
-    case 32: return cells_launch<CellCore, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 48: return cells_launch<CellCore, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 64: return cells_launch<CellCore, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 32: return cells_launch<CellRollCore, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 48: return cells_launch<CellRollCore, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 64: return cells_launch<CellRollCore, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
     default: return hipErrorInvalidValue;
   }
 }
