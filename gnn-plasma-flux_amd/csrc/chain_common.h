@@ -733,6 +733,12 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
   auto R = make_ring<CC>(W, lds);
   const int wave = R.wave, lane = R.lane, j = lane & 15, g = lane >> 4;
   constexpr bool kLd = CC::R_t::kLoader;
+#ifndef HF_LDR_EMIT
+#define HF_LDR_EMIT 0
+#endif
+  // HF_LDR_EMIT=1: the loader wave writes the per-step outputs instead of the
+  // lead (measured equal on cfg2, profiles/r02_cfg2_loader_ab.json)
+  constexpr bool kLdEmit = kLd && HF_LDR_EMIT;
   const bool shadow = wave >= IPW * WPI;     // (the loader wave, wave kWaves, too)
   const int slot = shadow ? 0 : wave / WPI;  // IC of this wave within the workgroup
   const int pos = shadow ? 0 : wave % WPI;   // cells 16*pos .. 16*pos + 15 of it
@@ -764,36 +770,51 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
     }
   }
   __syncthreads();  // small weights + IC state visible (no DMA in flight yet)
+  // outputs of state t of IC slot sl: trajectory row and metrics
+  auto emit = [&](int sl, int t) {
+    const int64_t bs = (int64_t)blockIdx.x * IPW + sl;
+    if (bs >= B) return;
+    const float *st = lds + kRingFloats + kSmallFloats + sl * kWaveScratchFloats;
+    if (traj) {
+      float *tj = traj + bs * (int64_t)(T + 1) * 3 * NX + (int64_t)t * 3 * NX;
+      for (int i = lane; i < 3 * NX; i += 64) tj[i] = st[(i / NX) * 64 + i % NX];
+    }
+    if (metrics) {
+      MetricAcc m;
+      m.init();
+      if (lane < NX) m.add(st[lane], st[64 + lane], st[128 + lane]);
+      m.wave_reduce();
+      if (lane == 0) m.store(metrics + bs * (int64_t)(T + 1) * HF_NUM_METRICS + t * HF_NUM_METRICS, NX);
+    }
+  };
   if constexpr (kLd) {
     if (wave == kWaves) {  // the loader: the compute waves' ring barriers and step barriers, in order
+#ifdef HF_LDR_PRIO  // A/B: the loader's wave priority
+      __builtin_amdgcn_s_setprio(HF_LDR_PRIO);
+#endif
       R.loader_prime();
       R.loader_next();  // CC::begin
       for (int t = 0; t < T; ++t) {
-        for (int k = 0; k < R.chunks; ++k) R.loader_next();  // one forward pass
+        for (int k = 0; k < R.chunks; ++k) {  // one forward pass
+          R.loader_next();
+          // state t is in LDS from the end of step t-1 to this step's FV
+          // (after the second barrier below): its outputs, off the lead's path
+          if (kLdEmit && k == 0)
+            for (int sl = 0; sl < IPW; ++sl) emit(sl, t);
+        }
         lds_barrier();  // readout_cells' last tile
         lds_barrier();  // face fluxes
         lds_barrier();  // new state
       }
+      if (kLdEmit)
+        for (int sl = 0; sl < IPW; ++sl) emit(sl, T);
       R.drain();
       return;
     }
   }
   const bool out = lead && live;
-  float *tj = (traj && out) ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
-  float *mt_out = (metrics && out) ? metrics + b * (int64_t)(T + 1) * HF_NUM_METRICS : nullptr;
   float *ftj = (flux_traj && out) ? flux_traj + b * (int64_t)T * NX : nullptr;
-  auto emit = [&](int t) {  // lead wave
-    if (tj)
-      for (int i = lane; i < 3 * NX; i += 64) tj[(int64_t)t * 3 * NX + i] = s_st[(i / NX) * 64 + i % NX];
-    if (mt_out) {
-      MetricAcc m;
-      m.init();
-      if (lane < NX) m.add(s_st[lane], s_st[64 + lane], s_st[128 + lane]);
-      m.wave_reduce();
-      if (lane == 0) m.store(mt_out + t * HF_NUM_METRICS, NX);
-    }
-  };
-  if (lead) emit(0);
+  if (!kLdEmit && lead) emit(slot, 0);
   R.prime();
   typename CC::Feed F;
   CC::begin(R, F);
@@ -827,8 +848,9 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
     }
     lds_barrier();  // new state visible to every wave
     // the lead's outputs of the new state overlap the other waves' next
-    // forward (nothing writes the state again before this step's FV)
-    if (lead) emit(t + 1);
+    // forward (nothing writes the state again before this step's FV); with a
+    // loader wave, the loader writes them
+    if (!kLdEmit && lead) emit(slot, t + 1);
   }
   R.drain();
   if (!out) return;
