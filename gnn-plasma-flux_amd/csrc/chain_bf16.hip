@@ -87,7 +87,7 @@ __device__ __forceinline__ void interleave() {
 // first two units after the pass, kBF16StreamTail), so the barrier falls
 // between unit 1's fragment reads and its MFMAs, after the seam publish in unit 0.
 template <int NW, int UPC, int WMT = 4, bool PF = false, int SLOTS = (UPC == 4 ? 3 : 4), int WG = 1, int DMAU = 0,
-          bool XCH = false>
+          bool XCH = false, bool LDR = false>
 struct CoreBF16 {
   static_assert(!XCH || (UPC == 4 && !PF && WMT == 4), "super-window core: 16 KiB chunks, 64-cell waves");
   static constexpr int kNW = NW;
@@ -110,7 +110,7 @@ struct CoreBF16 {
   // cfg4 3-5 % less time at DMAU = 0 (unit 3: 2-3 %, units 1-2: 2 %; spreading
   // the DMA over the units by wave number: 10 % more), tools/gpu_diag_cfg4.sh.
   static constexpr int kDmaUnit = DMAU;
-  using R_t = Ring<kChunkFloats, NW, kSlots, 2, (DMAU >= 0)>;
+  using R_t = Ring<kChunkFloats, NW, kSlots, 2, (DMAU >= 0), LDR>;  // LDR: a loader wave issues the ring DMA
   // ring position of pair-unit U (of readout unit U: the same, counted from the readout's start)
   static constexpr int pos(int U) { return XCH ? (U + 2) & 3 : U % UPC; }
 
@@ -821,16 +821,21 @@ hipError_t launch_flux_sw(const ChainW &w, const float *nf, const float *state, 
 // barrier (CellHalo::exchange), then the epilogue; the readout trades column 0
 // of P and Q the same way (CellHalo::xq).  It shares the weight ring of the
 // bf16 rollout kernel (8 KiB chunks, 4 slots, fragments read a unit ahead).
-struct CellBF16 {
-  using Base = CoreBF16<4, 2, 4, true, 4, 1, -1>;
+template <bool LDR = false>
+struct CellBF16T {
+  using Base = CoreBF16<4, 2, 4, true, 4, 1, -1, false, LDR>;
+  // barrier schedule of one pass (the loader wave's, chain_rollout_cells_kernel):
+  // 8 ring chunks per update layer, then the G trade's barrier
+  static constexpr int kLayerChunks = 8;
+  static constexpr bool kLayerBarrier = true;
   static constexpr int kNW = Base::kNW;
   static constexpr int kSlots = Base::kSlots;
   static constexpr int kChunkFloats = Base::kChunkFloats;
   static constexpr int kStreamOffset = 0;
-  using R_t = Base::R_t;
-  using Feed = Base::Feed;
-  using Acts = Base::Acts<1>;
-  using Pair = Base::Pair<1>;
+  using R_t = typename Base::R_t;
+  using Feed = typename Base::Feed;
+  using Acts = typename Base::template Acts<1>;
+  using Pair = typename Base::template Pair<1>;
   static __device__ __forceinline__ void begin(R_t &R, Feed &F) { Base::begin(R, F); }
 
   static __device__ __forceinline__ void gnn_cells(const ChainW &W, const Small &S, R_t &R, Feed &F,
@@ -840,7 +845,7 @@ struct CellBF16 {
     Acts A;
     {
       f4 h67[1][2];
-      Base::input<1>(S, lane, feat, A, h67);
+      Base::template input<1>(S, lane, feat, A, h67);
     }
     // message passing (src/flux_gnn.py:53-60)
     for (int l = 0; l < W.layers; ++l) {
@@ -848,14 +853,14 @@ struct CellBF16 {
       Pair acc[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        Base::init<1>(bias, q, g4, acc[q]);
-        Base::unit<1, 0>(R, F, A, acc[q]);
+        Base::template init<1>(bias, q, g4, acc[q]);
+        Base::template unit<1, 0>(R, F, A, acc[q]);
         interleave<4, 0>();
-        Base::unit<1, 1>(R, F, A, acc[q]);
+        Base::template unit<1, 1>(R, F, A, acc[q]);
         interleave<4, 0>();
-        Base::unit<1, 2>(R, F, A, acc[q]);
+        Base::template unit<1, 2>(R, F, A, acc[q]);
         interleave<4, 0>();
-        Base::unit<1, 3>(R, F, A, acc[q]);
+        Base::template unit<1, 3>(R, F, A, acc[q]);
         interleave<4, 0>();
       }
       {
@@ -889,10 +894,10 @@ struct CellBF16 {
     f4 P[kNT][1], Q[kNT][1];
 #pragma unroll
     for (int ot = 0; ot < kNT; ++ot) {
-      Base::init_ro<1>(S, ot, g4, P[ot], Q[ot]);
-      Base::ro_unit<1, 0, 0>(R, F, A, P[ot], Q[ot]);
+      Base::template init_ro<1>(S, ot, g4, P[ot], Q[ot]);
+      Base::template ro_unit<1, 0, 0>(R, F, A, P[ot], Q[ot]);
       interleave<4, 0>();
-      Base::ro_unit<1, 1, 1>(R, F, A, P[ot], Q[ot]);
+      Base::template ro_unit<1, 1, 1>(R, F, A, P[ot], Q[ot]);
       interleave<4, 0>();
       if (j == 0) {
         X.xq[((X.wave * kNT + ot) * 2 + 0) * 4 + g] = P[ot][0];
@@ -918,6 +923,11 @@ struct CellBF16 {
     readout_finish<1>(pf1, pb1, W.b2, ffwd, fbwd);
   }
 };
+using CellBF16 = CellBF16T<>;
+#ifndef HF_CELLS_LOADER
+#define HF_CELLS_LOADER 1
+#endif
+using CellBF16Roll = CellBF16T<HF_CELLS_LOADER != 0>;  // the rollout's: with a loader wave
 
 }  // namespace
 
@@ -949,9 +959,9 @@ hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float
   // small batches: each IC over nx/16 waves (cell-split kernel, same bits)
   if (ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx)) {
     switch (nx) {
-      case 32: return chain::cells_launch<CellBF16, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 48: return chain::cells_launch<CellBF16, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 64: return chain::cells_launch<CellBF16, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 32: return chain::cells_launch<CellBF16Roll, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 48: return chain::cells_launch<CellBF16Roll, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 64: return chain::cells_launch<CellBF16Roll, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
       default: break;
     }
   }

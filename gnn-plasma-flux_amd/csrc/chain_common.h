@@ -794,15 +794,20 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
 #endif
       R.loader_prime();
       R.loader_next();  // CC::begin
-      for (int t = 0; t < T; ++t) {
-        for (int k = 0; k < R.chunks; ++k) {  // one forward pass
-          R.loader_next();
-          // state t is in LDS from the end of step t-1 to this step's FV
-          // (after the second barrier below): its outputs, off the lead's path
-          if (kLdEmit && k == 0)
-            for (int sl = 0; sl < IPW; ++sl) emit(sl, t);
+      const int ro_chunks = R.chunks - W.layers * CC::kLayerChunks;
+      for (int t = 0; t < T; ++t) {  // one forward pass: update layers, then the readout
+        for (int l = 0; l < W.layers; ++l) {
+          for (int k = 0; k < CC::kLayerChunks; ++k) {
+            R.loader_next();
+            // state t is in LDS from the end of step t-1 to this step's FV
+            // (after the second step barrier below): its outputs, off the lead's path
+            if (kLdEmit && l == 0 && k == 0)
+              for (int sl = 0; sl < IPW; ++sl) emit(sl, t);
+          }
+          if constexpr (CC::kLayerBarrier) lds_barrier();  // the layer's halo trade (CellHalo::exchange)
         }
-        lds_barrier();  // readout_cells' last tile
+        for (int k = 0; k < ro_chunks; ++k) R.loader_next();
+        lds_barrier();  // the readout's column-0 trade
         lds_barrier();  // face fluxes
         lds_barrier();  // new state
       }

@@ -38,6 +38,10 @@ struct CoreF32T {
   static constexpr int kUPC = 4;
   static constexpr int kChunkFloats = 512 * kUPC;  // 4 units of 2 KiB (2 ds_read_b128 per lane)
   static constexpr int kParkFloats = 0;
+  // barrier schedule of one cell-split pass (the loader wave's,
+  // chain_rollout_cells_kernel): 16 ring chunks per update layer, no other barrier
+  static constexpr int kLayerChunks = 16;
+  static constexpr bool kLayerBarrier = false;
   using R_t = Ring<kChunkFloats, kNW, kSlots, kAhead, false, LDR>;  // LDR: a loader wave issues the ring DMA
 
   // Register-prefetched weight feed.  A chunk is 4 units; unit u is the lane's

@@ -80,7 +80,7 @@ __device__ __forceinline__ void interleave() {
 
 // UPC = units (4 split fragments, 8 KiB) per ring chunk: 1 (8 KiB chunks,
 // 4 slots: fits beside the rollout's per-IC scratch) or 2 (16 KiB, 3 slots).
-template <int UPC>
+template <int UPC, bool LDR = false>
 struct CoreF16x3T {
   static constexpr int kNW = kWaves;
   static constexpr int kWGPerCU = 1;
@@ -93,7 +93,7 @@ struct CoreF16x3T {
   static constexpr int kKB = kH / 32;
   // parked fragments of k-blocks 0..2: [kb 3][mt 4][term 2][lane 64][4 dwords]
   static constexpr int kParkFloats = 3 * 4 * 2 * 64 * 4;
-  using R_t = Ring<kChunkFloats, kNW, kSlots>;
+  using R_t = Ring<kChunkFloats, kNW, kSlots, 2, false, LDR>;  // LDR: a loader wave issues the ring DMA
 
   template <int MT>
   struct Acts {
@@ -431,21 +431,26 @@ struct CoreF16x3T {
 // selects), laid out like chain_bf16.hip's CellBF16: a layer's four output
 // pairs, then the G values of the edge columns traded through LDS around one
 // barrier, then the epilogue; the readout trades column 0 of P and Q.
-struct CellF16x3 {
-  using Base = CoreF16x3T<1>;  // the rollout's ring: 8 KiB chunks (one unit), 4 slots
+template <bool LDR = false>
+struct CellF16x3T {
+  using Base = CoreF16x3T<1, LDR>;  // the rollout's ring: 8 KiB chunks (one unit), 4 slots
+  // barrier schedule of one pass (the loader wave's, chain_rollout_cells_kernel):
+  // 16 ring chunks per update layer, then the G trade's barrier
+  static constexpr int kLayerChunks = 16;
+  static constexpr bool kLayerBarrier = true;
   static constexpr int kNW = Base::kNW;
   static constexpr int kSlots = Base::kSlots;
   static constexpr int kChunkFloats = Base::kChunkFloats;
   static constexpr int kStreamOffset = 0;
-  using R_t = Base::R_t;
-  using Feed = Base::Feed;
+  using R_t = typename Base::R_t;
+  using Feed = typename Base::Feed;
   static __device__ __forceinline__ void begin(R_t &R, Feed &F) { Base::begin(R, F); }
 
   static __device__ __forceinline__ void gnn_cells(const ChainW &W, const Small &S, R_t &R, Feed &F,
                                                    const float (&feat)[1], float (&ffwd)[1], float (&fbwd)[1],
                                                    CellHalo &X) {
     const int lane = R.lane, g4 = 4 * (lane >> 4), g = lane >> 4, j = lane & 15;
-    Base::Acts<1> A;
+    typename Base::template Acts<1> A;
     {
       f4 h[1][kNT];
       input_layer<1>(S, lane, feat, h);  // f32 MFMA, ReLU applied
@@ -462,17 +467,17 @@ struct CellF16x3 {
     // message passing (src/flux_gnn.py:53-60)
     for (int l = 0; l < W.layers; ++l) {
       const float *bias = S.bl + l * kH;
-      Base::PairAcc<1> acc[4];
+      typename Base::template PairAcc<1> acc[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        Base::init_pair<1>(bias, q, g4, acc[q]);
-        Base::unit<1, 0, 0>(R, F, A, acc[q]);
+        Base::template init_pair<1>(bias, q, g4, acc[q]);
+        Base::template unit<1, 0, 0>(R, F, A, acc[q]);
         interleave<12, 0>();
-        Base::unit<1, 1, 0>(R, F, A, acc[q]);
+        Base::template unit<1, 1, 0>(R, F, A, acc[q]);
         interleave<12, 0>();
-        Base::unit<1, 2, 0>(R, F, A, acc[q]);
+        Base::template unit<1, 2, 0>(R, F, A, acc[q]);
         interleave<12, 0>();
-        Base::unit<1, 3, 0>(R, F, A, acc[q]);
+        Base::template unit<1, 3, 0>(R, F, A, acc[q]);
         interleave<12, 0>();
       }
       {
@@ -505,10 +510,10 @@ struct CellF16x3 {
     f4 P[kNT][1], Q[kNT][1];
 #pragma unroll
     for (int ot = 0; ot < kNT; ++ot) {
-      Base::init_ro<1>(S, ot, g4, P[ot], Q[ot]);
-      Base::ro_unit<1, 0, 0>(R, F, A, P[ot], Q[ot]);
+      Base::template init_ro<1>(S, ot, g4, P[ot], Q[ot]);
+      Base::template ro_unit<1, 0, 0>(R, F, A, P[ot], Q[ot]);
       interleave<12, 0>();
-      Base::ro_unit<1, 1, 0>(R, F, A, P[ot], Q[ot]);
+      Base::template ro_unit<1, 1, 0>(R, F, A, P[ot], Q[ot]);
       interleave<12, 0>();
       if (j == 0) {
         X.xq[((X.wave * kNT + ot) * 2 + 0) * 4 + g] = P[ot][0];
@@ -531,6 +536,11 @@ struct CellF16x3 {
     readout_finish<1>(pf1, pb1, W.b2, ffwd, fbwd);
   }
 };
+using CellF16x3 = CellF16x3T<>;
+#ifndef HF_CELLS_LOADER
+#define HF_CELLS_LOADER 1
+#endif
+using CellF16x3Roll = CellF16x3T<HF_CELLS_LOADER != 0>;  // the rollout's: with a loader wave
 
 }  // namespace
 
@@ -555,9 +565,9 @@ hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float 
                                     float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
   if (w.prec == kPrecF16x3 && ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx)) {
     switch (nx) {  // small batches: each IC over nx/16 waves (cell-split kernel, same bits)
-      case 32: return chain::cells_launch<CellF16x3, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 48: return chain::cells_launch<CellF16x3, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 64: return chain::cells_launch<CellF16x3, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 32: return chain::cells_launch<CellF16x3Roll, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 48: return chain::cells_launch<CellF16x3Roll, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 64: return chain::cells_launch<CellF16x3Roll, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
       default: break;
     }
   }
