@@ -923,11 +923,10 @@ struct CellBF16T {
     readout_finish<1>(pf1, pb1, W.b2, ffwd, fbwd);
   }
 };
-using CellBF16 = CellBF16T<>;
 #ifndef HF_CELLS_LOADER
 #define HF_CELLS_LOADER 1
 #endif
-using CellBF16Roll = CellBF16T<HF_CELLS_LOADER != 0>;  // the rollout's: with a loader wave
+using CellBF16Ld = CellBF16T<HF_CELLS_LOADER != 0>;  // with a loader wave (the cell-split kernels)
 
 }  // namespace
 
@@ -938,9 +937,9 @@ hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float 
   if (B <= 0) return hipSuccess;
   if (chain_rollout_prefers_cells(w, B, nx)) {  // small batches: each chain over nx/16 waves
     switch (nx) {
-      case 32: return chain::flux_cells_launch<CellBF16, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
-      case 48: return chain::flux_cells_launch<CellBF16, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
-      case 64: return chain::flux_cells_launch<CellBF16, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 32: return chain::flux_cells_launch<CellBF16Ld, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 48: return chain::flux_cells_launch<CellBF16Ld, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 64: return chain::flux_cells_launch<CellBF16Ld, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
       default: break;
     }
   }
@@ -959,9 +958,9 @@ hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float
   // small batches: each IC over nx/16 waves (cell-split kernel, same bits)
   if (ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx)) {
     switch (nx) {
-      case 32: return chain::cells_launch<CellBF16Roll, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 48: return chain::cells_launch<CellBF16Roll, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 64: return chain::cells_launch<CellBF16Roll, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 32: return chain::cells_launch<CellBF16Ld, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 48: return chain::cells_launch<CellBF16Ld, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 64: return chain::cells_launch<CellBF16Ld, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
       default: break;
     }
   }

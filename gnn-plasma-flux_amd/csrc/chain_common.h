@@ -866,7 +866,7 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
 // FluxGNN.forward on B chains of 16*WPI cells, cell-split as above (the
 // small-batch counterpart of chain_flux_kernel<CoreF32, MT, true>, bit-identical to it).
 template <class CC, int WPI>
-__global__ __launch_bounds__(256, 1) void chain_flux_cells_kernel(ChainW W, const float *__restrict__ nf,
+__global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_flux_cells_kernel(ChainW W, const float *__restrict__ nf,
                                                                   const float *__restrict__ state, int64_t ld_state,
                                                                   const float *__restrict__ x, int B,
                                                                   float *__restrict__ fe, float *__restrict__ ff) {
@@ -895,6 +895,20 @@ __global__ __launch_bounds__(256, 1) void chain_flux_cells_kernel(ChainW W, cons
   const float feat[1] = {nf ? nf[(b * NX + cell) * kIn + g]
                             : (g < 3 ? state[b * ld_state + (int64_t)g * NX + cell] : x[cell])};
   __syncthreads();  // small weights staged (no DMA in flight yet)
+  if constexpr (CC::R_t::kLoader) {
+    if (wave == kWaves) {  // the loader (chain_rollout_cells_kernel): one pass's barriers, in order
+      R.loader_prime();
+      R.loader_next();  // CC::begin
+      for (int l = 0; l < W.layers; ++l) {
+        for (int k = 0; k < CC::kLayerChunks; ++k) R.loader_next();
+        if constexpr (CC::kLayerBarrier) lds_barrier();
+      }
+      for (int k = R.chunks - W.layers * CC::kLayerChunks; k > 0; --k) R.loader_next();
+      lds_barrier();  // the readout's column-0 trade
+      R.drain();
+      return;
+    }
+  }
   R.prime();
   typename CC::Feed F;
   CC::begin(R, F);
@@ -911,7 +925,7 @@ template <class CC, int WPI>
 hipError_t flux_cells_launch(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
                              int B, float *fe, float *ff, hipStream_t s) {
   constexpr int IPW = kWaves / WPI;
-  hipLaunchKernelGGL((chain_flux_cells_kernel<CC, WPI>), dim3((B + IPW - 1) / IPW), dim3(64 * kWaves), 0, s, w, nf,
+  hipLaunchKernelGGL((chain_flux_cells_kernel<CC, WPI>), dim3((B + IPW - 1) / IPW), dim3(cells_threads<CC>()), 0, s, w, nf,
                      state, ld_state, x, B, fe, ff);
   return hipGetLastError();
 }

@@ -346,14 +346,13 @@ using CoreF32 = CoreF32T<>;
 #define HF_CELLS_AHEAD 4
 #endif
 constexpr int kCellsAhead = HF_CELLS_AHEAD;
-using CellCore = CoreF32T<kCellsAhead, kCellsAhead + 1>;
-// The cell-split rollout's core: a fifth (loader) wave issues the weight
+// The cell-split kernels' core: a fifth (loader) wave issues the weight
 // ring's DMA, so the four compute waves carry none (chain_common.h Ring
 // LOADER).  HF_CELLS_LOADER=0 builds the four-wave form (A/B).
 #ifndef HF_CELLS_LOADER
 #define HF_CELLS_LOADER 1
 #endif
-using CellRollCore = CoreF32T<kCellsAhead, kCellsAhead + 1, HF_CELLS_LOADER != 0>;
+using CellCoreLd = CoreF32T<kCellsAhead, kCellsAhead + 1, HF_CELLS_LOADER != 0>;
 }  // namespace
 
 // Whether the cell-split kernel beats the IC-per-wave kernel for B ICs of nx
@@ -373,9 +372,9 @@ hipError_t launch_chain_rollout_cells(const ChainW &w, const float *state0, floa
                                       float *flux_traj, float *metrics, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (nx) {
-    case 32: return cells_launch<CellRollCore, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 48: return cells_launch<CellRollCore, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 64: return cells_launch<CellRollCore, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 32: return cells_launch<CellCoreLd, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 48: return cells_launch<CellCoreLd, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 64: return cells_launch<CellCoreLd, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -385,9 +384,9 @@ hipError_t launch_chain_flux_f32(const ChainW &w, const float *nf, const float *
   // small batches: each chain spread over nx/16 waves, as the rollout
   if (chain_rollout_prefers_cells(w, B, nx)) {
     switch (nx) {
-      case 32: return flux_cells_launch<CellCore, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
-      case 48: return flux_cells_launch<CellCore, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
-      case 64: return flux_cells_launch<CellCore, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 32: return flux_cells_launch<CellCoreLd, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 48: return flux_cells_launch<CellCoreLd, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 64: return flux_cells_launch<CellCoreLd, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
       default: break;
     }
   }

@@ -536,11 +536,10 @@ struct CellF16x3T {
     readout_finish<1>(pf1, pb1, W.b2, ffwd, fbwd);
   }
 };
-using CellF16x3 = CellF16x3T<>;
 #ifndef HF_CELLS_LOADER
 #define HF_CELLS_LOADER 1
 #endif
-using CellF16x3Roll = CellF16x3T<HF_CELLS_LOADER != 0>;  // the rollout's: with a loader wave
+using CellF16x3Ld = CellF16x3T<HF_CELLS_LOADER != 0>;  // with a loader wave (the cell-split kernels)
 
 }  // namespace
 
@@ -549,9 +548,9 @@ hipError_t launch_chain_flux_k32(const ChainW &w, const float *nf, const float *
   if (w.prec != kPrecF16x3) return launch_chain_flux_bf16(w, nf, state, ld_state, x, B, nx, fe, ff, s);
   if (chain_rollout_prefers_cells(w, B, nx)) {  // small batches: each chain over nx/16 waves
     switch (nx) {
-      case 32: return chain::flux_cells_launch<CellF16x3, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
-      case 48: return chain::flux_cells_launch<CellF16x3, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
-      case 64: return chain::flux_cells_launch<CellF16x3, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 32: return chain::flux_cells_launch<CellF16x3Ld, 2>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 48: return chain::flux_cells_launch<CellF16x3Ld, 3>(w, nf, state, ld_state, x, B, fe, ff, s);
+      case 64: return chain::flux_cells_launch<CellF16x3Ld, 4>(w, nf, state, ld_state, x, B, fe, ff, s);
       default: break;
     }
   }
@@ -565,9 +564,9 @@ hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float 
                                     float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
   if (w.prec == kPrecF16x3 && ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx)) {
     switch (nx) {  // small batches: each IC over nx/16 waves (cell-split kernel, same bits)
-      case 32: return chain::cells_launch<CellF16x3Roll, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 48: return chain::cells_launch<CellF16x3Roll, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 64: return chain::cells_launch<CellF16x3Roll, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 32: return chain::cells_launch<CellF16x3Ld, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 48: return chain::cells_launch<CellF16x3Ld, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 64: return chain::cells_launch<CellF16x3Ld, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
       default: break;
     }
   }

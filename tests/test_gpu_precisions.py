@@ -247,6 +247,12 @@ def test_cell_split_rollout_any_layer_count(hf, layers, precision):
     for k in ("final", "traj", "flux", "metrics"):
         assert torch.equal(small[k], big[k][:5]), k
     assert torch.isfinite(small["traj"]).all()
+    # FluxGNN.forward: the cell-split flux kernel (5 chains) == the IC-per-wave one (2048)
+    x = torch.as_tensor(G.x, dtype=torch.float32, device=dev)
+    nf = torch.cat([ics, x.expand(len(ics), 1, 48)], dim=1).transpose(1, 2).reshape(-1, 4).contiguous()
+    fe_big = engine.chain_flux(m, nf, len(ics), 48).reshape(len(ics), 96)
+    fe_small = engine.chain_flux(m, nf[:5 * 48].contiguous(), 5, 48).reshape(5, 96)
+    assert torch.equal(fe_small, fe_big[:5])
 
 
 def test_bf16_full_size_cfg4_properties(hf, record):
