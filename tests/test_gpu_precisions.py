@@ -278,6 +278,31 @@ def test_bf16_full_size_cfg4_properties(hf, record):
     close(fin, g["states_wbf16"][:, -1], BF16_STATE_WBF16)
 
 
+@pytest.mark.parametrize("precision", ["bf16", "f32"])
+def test_run_lanes_every_output(hf, precision):
+    """hf_run's lanes (capi.cpp run_lanes: B*nx >= 2^21 cells splits the batch
+    over up to 3 lane streams) slice every output: 3075 ICs x 1024 cells, 3 steps,
+    trajectory, face flux and metrics of ICs on each lane == the same ICs run
+    alone on one stream, bitwise; state0 aliasing state_final as well."""
+    from hybridflux import engine
+    dev = torch.device(DEV)
+    B, nx, T = 3075, 1024, 3  # 3 lanes: ICs [0,1025) [1025,2050) [2050,3075)
+    grid = engine.Grid(nx, dt=3.125e-4)
+    m = engine.DeviceModel(weights("W1_r2"), dev, precision)
+    G = O.Grid(nx, dt=3.125e-4)
+    base = np.stack([O.initial_condition(G, s) for s in range(4000, 4004)])
+    ics = torch.as_tensor(np.tile(base, (B // 4 + 1, 1, 1))[:B], device=dev, dtype=torch.float32)
+    ics = ics * (1 + 1e-3 * torch.arange(B, device=dev, dtype=torch.float32)[:, None, None] / B)
+    full = engine.run(m, grid, ics, T, traj=True, flux=True, metrics=True)
+    for lo, hi in ((0, 3), (1023, 1027), (2048, 2052), (3072, 3075)):  # across the lane edges
+        one = engine.run(m, grid, ics[lo:hi].contiguous(), T, traj=True, flux=True, metrics=True)
+        for k in ("final", "traj", "flux", "metrics"):
+            assert torch.equal(one[k], full[k][lo:hi]), (lo, k)
+    st = ics.clone()
+    engine.run(m, grid, st, T, traj=False, out=st)
+    assert torch.equal(st, full["final"])
+
+
 @pytest.mark.parametrize("layers", [0, 1, 3])
 @pytest.mark.parametrize("nx", [16, 48, 64, 100])
 def test_bf16_flux_layers_and_nx(hf, record, layers, nx):
