@@ -782,24 +782,37 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   // lane i steps ICs [B*i/lanes, B*(i+1)/lanes); lane 0 on the caller's stream
   hipStream_t ls[kMaxLanes] = {s};
   for (int i = 1; i < lanes; ++i) HF_CHECK_HIP(lane_stream(i, &ls[i]), "hf_run lane stream");
-  hipEvent_t fork, join[kMaxLanes] = {};
-  HF_CHECK_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming), "hf_run lane event");
-  hipError_t e = hipEventRecord(fork, s);
+  hipEvent_t fork = nullptr, join[kMaxLanes] = {};
+  for (int i = 1; i < lanes; ++i) {
+    hipError_t ce = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
+    if (ce != hipSuccess) {
+      for (int k = 1; k < i; ++k) (void)hipEventDestroy(join[k]);
+      return fail_hip(ce, "hf_run lane event");
+    }
+  }
+  hipError_t e = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(fork, s);
+  bool used[kMaxLanes] = {};  // lane streams that received work
   for (int i = lanes - 1; i >= 0 && e == hipSuccess; --i) {
     const int64_t o = (int64_t)B * i / lanes, n = (int64_t)B * (i + 1) / lanes - o;
-    if (i > 0) {
-      e = hipStreamWaitEvent(ls[i], fork, 0);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
-    }
-    if (e == hipSuccess)
-      e = run_steps(m, state0 + o * S, state_final + o * S, x, pc, (int)n, nx, T, c, dt, nu, dx2,
-                    traj ? traj + o * ldT : nullptr, flux_traj ? flux_traj + o * T * nx : nullptr,
-                    metrics ? metrics + o * ldM : nullptr, buf0 ? buf0 + o * S : nullptr,
-                    buf1 ? buf1 + o * S : nullptr, F + o * nx, ls[i]);
-    if (i > 0 && e == hipSuccess) e = hipEventRecord(join[i], ls[i]);
+    if (i > 0) e = hipStreamWaitEvent(ls[i], fork, 0);
+    if (e != hipSuccess) break;
+    used[i] = true;
+    e = run_steps(m, state0 + o * S, state_final + o * S, x, pc, (int)n, nx, T, c, dt, nu, dx2,
+                  traj ? traj + o * ldT : nullptr, flux_traj ? flux_traj + o * T * nx : nullptr,
+                  metrics ? metrics + o * ldM : nullptr, buf0 ? buf0 + o * S : nullptr,
+                  buf1 ? buf1 + o * S : nullptr, F + o * nx, ls[i]);
   }
-  for (int i = 1; i < lanes && e == hipSuccess; ++i) e = hipStreamWaitEvent(s, join[i], 0);
-  (void)hipEventDestroy(fork);
+  // join every lane that received work, also after an error, so that nothing
+  // enqueued on a lane outlives the call's scratch (freed on `s`) unordered
+  for (int i = 1; i < lanes; ++i) {
+    if (!used[i]) continue;
+    hipError_t je = hipEventRecord(join[i], ls[i]);
+    if (je == hipSuccess) je = hipStreamWaitEvent(s, join[i], 0);
+    if (je != hipSuccess) (void)hipStreamSynchronize(ls[i]);
+    if (e == hipSuccess) e = je;
+  }
+  if (fork) (void)hipEventDestroy(fork);
   for (int i = 1; i < lanes; ++i)
     if (join[i]) (void)hipEventDestroy(join[i]);
   HF_CHECK_HIP(e, "hf_run");
