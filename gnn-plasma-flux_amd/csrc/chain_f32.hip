@@ -25,7 +25,7 @@ using namespace chain;
 // (chain_common.h Ring): 2 in 4 for the IC-per-wave kernels; the cell-split
 // kernels consume a chunk in a quarter of the time (16 cells per wave) and run
 // deeper (kCellsAhead).
-template <int D = 2, int SLOTS = kRingSlots, bool LDR = false>
+template <int D = 2, int SLOTS = kRingSlots, bool LDR = false, bool DEF = false>
 struct CoreF32T {
   static constexpr int kNW = kWaves;   // waves sharing the weight ring
   static constexpr int kWGPerCU = 1;   // persistent flux kernel: workgroups per CU
@@ -42,7 +42,9 @@ struct CoreF32T {
   // chain_rollout_cells_kernel): 16 ring chunks per update layer, no other barrier
   static constexpr int kLayerChunks = 16;
   static constexpr bool kLayerBarrier = false;
-  using R_t = Ring<kChunkFloats, kNW, kSlots, kAhead, false, LDR>;  // LDR: a loader wave issues the ring DMA
+  // LDR: a loader wave issues the ring DMA; DEF: each wave's DMA for chunk p+D
+  // is issued after unit 0's fragment reads of chunk p, not at the barrier
+  using R_t = Ring<kChunkFloats, kNW, kSlots, kAhead, DEF, LDR>;
 
   // Register-prefetched weight feed.  A chunk is 4 units; unit u is the lane's
   // fragments 2u, 2u+1 and feeds 32 MFMAs (one update k-step, or four readout
@@ -60,7 +62,7 @@ struct CoreF32T {
   }
   static __device__ __forceinline__ void begin(R_t &R, Feed &F) {
     F.slot = R.next();
-    load_unit(F, 0, R.lane);
+    load_unit(F, 0, R.lane);  // (DEF: the DMA this next() owes goes out in take<0>)
   }
   // Hand out unit U of the current chunk and start reading the next unit.
   template <int U>
@@ -71,6 +73,7 @@ struct CoreF32T {
 #ifndef HF_DIAG_NODS  // timing diagnostic only: results are wrong
     load_unit(F, (U + 1) % kUPC, R.lane);
 #endif
+    if constexpr (DEF && U == 0) R.issue_pending();  // after unit 1's fragment reads of the new chunk
   }
   // B operand of flat k-step KS (0..63) of an update layer: k-steps 0..31 read
   // h itself, 32..63 the neighbour mean (h[i+1] + h[i-1]) / 2.  H = CellHalo:
@@ -338,7 +341,10 @@ struct CoreF32T {
   }
 };
 
-using CoreF32 = CoreF32T<>;
+#ifndef HF_F32_DEFER
+#define HF_F32_DEFER 1
+#endif
+using CoreF32 = CoreF32T<2, kRingSlots, false, HF_F32_DEFER != 0>;
 
 // ---------------------------------------------------------------------------
 // Cell-split small-batch kernels (chain_common.h) on the f32 core at MT = 1.

@@ -80,7 +80,7 @@ __device__ __forceinline__ void interleave() {
 
 // UPC = units (4 split fragments, 8 KiB) per ring chunk: 1 (8 KiB chunks,
 // 4 slots: fits beside the rollout's per-IC scratch) or 2 (16 KiB, 3 slots).
-template <int UPC, bool LDR = false>
+template <int UPC, bool LDR = false, bool DEF = false>
 struct CoreF16x3T {
   static constexpr int kNW = kWaves;
   static constexpr int kWGPerCU = 1;
@@ -93,7 +93,9 @@ struct CoreF16x3T {
   static constexpr int kKB = kH / 32;
   // parked fragments of k-blocks 0..2: [kb 3][mt 4][term 2][lane 64][4 dwords]
   static constexpr int kParkFloats = 3 * 4 * 2 * 64 * 4;
-  using R_t = Ring<kChunkFloats, kNW, kSlots, 2, false, LDR>;  // LDR: a loader wave issues the ring DMA
+  // LDR: a loader wave issues the ring DMA; DEF: each wave's DMA owed by a
+  // next() is issued after the following unit's fragment reads
+  using R_t = Ring<kChunkFloats, kNW, kSlots, 2, DEF, LDR>;
 
   template <int MT>
   struct Acts {
@@ -122,6 +124,7 @@ struct CoreF16x3T {
   static __device__ __forceinline__ void begin(R_t &R, Feed &F) {
     F.slot = R.next();
     load_unit(F, 0, R.lane);
+    if constexpr (DEF && UPC == 1) R.issue_pending();  // (UPC > 1: take<0> issues it)
   }
   template <int U>
   static __device__ __forceinline__ void take(R_t &R, Feed &F, Frag (&w)[4]) {
@@ -131,6 +134,7 @@ struct CoreF16x3T {
 #ifndef HF_DIAG_NODS  // timing diagnostic only: results are wrong
     load_unit(F, (U + 1) % UPC, R.lane);
 #endif
+    if constexpr (DEF && U == 0) R.issue_pending();
   }
 
   static __device__ __forceinline__ float *park_at(float *park, int kb, int mt, int s, int lane) {
@@ -540,6 +544,10 @@ struct CellF16x3T {
 #define HF_CELLS_LOADER 1
 #endif
 using CellF16x3Ld = CellF16x3T<HF_CELLS_LOADER != 0>;  // with a loader wave (the cell-split kernels)
+#ifndef HF_K32_DEFER
+#define HF_K32_DEFER 1
+#endif
+constexpr bool kK32Defer = HF_K32_DEFER != 0;  // IC-per-wave f16x3 cores: deferred ring DMA (CoreF16x3T DEF)
 
 }  // namespace
 
@@ -555,8 +563,8 @@ hipError_t launch_chain_flux_k32(const ChainW &w, const float *nf, const float *
     }
   }
   if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
-    return chain::launch_flux_core<CoreF16x3T<1>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
-  return chain::launch_flux_windowed<CoreF16x3T<2>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+    return chain::launch_flux_core<CoreF16x3T<1, false, kK32Defer>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  return chain::launch_flux_windowed<CoreF16x3T<2, false, kK32Defer>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float *state_final, const float *x,
@@ -571,7 +579,7 @@ hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float 
     }
   }
   if (w.prec == kPrecF16x3)
-    return chain::launch_rollout_core<CoreF16x3T<1>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
+    return chain::launch_rollout_core<CoreF16x3T<1, false, kK32Defer>>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj,
                                                      flux_traj, metrics, ex, s);
   return launch_chain_rollout_bf16(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, ex,
                                    s);
