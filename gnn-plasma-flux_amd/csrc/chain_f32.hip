@@ -73,7 +73,11 @@ struct CoreF32T {
 #ifndef HF_DIAG_NODS  // timing diagnostic only: results are wrong
     load_unit(F, (U + 1) % kUPC, R.lane);
 #endif
-    if constexpr (DEF && U == 0) R.issue_pending();  // after unit 1's fragment reads of the new chunk
+#ifndef HF_F32_DEFU
+#define HF_F32_DEFU 0
+#endif
+    // after unit DEFU+1's fragment reads of the new chunk (A/B: HF_F32_DEFU 0..2)
+    if constexpr (DEF && U == HF_F32_DEFU) R.issue_pending();
   }
   // B operand of flat k-step KS (0..63) of an update layer: k-steps 0..31 read
   // h itself, 32..63 the neighbour mean (h[i+1] + h[i-1]) / 2.  H = CellHalo:
