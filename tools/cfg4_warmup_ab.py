@@ -31,6 +31,19 @@ def main():
     met = torch.empty(B, T + 1, 4, device=dev)
     stream = torch.cuda.current_stream(dev)
     res = {}
+    if os.environ.get("CFG4_SEQ"):  # one warmup, then 6 back-to-back timed rollouts, each timed
+        torch.cuda.synchronize(dev)
+        time.sleep(1.0)
+        solver.run_batch(ics, 30, traj=False, ws=ws)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
+        ev[0].record(stream)
+        for i in range(6):
+            solver.run_batch(ics, T, traj=False, metrics=met, out=final, ws=ws)
+            ev[i + 1].record(stream)
+        torch.cuda.synchronize(dev)
+        print(json.dumps({"what": "cfg4: 30 warmup steps after 1 s idle, then six back-to-back 30-step rollouts (ms each)",
+                          "ms": [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(6)]}))
+        return
     for W in (30, 90, 30, 90, 60):
         torch.cuda.synchronize(dev)
         time.sleep(1.0)
