@@ -65,10 +65,10 @@ def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=Non
     """Time one more BASELINE.json single-GPU config the same way as the
     headline (preallocated outputs and workspace, HIP events on the launch
     stream, wall clock around the launches).  Reported next to the headline,
-    never as it.  W untimed warmup steps run first as one rollout (cfg2: as
-    many as one timed rollout; cfg4: two, ~70 ms, so the timed rollouts run at
-    the sustained clock rather than in the clock ramp after the host-side
-    setup; the headline keeps the driver's --warmup).  also: the same workload in another precision,
+    never as it.  W untimed warmup steps run first as one rollout (cfg4: as
+    many as it times (cfg4 ~40 ms), so the timed rollout runs at the sustained
+    clock rather than in the clock ramp after the host-side setup; the headline
+    keeps the driver's --warmup).  also: the same workload in another precision,
     timed the same way and reported under alt_<precision>.  fixture: {label: states [n, K+1, 3, nx]} of the batch's first
     n ICs (committed test vectors); the final states' max |error| against each
     is reported."""
@@ -278,16 +278,13 @@ def main():
               "reference_f32": ref["states"]}
         w_r1 = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r1.npz"), allow_pickle=False))
         w_r2 = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r2.npz"), allow_pickle=False))
-        # both at BASELINE's T = 30; cfg2's 30-step rollout lasts
-        # ~1.5 ms, so five run back to back (the first launch's host latency
-        # would otherwise be ~4 % of the timed region); cfg4 is warmed for 60
-        # steps (after the idle of its host-side setup the clock needs more than
-        # one 30-step rollout to settle: profiles/r02_cfg4_warmup_ab.json) and
-        # timed as two back-to-back 30-step rollouts
+        # both at BASELINE's T = 30, warmed for as many steps as they time
+        # cfg2's 30-step rollout lasts ~1.6 ms, so five run back to back (the
+        # first launch's host latency would otherwise be ~4 % of the timed region)
         others = [other_config(w_r1, dev, "cfg2: 64-cell chain, 256-IC batch, r=1, f32", 256, 64, "f32", 30, 30, 1,
                                also="f16x3", reps=5),
                   other_config(w_r2, dev, "cfg4: 1024-cell chain, 4096-IC batch, r=2, bf16 MLP weights, dt=3.125e-4",
-                               4096, 1024, "bf16", 30, 60, 2, fixture=fx, reps=2)]
+                               4096, 1024, "bf16", 30, 30, 2, fixture=fx)]
 
     wall_max = max_over_ranks(wall, device=dev if args.dist_backend == "nccl" else "cpu")
     finite = float(gathered["metrics"][:, -1, 2].float().mean().item())
