@@ -673,6 +673,17 @@ int run_lanes() {
   return lanes;
 }
 
+// The classical rollout at FFT sizes runs as one persistent launch
+// (fv_run_fft_kernel); HF_FV_PERSIST=0 in the environment selects the
+// per-step launches instead (A/B timing and the bitwise equality test only).
+bool fv_run_persistent() {
+  static const bool on = [] {
+    const char *v = std::getenv("HF_FV_PERSIST");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 // lane stream i (1..kMaxLanes-1) of the current device, created on first use
 hipError_t lane_stream(int i, hipStream_t *out) {
   static std::mutex mu;
@@ -756,6 +767,11 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
     if (state_final != state0)
       HF_CHECK_HIP(hipMemcpyAsync(state_final, state0, sizeof(float) * B * S, hipMemcpyDeviceToDevice, s),
                    "hf_run copy");
+    return HF_OK;
+  }
+  if (!m && hf::fv_run_fused(nx) && fv_run_persistent()) {  // BaselineSolver.run at FFT sizes: one launch
+    HF_CHECK_HIP(hf::launch_fv_run(state0, state_final, traj, pc, B, nx, T, c, dt, nu, dx2, flux_traj, metrics, s),
+                 "hf_run(classical fused)");
     return HF_OK;
   }
   // scratch: two state buffers unless the trajectory is the ping-pong, the face flux for the hybrid step

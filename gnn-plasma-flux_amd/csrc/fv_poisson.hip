@@ -289,6 +289,128 @@ __global__ __launch_bounds__(64 * kFftWaves, 2) void fv_step_fft_kernel(
   if (two) fv_finish_lane<N, true>(out + b * ld_out, v, mb, metrics ? metrics + b * ld_metrics : nullptr, lane);
 }
 
+// ---------------------------------------------- classical rollout, FFT sizes
+// BaselineSolver.run over T steps in ONE launch (src/baseline_solver.py:80-118):
+// the wave of an IC pair keeps both states in registers for the whole
+// rollout, so HBM sees state0 once, the trajectory rows it is asked for
+// (12 B/cell-step) and the final state; no state is re-read.  Every step is
+// the arithmetic of fv_step_fft_kernel<false, N> in the same order (update of
+// IC a, of IC b, the packed transform, E of a, of b; the metrics' partial sums
+// the same), so the rollout equals T launches of it bit for bit.  Registers:
+// n, u, E of two ICs (6 N/64) + the packed rho/E (4 N/64): N <= kFvRunMaxNx.
+constexpr int kFvRunMaxNx = 1024;
+
+// classical update of one IC held in registers (fv_update_lane<false, N>'s
+// expressions); n, u become n', u'; rho = n' - 1.  ro: trajectory row or null.
+template <int N>
+__device__ __forceinline__ void fv_update_regs(float (&n)[N / 64], float (&u)[N / 64], const float (&E)[N / 64],
+                                               float *ro, float *fo, float c, float dt, float nu, float dx2,
+                                               bool want_m, MetricAcc &m, int lane, double (&rho)[N / 64]) {
+  constexpr int V = N / 64;
+  float F[V], ul[V], Fl[V], ur[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) F[i] = __fmul_rn(n[i], u[i]);  // F_n = n*u (src/baseline_solver.py:70-71)
+  left_of<V>(u, ul);
+  left_of<V>(F, Fl);
+  right_of<V>(u, ur);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int cell = lane + 64 * i;
+    const float n_new = continuity(n[i], F[i], Fl[i], c);
+    const float u_new = velocity_classical(u[i], ul[i], ur[i], E[i], c, dt, nu, dx2);
+    if (ro) {
+      ro[cell] = n_new;
+      ro[N + cell] = u_new;
+    }
+    if (fo) fo[cell] = F[i];
+    if (want_m) m.add_nu(n_new, u_new);
+    rho[i] = (double)__fsub_rn(n_new, 1.0f);
+    n[i] = n_new;
+    u[i] = u_new;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void fv_run_E(float (&E)[N / 64], const double2 (&v)[N / 64], bool imag, float *ro,
+                                         MetricAcc &m, float *mo, int lane) {
+#pragma unroll
+  for (int i = 0; i < N / 64; ++i) {
+    E[i] = (float)((imag ? v[i].y : v[i].x) / N);
+    if (ro) ro[2 * N + lane + 64 * i] = E[i];
+    if (mo) m.add_E(E[i]);
+  }
+  if (mo) {
+    m.wave_reduce();
+    if (lane == 0) m.store(mo, N);
+  }
+}
+
+// state0 and state_final may alias: a wave reads its pair whole before its
+// last step writes it, and no other wave touches that pair.
+template <int N>
+__global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_kernel(
+    const float *state0, float *state_final, float *__restrict__ traj, const double *__restrict__ pc, float c,
+    float dt, float nu, float dx2, float *__restrict__ flux_traj, float *__restrict__ metrics, int B, int T) {
+  constexpr int V = N / 64;
+  constexpr int64_t S = 3LL * N;
+  __shared__ double2 s_fft[kFftWaves][fft_lds_elems<N>()];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t a = 2 * ((int64_t)blockIdx.x * kFftWaves + wave), b = a + 1;
+  if (a >= B) return;  // a whole wave; nothing below synchronises the workgroup
+  const bool two = b < B;
+  const int64_t ldT = (T + 1) * S, ldM = (int64_t)(T + 1) * HF_NUM_METRICS;
+  float na[V], ua[V], Ea[V], nb[V], ub[V], Eb[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int cell = lane + 64 * i;
+    na[i] = state0[a * S + cell];
+    ua[i] = state0[a * S + N + cell];
+    Ea[i] = state0[a * S + 2 * N + cell];
+    nb[i] = two ? state0[b * S + cell] : 0.f;
+    ub[i] = two ? state0[b * S + N + cell] : 0.f;
+    Eb[i] = two ? state0[b * S + 2 * N + cell] : 0.f;
+  }
+  for (int t = 0; t < T; ++t) {
+    float *ra = traj ? traj + a * ldT + (t + 1) * S : nullptr;
+    float *rb = traj && two ? traj + b * ldT + (t + 1) * S : nullptr;
+    float *fa = flux_traj ? flux_traj + a * (int64_t)T * N + (int64_t)t * N : nullptr;
+    float *fb = flux_traj && two ? flux_traj + b * (int64_t)T * N + (int64_t)t * N : nullptr;
+    float *ma_o = metrics ? metrics + a * ldM + (int64_t)(t + 1) * HF_NUM_METRICS : nullptr;
+    float *mb_o = metrics && two ? metrics + b * ldM + (int64_t)(t + 1) * HF_NUM_METRICS : nullptr;
+    MetricAcc ma, mb;
+    ma.init();
+    mb.init();
+    double2 v[V];
+    {
+      double r[V];
+      fv_update_regs<N>(na, ua, Ea, ra, fa, c, dt, nu, dx2, metrics != nullptr, ma, lane, r);
+#pragma unroll
+      for (int i = 0; i < V; ++i) v[i].x = r[i];
+    }
+    {
+      double r[V];
+      if (two) fv_update_regs<N>(nb, ub, Eb, rb, fb, c, dt, nu, dx2, metrics != nullptr, mb, lane, r);
+#pragma unroll
+      for (int i = 0; i < V; ++i) v[i].y = two ? r[i] : 0.0;
+    }
+    poisson_wave<N>(v, s_fft[wave], pc, lane);
+    fv_run_E<N>(Ea, v, false, ra, ma, ma_o, lane);
+    if (two) fv_run_E<N>(Eb, v, true, rb, mb, mb_o, lane);
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int cell = lane + 64 * i;
+    state_final[a * S + cell] = na[i];
+    state_final[a * S + N + cell] = ua[i];
+    state_final[a * S + 2 * N + cell] = Ea[i];
+    if (two) {
+      state_final[b * S + cell] = nb[i];
+      state_final[b * S + N + cell] = ub[i];
+      state_final[b * S + 2 * N + cell] = Eb[i];
+    }
+  }
+}
+
 // hf_poisson at FFT sizes: one wave per pair of ICs, as above.
 template <int N>
 __global__ __launch_bounds__(64 * kFftWaves, 2) void poisson_fft_kernel(const float *__restrict__ n, int ld_n,
@@ -429,6 +551,28 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
                        ld_out, face_flux, pc, nx, c, dt, nu, dx2, flux_out, ld_flux, metrics,
                        ld_metrics);
   return hipGetLastError();
+}
+
+template <int N>
+hipError_t fv_run_fft_launch(const float *state0, float *state_final, float *traj, const double *pc, int B, int T,
+                             float c, float dt, float nu, float dx2, float *flux_traj, float *metrics, hipStream_t s) {
+  const unsigned grid = (unsigned)((B + 2 * kFftWaves - 1) / (2 * kFftWaves));
+  hipLaunchKernelGGL((fv_run_fft_kernel<N>), dim3(grid), dim3(64 * kFftWaves), 0, s, state0, state_final, traj, pc, c,
+                     dt, nu, dx2, flux_traj, metrics, B, T);
+  return hipGetLastError();
+}
+
+bool fv_run_fused(int nx) { return poisson_uses_fft(nx) && nx <= kFvRunMaxNx; }
+
+hipError_t launch_fv_run(const float *state0, float *state_final, float *traj, const double *pc, int B, int nx, int T,
+                         float c, float dt, float nu, float dx2, float *flux_traj, float *metrics, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  switch (fv_run_fused(nx) ? nx : 0) {
+    case 256: return fv_run_fft_launch<256>(state0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, s);
+    case 512: return fv_run_fft_launch<512>(state0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, s);
+    case 1024: return fv_run_fft_launch<1024>(state0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_state_metrics(const float *st, int64_t ld, int B, int nx, float *metrics,

@@ -174,6 +174,34 @@ def test_classical_run_vs_reference(hf):
     close(r["traj"].cpu().numpy(), g["nx1024_states"], ROLL_ATOL, ROLL_RTOL)
 
 
+@pytest.mark.parametrize("nx", [256, 512, 1024, 2048])
+def test_classical_run_fused_equals_steps(hf, nx):
+    """BaselineSolver.run at FFT sizes (src/baseline_solver.py:80-118): the
+    one-launch register-resident rollout (fv_run_fft_kernel, nx <= 1024; 2048
+    stays per-step) equals T per-step launches (hf_step) bit for bit, in every
+    output: trajectory, flux, metrics, final state; odd B leaves a half pair;
+    state0 aliased with the final state."""
+    from hybridflux import engine
+    T, B = 12, 7
+    s = hf.BaselineSolver(nx, dt=3.125e-4, device=DEV)
+    st0 = torch.as_tensor(s.initial_conditions(list(range(40, 40 + B))), device=DEV).contiguous()
+    r = engine.run(None, s.grid, st0, T, traj=True, flux=True, metrics=True)
+    cur, traj, flux, met = st0, [st0], [], [None]
+    for _ in range(T):
+        cur, F, M = engine.step(None, s.grid, cur, flux_face=True, metrics=True)
+        traj.append(cur)
+        flux.append(F)
+        met.append(M)
+    torch.cuda.synchronize()
+    assert torch.equal(r["traj"], torch.stack(traj, 1))
+    assert torch.equal(r["flux"], torch.stack(flux, 1))
+    assert torch.equal(r["metrics"][:, 1:], torch.stack(met[1:], 1))
+    assert torch.equal(r["final"], cur)
+    alias = st0.clone()
+    engine.run(None, s.grid, alias, T, traj=False, out=alias)       # no trajectory, in place
+    assert torch.equal(alias, cur)
+
+
 # ------------------------------------------------------------------- hybrid
 @pytest.mark.parametrize("w", ["W0", "W1_r1", "W1_r2", "W1_r3"])
 def test_hybrid_rollout_vs_reference(hf, w):
