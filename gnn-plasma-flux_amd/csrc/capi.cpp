@@ -574,7 +574,7 @@ int64_t hf_run_workspace_bytes(int op, int B, int nx, int T) {
   switch (op) {
     case HF_OP_STEP: return up(B * F);
     case HF_OP_RUN: return 2 * up(B * S) + up(B * F);
-    default: return 2 * up(B * (T + 1) * S) + up(B * S) + up(B * F);
+    default: return 2 * up((int64_t)B * (T + 1) * S) + up(B * S) + up(B * F);
   }
 }
 
