@@ -354,6 +354,12 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_
   constexpr int V = N / 64;
   constexpr int64_t S = 3LL * N;
   __shared__ double2 s_fft[kFftWaves][fft_lds_elems<N>()];
+  // the plan's twiddles and 1/k, staged once: the step loop then issues no
+  // global load, so no vmcnt wait holds a wave until its trajectory stores
+  // have drained (stores and loads share the counter)
+  __shared__ double2 s_plan[N];
+  for (int i = threadIdx.x; i < 2 * N; i += 64 * kFftWaves) reinterpret_cast<double *>(s_plan)[i] = pc[N + i];
+  __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t a = 2 * ((int64_t)blockIdx.x * kFftWaves + wave), b = a + 1;
   if (a >= B) return;  // a whole wave; nothing below synchronises the workgroup
@@ -393,7 +399,7 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_
 #pragma unroll
       for (int i = 0; i < V; ++i) v[i].y = two ? r[i] : 0.0;
     }
-    poisson_wave<N>(v, s_fft[wave], pc, lane);
+    poisson_wave_tw<N>(v, s_fft[wave], s_plan, reinterpret_cast<const double *>(s_plan) + N, lane);
     fv_run_E<N>(Ea, v, false, ra, ma, ma_o, lane);
     if (two) fv_run_E<N>(Eb, v, true, rb, mb, mb_o, lane);
   }

@@ -205,11 +205,11 @@ __device__ __forceinline__ void fft_passes(double2 (&v)[N / 64], double2 *lds, c
 // i/k maps the FFT of a real signal to the FFT of a real signal, so the real
 // and imaginary parts of the packed transform are the two fields.  plan =
 // hf_poisson_coeffs (twiddles at plan + N, 1/k at plan + 2N).
+// poisson_wave_tw takes the plan's twiddles and 1/k wherever they are staged
+// (global memory, or an LDS copy in fv_run_fft_kernel).
 template <int N>
-__device__ __forceinline__ void poisson_wave(double2 (&v)[N / 64], double2 *lds, const double *__restrict__ plan,
-                                             int lane) {
-  const double2 *tw = reinterpret_cast<const double2 *>(plan + N);
-  const double *inv_k = plan + 2 * N;
+__device__ __forceinline__ void poisson_wave_tw(double2 (&v)[N / 64], double2 *lds, const double2 *__restrict__ tw,
+                                                const double *__restrict__ inv_k, int lane) {
 #ifndef HF_DIAG_NOFFT  // timing diagnostic only: results are wrong (no transforms)
   fft_passes<N, 1, false>(v, lds, tw, lane);
 #endif
@@ -221,6 +221,11 @@ __device__ __forceinline__ void poisson_wave(double2 (&v)[N / 64], double2 *lds,
 #ifndef HF_DIAG_NOFFT
   fft_passes<N, 1, true>(v, lds, tw, lane);
 #endif
+}
+template <int N>
+__device__ __forceinline__ void poisson_wave(double2 (&v)[N / 64], double2 *lds, const double *__restrict__ plan,
+                                             int lane) {
+  poisson_wave_tw<N>(v, lds, reinterpret_cast<const double2 *>(plan + N), plan + 2 * N, lane);
 }
 
 // Per-state rollout metrics, partial sums for one cell.
