@@ -770,7 +770,8 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
     return HF_OK;
   }
   if (!m && hf::fv_run_fused(nx) && fv_run_persistent()) {  // BaselineSolver.run at FFT sizes: one launch
-    HF_CHECK_HIP(hf::launch_fv_run(state0, state_final, traj, pc, B, nx, T, c, dt, nu, dx2, flux_traj, metrics, s),
+    HF_CHECK_HIP(hf::launch_fv_run(state0, S, state_final, traj, pc, B, nx, T, c, dt, nu, dx2, flux_traj, metrics,
+                                   nullptr, nullptr, s),
                  "hf_run(classical fused)");
     return HF_OK;
   }
@@ -853,6 +854,28 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
     HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, state0, state_final, x, pc, B, nx, T, c, dt, nullptr, nullptr,
                                           metrics, s, ex),
                  "hf_run_compare(fused)");
+    return HF_OK;
+  }
+  if (hf::fv_run_fused(nx) && fv_run_persistent()) {
+    // FFT nx <= 1024: the hybrid rollout first, recording its trajectory; then
+    // the classical twin as one launch from that trajectory's row 0 (state0,
+    // also when state_final aliases it), scoring each step against the hybrid
+    // row as it goes: no classical trajectory, no MSE pass.  Same bits as below.
+    Scratch sc;
+    if (int rc = sc.init(ws, ws_bytes, hf_run_workspace_bytes(HF_OP_COMPARE, B, nx, T), s, "hf_run_compare"))
+      return rc;
+    const int64_t S = 3LL * nx, ldT = (T + 1) * S;
+    float *th = sc.take(sizeof(float) * (int64_t)B * ldT);
+    const int64_t fbytes = (sizeof(float) * (int64_t)B * nx + 255) / 256 * 256;
+    float *F = sc.take(fbytes);
+    int rc = hf_run(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, th, nullptr, metrics, F, fbytes, stream);
+    if (rc != HF_OK) return rc;
+    if (metrics_cl)
+      HF_CHECK_HIP(hf::launch_state_metrics(th, ldT, B, nx, metrics_cl, (int64_t)(T + 1) * HF_NUM_METRICS, s),
+                   "hf_run_compare metrics[0]");
+    HF_CHECK_HIP(hf::launch_fv_run(th, ldT, nullptr, nullptr, pc, B, nx, T, c, dt, nu, dx2, nullptr, metrics_cl, th, mse,
+                                   s),
+                 "hf_run_compare(classical twin)");
     return HF_OK;
   }
   // generic nx: both trajectories through HBM, then the MSE reduction.  The

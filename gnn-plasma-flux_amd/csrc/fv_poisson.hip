@@ -345,12 +345,52 @@ __device__ __forceinline__ void fv_run_E(float (&E)[N / 64], const double2 (&v)[
   }
 }
 
-// state0 and state_final may alias: a wave reads its pair whole before its
-// last step writes it, and no other wave touches that pair.
+// Channel MSE of one IC's state (x) against a row of a reference trajectory,
+// in traj_mse_kernel's arithmetic and order: its thread 64w + l sums cells
+// l + 64(w + 4k) in k order, each wave xor-reduces, then the 4 wave partials
+// are added in w order (scripts/evaluation/evaluate_multi_ic.py:88-90).
 template <int N>
+__device__ __forceinline__ float mse_channel(const float (&x)[N / 64], const float *__restrict__ ref, int lane) {
+  constexpr int V = N / 64, W = kFvThreads / 64;
+  double p[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    p[w] = 0.0;
+#pragma unroll
+    for (int i = w; i < V; i += W) {
+      const double d = (double)ref[lane + 64 * i] - (double)x[i];
+      p[w] += d * d;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) p[w] += __shfl_xor(p[w], o, 64);
+  }
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) t += p[w];
+  return (float)(t / N);
+}
+template <int N>
+__device__ __forceinline__ void mse_row(const float (&n)[N / 64], const float (&u)[N / 64], const float (&E)[N / 64],
+                                        const float *__restrict__ ref, float *mo, int lane) {
+  const float m0 = mse_channel<N>(n, ref, lane), m1 = mse_channel<N>(u, ref + N, lane),
+              m2 = mse_channel<N>(E, ref + 2 * N, lane);
+  if (lane == 0) {
+    mo[0] = m0;
+    mo[1] = m1;
+    mo[2] = m2;
+  }
+}
+
+// state0 (IC stride ld_s0) and state_final may alias: a wave reads its pair
+// whole before its last step writes it, and no other wave touches that pair.
+// state_final may be NULL.  ref/mse (both or neither): the per-step channel
+// MSE [B][T+1][3] of the reference trajectory ref [B][T+1][3][N] minus this
+// rollout (hf_run_compare's classical twin, scored as it steps).
+template <int N, bool SCORE>
 __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_kernel(
-    const float *state0, float *state_final, float *__restrict__ traj, const double *__restrict__ pc, float c,
-    float dt, float nu, float dx2, float *__restrict__ flux_traj, float *__restrict__ metrics, int B, int T) {
+    const float *state0, int64_t ld_s0, float *state_final, float *__restrict__ traj, const double *__restrict__ pc,
+    float c, float dt, float nu, float dx2, float *__restrict__ flux_traj, float *__restrict__ metrics,
+    const float *__restrict__ ref, float *__restrict__ mse, int B, int T) {
   constexpr int V = N / 64;
   constexpr int64_t S = 3LL * N;
   __shared__ double2 s_fft[kFftWaves][fft_lds_elems<N>()];
@@ -369,12 +409,16 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int cell = lane + 64 * i;
-    na[i] = state0[a * S + cell];
-    ua[i] = state0[a * S + N + cell];
-    Ea[i] = state0[a * S + 2 * N + cell];
-    nb[i] = two ? state0[b * S + cell] : 0.f;
-    ub[i] = two ? state0[b * S + N + cell] : 0.f;
-    Eb[i] = two ? state0[b * S + 2 * N + cell] : 0.f;
+    na[i] = state0[a * ld_s0 + cell];
+    ua[i] = state0[a * ld_s0 + N + cell];
+    Ea[i] = state0[a * ld_s0 + 2 * N + cell];
+    nb[i] = two ? state0[b * ld_s0 + cell] : 0.f;
+    ub[i] = two ? state0[b * ld_s0 + N + cell] : 0.f;
+    Eb[i] = two ? state0[b * ld_s0 + 2 * N + cell] : 0.f;
+  }
+  if constexpr (SCORE) {
+    mse_row<N>(na, ua, Ea, ref + a * ldT, mse + a * (T + 1) * 3, lane);
+    if (two) mse_row<N>(nb, ub, Eb, ref + b * ldT, mse + b * (T + 1) * 3, lane);
   }
   for (int t = 0; t < T; ++t) {
     float *ra = traj ? traj + a * ldT + (t + 1) * S : nullptr;
@@ -402,7 +446,12 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_
     poisson_wave_tw<N>(v, s_fft[wave], s_plan, reinterpret_cast<const double *>(s_plan) + N, lane);
     fv_run_E<N>(Ea, v, false, ra, ma, ma_o, lane);
     if (two) fv_run_E<N>(Eb, v, true, rb, mb, mb_o, lane);
+    if constexpr (SCORE) {
+      mse_row<N>(na, ua, Ea, ref + a * ldT + (t + 1) * S, mse + (a * (T + 1) + t + 1) * 3, lane);
+      if (two) mse_row<N>(nb, ub, Eb, ref + b * ldT + (t + 1) * S, mse + (b * (T + 1) + t + 1) * 3, lane);
+    }
   }
+  if (!state_final) return;
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int cell = lane + 64 * i;
@@ -560,23 +609,30 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
 }
 
 template <int N>
-hipError_t fv_run_fft_launch(const float *state0, float *state_final, float *traj, const double *pc, int B, int T,
-                             float c, float dt, float nu, float dx2, float *flux_traj, float *metrics, hipStream_t s) {
+hipError_t fv_run_fft_launch(const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *pc,
+                             int B, int T, float c, float dt, float nu, float dx2, float *flux_traj, float *metrics,
+                             const float *ref, float *mse, hipStream_t s) {
   const unsigned grid = (unsigned)((B + 2 * kFftWaves - 1) / (2 * kFftWaves));
-  hipLaunchKernelGGL((fv_run_fft_kernel<N>), dim3(grid), dim3(64 * kFftWaves), 0, s, state0, state_final, traj, pc, c,
-                     dt, nu, dx2, flux_traj, metrics, B, T);
+  if (mse)
+    hipLaunchKernelGGL((fv_run_fft_kernel<N, true>), dim3(grid), dim3(64 * kFftWaves), 0, s, state0, ld_s0,
+                       state_final, traj, pc, c, dt, nu, dx2, flux_traj, metrics, ref, mse, B, T);
+  else
+    hipLaunchKernelGGL((fv_run_fft_kernel<N, false>), dim3(grid), dim3(64 * kFftWaves), 0, s, state0, ld_s0,
+                       state_final, traj, pc, c, dt, nu, dx2, flux_traj, metrics, ref, mse, B, T);
   return hipGetLastError();
 }
 
 bool fv_run_fused(int nx) { return poisson_uses_fft(nx) && nx <= kFvRunMaxNx; }
 
-hipError_t launch_fv_run(const float *state0, float *state_final, float *traj, const double *pc, int B, int nx, int T,
-                         float c, float dt, float nu, float dx2, float *flux_traj, float *metrics, hipStream_t s) {
+hipError_t launch_fv_run(const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *pc, int B,
+                         int nx, int T, float c, float dt, float nu, float dx2, float *flux_traj, float *metrics,
+                         const float *ref, float *mse, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  if ((ref == nullptr) != (mse == nullptr)) return hipErrorInvalidValue;
   switch (fv_run_fused(nx) ? nx : 0) {
-    case 256: return fv_run_fft_launch<256>(state0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, s);
-    case 512: return fv_run_fft_launch<512>(state0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, s);
-    case 1024: return fv_run_fft_launch<1024>(state0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, s);
+    case 256: return fv_run_fft_launch<256>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, s);
+    case 512: return fv_run_fft_launch<512>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, s);
+    case 1024: return fv_run_fft_launch<1024>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -172,12 +172,15 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
 
 // The whole classical rollout (T steps of launch_fv_step's classical update)
 // in one launch, states held in registers: FFT nx up to 1024 (fv_run_fused).
-// Contiguous [B][3][nx] states (state0 may alias state_final); traj
-// [B][T+1][3][nx] rows 1..T, flux_traj [B][T][nx], metrics [B][T+1][4] rows
-// 1..T, each optional.
+// state0 [B] x IC stride ld_s0 floats, state_final [B][3][nx] (may alias
+// state0, may be NULL); traj [B][T+1][3][nx] rows 1..T, flux_traj [B][T][nx],
+// metrics [B][T+1][4] rows 1..T, each optional; ref + mse (both or neither):
+// per-step channel MSE [B][T+1][3] of ref [B][T+1][3][nx] minus this rollout,
+// rows 0..T, bit-identical to launch_traj_mse on the recorded trajectory.
 bool fv_run_fused(int nx);
-hipError_t launch_fv_run(const float *state0, float *state_final, float *traj, const double *pc, int B, int nx, int T,
-                         float c, float dt, float nu, float dx2, float *flux_traj, float *metrics, hipStream_t s);
+hipError_t launch_fv_run(const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *pc, int B,
+                         int nx, int T, float c, float dt, float nu, float dx2, float *flux_traj, float *metrics,
+                         const float *ref, float *mse, hipStream_t s);
 
 // Metrics of a state batch (used for t=0 of non-fused rollouts).
 hipError_t launch_state_metrics(const float *st, int64_t ld, int B, int nx, float *metrics,

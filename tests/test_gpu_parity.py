@@ -445,6 +445,30 @@ def test_compare_vs_oracle(hf, nx, precision):
     close(per_ic, want.sum(-1).mean(-1), 1e-9, 2e-3)
 
 
+@pytest.mark.parametrize("nx", [256, 512, 1024])
+def test_compare_scored_twin_equals_recorded(hf, nx):
+    """hf_run_compare at FFT nx <= 1024 scores its classical twin inside the
+    one-launch classical rollout (no classical trajectory, no MSE pass): the MSE
+    and classical metrics equal hf_traj_mse / the metrics of the two rollouts
+    recorded separately, bit for bit; also with state0 aliased to the final
+    state (evaluate_multi_ic.py:21-94)."""
+    from hybridflux import engine
+    T, B = 9, 5
+    solver = hf.HybridSolver(weights("W1_r1"), radius=1, nx=nx, dt=3.125e-4, device=DEV)
+    ics = torch.as_tensor(solver.baseline.initial_conditions(list(range(70, 70 + B))), device=DEV).contiguous()
+    out = solver.compare_batch(ics, T)
+    h = solver.run_batch(ics, T, metrics=True)
+    cl = solver.baseline.run_batch(ics, T, metrics=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out["mse"], engine.traj_mse(h["traj"], cl["traj"]))
+    assert torch.equal(out["metrics_classical"], cl["metrics"])
+    assert torch.equal(out["metrics"], h["metrics"])
+    assert torch.equal(out["final"], h["final"])
+    alias = ics.clone()
+    out2 = solver.compare_batch(alias, T, out=alias)
+    assert torch.equal(out2["mse"], out["mse"]) and torch.equal(alias, h["final"])
+
+
 # ------------------------------------------------------------- dataset writer
 def test_generate_dataset_vs_oracle(hf, tmp_path):
     """hybridflux.datagen == scripts/training/generate_data.py (keys, order, values)."""
