@@ -202,36 +202,50 @@ __device__ __forceinline__ void right_of(const float (&x)[V], float (&rt)[V]) {
 
 constexpr int kFftWaves = 4;
 
+// One IC's step inputs, cells lane + 64v: n, u, E and the face flux F
+// (hybrid: the GNN's; classical: n*u, src/baseline_solver.py:70-71).
+template <int N>
+struct FvIn {
+  float n[N / 64], u[N / 64], E[N / 64], F[N / 64];
+};
+template <bool HYBRID, int N>
+__device__ __forceinline__ void fv_load(const float *__restrict__ st, const float *__restrict__ Fb, int lane,
+                                        FvIn<N> &x) {
+#pragma unroll
+  for (int i = 0; i < N / 64; ++i) {
+    const int cell = lane + 64 * i;
+    x.n[i] = st[cell];
+    x.u[i] = st[N + cell];
+    x.E[i] = st[2 * N + cell];
+    if constexpr (HYBRID) x.F[i] = Fb[cell];
+  }
+  if constexpr (!HYBRID) {
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) x.F[i] = __fmul_rn(x.n[i], x.u[i]);
+  }
+}
+
 // The update of one IC's cells (lane + 64v) held by this lane: writes n', u'
 // (and F), accumulates the n, u part of the metrics, returns rho = n' - 1.
 template <bool HYBRID, int N>
-__device__ __forceinline__ void fv_update_lane(const float *__restrict__ st, float *__restrict__ so,
-                                               const float *__restrict__ Fb, float c, float dt, float nu, float dx2,
-                                               float *__restrict__ fo, bool want_m, MetricAcc &m, int lane,
-                                               double (&rho)[N / 64]) {
+__device__ __forceinline__ void fv_update_in(const FvIn<N> &x, float *__restrict__ so, float c, float dt, float nu,
+                                             float dx2, float *__restrict__ fo, bool want_m, MetricAcc &m, int lane,
+                                             double (&rho)[N / 64]) {
   constexpr int V = N / 64;
-  float n[V], u[V], E[V], F[V], ul[V], Fl[V], ur[V];
+  float ul[V], Fl[V], ur[V];
+  left_of<V>(x.u, ul);
+  left_of<V>(x.F, Fl);
+  if constexpr (!HYBRID) right_of<V>(x.u, ur);
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int cell = lane + 64 * i;
-    n[i] = st[cell];
-    u[i] = st[N + cell];
-    E[i] = st[2 * N + cell];
-    F[i] = HYBRID ? Fb[cell] : __fmul_rn(n[i], u[i]);  // F_n = n*u (src/baseline_solver.py:70-71)
-  }
-  left_of<V>(u, ul);
-  left_of<V>(F, Fl);
-  if constexpr (!HYBRID) right_of<V>(u, ur);
-#pragma unroll
-  for (int i = 0; i < V; ++i) {
-    const int cell = lane + 64 * i;
-    const float n_new = continuity(n[i], F[i], Fl[i], c);
+    const float n_new = continuity(x.n[i], x.F[i], Fl[i], c);
     float u_new;
-    if constexpr (HYBRID) u_new = velocity_hybrid(u[i], ul[i], E[i], c, dt);
-    else u_new = velocity_classical(u[i], ul[i], ur[i], E[i], c, dt, nu, dx2);
+    if constexpr (HYBRID) u_new = velocity_hybrid(x.u[i], ul[i], x.E[i], c, dt);
+    else u_new = velocity_classical(x.u[i], ul[i], ur[i], x.E[i], c, dt, nu, dx2);
     so[cell] = n_new;
     so[N + cell] = u_new;
-    if (fo) fo[cell] = F[i];
+    if (fo) fo[cell] = x.F[i];
     if (want_m) m.add_nu(n_new, u_new);
     rho[i] = (double)__fsub_rn(n_new, 1.0f);
   }
@@ -268,18 +282,30 @@ __global__ __launch_bounds__(64 * kFftWaves, 2) void fv_step_fft_kernel(
   ma.init();
   mb.init();
   double2 v[V];
+  // IC b's inputs are loaded before IC a's stores: loads and stores share
+  // vmcnt, so a load issued after them would wait until they had drained
+  // (HF_FV_NO_PREFETCH: the old order, A/B builds only)
+  FvIn<N> xb;
+#ifndef HF_FV_NO_PREFETCH
+  if (two) fv_load<HYBRID, N>(in + b * ld_in, HYBRID ? face_flux + b * N : nullptr, lane, xb);
+#endif
   {
+    FvIn<N> xa;
+    fv_load<HYBRID, N>(in + a * ld_in, HYBRID ? face_flux + a * N : nullptr, lane, xa);
     double r[V];
-    fv_update_lane<HYBRID, N>(in + a * ld_in, out + a * ld_out, HYBRID ? face_flux + a * N : nullptr, c, dt, nu,
-                              dx2, flux_out ? flux_out + a * ld_flux : nullptr, metrics != nullptr, ma, lane, r);
+    fv_update_in<HYBRID, N>(xa, out + a * ld_out, c, dt, nu, dx2, flux_out ? flux_out + a * ld_flux : nullptr,
+                            metrics != nullptr, ma, lane, r);
 #pragma unroll
     for (int i = 0; i < V; ++i) rho_a[lane + 64 * i] = r[i];  // parked while IC b's update holds the registers
   }
   {
     double r[V];
+#ifdef HF_FV_NO_PREFETCH
+    if (two) fv_load<HYBRID, N>(in + b * ld_in, HYBRID ? face_flux + b * N : nullptr, lane, xb);
+#endif
     if (two)
-      fv_update_lane<HYBRID, N>(in + b * ld_in, out + b * ld_out, HYBRID ? face_flux + b * N : nullptr, c, dt, nu,
-                                dx2, flux_out ? flux_out + b * ld_flux : nullptr, metrics != nullptr, mb, lane, r);
+      fv_update_in<HYBRID, N>(xb, out + b * ld_out, c, dt, nu, dx2, flux_out ? flux_out + b * ld_flux : nullptr,
+                              metrics != nullptr, mb, lane, r);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int i = 0; i < V; ++i) v[i] = make_double2(rho_a[lane + 64 * i], two ? r[i] : 0.0);
@@ -300,7 +326,7 @@ __global__ __launch_bounds__(64 * kFftWaves, 2) void fv_step_fft_kernel(
 // n, u, E of two ICs (6 N/64) + the packed rho/E (4 N/64): N <= kFvRunMaxNx.
 constexpr int kFvRunMaxNx = 1024;
 
-// classical update of one IC held in registers (fv_update_lane<false, N>'s
+// classical update of one IC held in registers (fv_update_in<false, N>'s
 // expressions); n, u become n', u'; rho = n' - 1.  ro: trajectory row or null.
 template <int N>
 __device__ __forceinline__ void fv_update_regs(float (&n)[N / 64], float (&u)[N / 64], const float (&E)[N / 64],
