@@ -409,14 +409,14 @@ __device__ __forceinline__ void mse_row(const float (&n)[N / 64], const float (&
 
 // state0 (IC stride ld_s0) and state_final may alias: a wave reads its pair
 // whole before its last step writes it, and no other wave touches that pair.
-// state_final may be NULL.  ref/mse (both or neither): the per-step channel
+// state_final may be NULL.  No pointer is __restrict__: hf_run_compare passes
+// the hybrid trajectory as both state0 (its row 0) and ref.  ref/mse (both or neither): the per-step channel
 // MSE [B][T+1][3] of the reference trajectory ref [B][T+1][3][N] minus this
 // rollout (hf_run_compare's classical twin, scored as it steps).
 template <int N, bool SCORE>
 __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_kernel(
-    const float *state0, int64_t ld_s0, float *state_final, float *__restrict__ traj, const double *__restrict__ pc,
-    float c, float dt, float nu, float dx2, float *__restrict__ flux_traj, float *__restrict__ metrics,
-    const float *__restrict__ ref, float *__restrict__ mse, int B, int T) {
+    const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *__restrict__ pc, float c,
+    float dt, float nu, float dx2, float *flux_traj, float *metrics, const float *ref, float *mse, int B, int T) {
   constexpr int V = N / 64;
   constexpr int64_t S = 3LL * N;
   __shared__ double2 s_fft[kFftWaves][fft_lds_elems<N>()];
