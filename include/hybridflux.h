@@ -284,6 +284,11 @@ int hf_run(hf_model_t model, const float *dev_state0, float *dev_state_final,
  * dev_metrics / dev_metrics_classical [B][T+1][HF_NUM_METRICS] (may be NULL).
  * dev_state_final receives the hybrid final state; it may alias dev_state0.
  * For nx in {16,32,48,64} both solvers advance inside the one persistent kernel.
+ * For nx in {256, 512, 1024} (model not fused) the hybrid rollout runs first and
+ * the classical twin is one launch that scores each step against the hybrid
+ * trajectory as it goes; the results equal the recorded-trajectory path bit
+ * for bit.  dev_workspace, if given, is sized by hf_run_workspace_bytes(
+ * HF_OP_COMPARE, ...) for every nx.
  */
 int hf_run_compare(hf_model_t model, const float *dev_state0, float *dev_state_final,
                    const float *dev_x, const double *dev_c, int B, int nx, int T,
