@@ -126,7 +126,7 @@ def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=Non
 
 def pmc_traffic(K, B, nx, traj):
     """HBM bytes per launch of the headline kernel from the committed PMC passes
-    (tools/gpu_pmc.sh + tools/pmc_traffic.py): FETCH_SIZE / WRITE_SIZE at two
+    (tools/gpu_pmc_traffic.sh + tools/pmc_traffic.py): FETCH_SIZE / WRITE_SIZE at two
     step counts give a fixed part and a per-step part, so the figure applies to
     any --steps of the same workload."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")

@@ -18,7 +18,7 @@ import sqlite3
 import sys
 from glob import glob
 
-KERNEL = "CoreF32, 4>"   # the headline (f32) kernel; bench times alt precisions after it
+KERNEL = "CoreF32T<2, 4, false, true>, 4>"   # the headline (f32) kernel; bench times alt precisions after it
 
 
 def last_value(db, counter):
