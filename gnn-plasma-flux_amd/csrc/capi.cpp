@@ -769,7 +769,7 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
                    "hf_run copy");
     return HF_OK;
   }
-  if (!m && hf::fv_run_fused(nx) && fv_run_persistent()) {  // BaselineSolver.run at FFT sizes: one launch
+  if (!m && hf::fv_run_fused(nx) && fv_run_persistent()) {  // BaselineSolver.run at FFT nx <= 1024 and nx <= 64: one launch
     HF_CHECK_HIP(hf::launch_fv_run(state0, S, state_final, traj, pc, B, nx, T, c, dt, nu, dx2, flux_traj, metrics,
                                    nullptr, nullptr, s),
                  "hf_run(classical fused)");
@@ -856,7 +856,7 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
                  "hf_run_compare(fused)");
     return HF_OK;
   }
-  if (hf::fv_run_fused(nx) && fv_run_persistent()) {
+  if (hf::poisson_uses_fft(nx) && hf::fv_run_fused(nx) && fv_run_persistent()) {
     // FFT nx <= 1024: the hybrid rollout first, recording its trajectory; then
     // the classical twin as one launch from that trajectory's row 0 (state0,
     // also when state_final aliases it), scoring each step against the hybrid

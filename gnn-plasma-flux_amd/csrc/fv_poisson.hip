@@ -492,6 +492,82 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_
   }
 }
 
+// ------------------------------------- classical rollout, nx <= 64 (circulant)
+// BaselineSolver.run over T steps in one launch for small chains (the
+// reference's default nx = 64, src/baseline_solver.py:80-118): one WAVE per
+// IC, lane i holds cell i's n, u, E in registers for the whole rollout; the
+// chain neighbours come by lane shuffle, rho goes through a wave-private LDS
+// row, and E is poisson_cell over it, exactly as fv_step_kernel<false>
+// evaluates every expression (its cells all sit in its wave 0, so its
+// workgroup reduction of the metrics is this wave's reduction followed by
+// three +0.0 partials, reproduced below).  Bit-identical to T hf_step calls.
+constexpr int kFvSmallMaxNx = 64;
+
+__global__ __launch_bounds__(kFvThreads) void fv_run_small_kernel(const float *state0, float *state_final,
+                                                                  float *traj, const double *__restrict__ pc, int nx,
+                                                                  float c, float dt, float nu, float dx2,
+                                                                  float *flux_traj, float *metrics, int B, int T) {
+  __shared__ double s_c[kFvSmallMaxNx];
+  __shared__ float s_rho[kFvThreads / 64][kFvSmallMaxNx];
+  for (int i = threadIdx.x; i < nx; i += kFvThreads) s_c[i] = pc[i];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, i = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (kFvThreads / 64) + wave;
+  if (b >= B) return;  // a whole wave; nothing below synchronises the workgroup
+  const int64_t S = 3LL * nx, ldT = (T + 1) * S, ldM = (int64_t)(T + 1) * HF_NUM_METRICS;
+  const bool on = i < nx;
+  const int im = i == 0 ? nx - 1 : i - 1, ip = i >= nx - 1 ? 0 : i + 1;
+  float n = on ? state0[b * S + i] : 0.f, u = on ? state0[b * S + nx + i] : 0.f,
+        E = on ? state0[b * S + 2 * nx + i] : 0.f;
+  float *rho = s_rho[wave];
+  for (int t = 0; t < T; ++t) {
+    const float F = __fmul_rn(n, u);  // F_n = n*u (:70-71)
+    const float um = __shfl(u, im, 64), up = __shfl(u, ip, 64), Fm = __shfl(F, im, 64);
+    const float n_new = continuity(n, F, Fm, c);
+    const float u_new = velocity_classical(u, um, up, E, c, dt, nu, dx2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous step's rho reads are done
+    if (on) rho[i] = __fsub_rn(n_new, 1.0f);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's rho is in LDS
+    float *row = traj ? traj + b * ldT + (int64_t)(t + 1) * S : nullptr;
+    if (on) {
+      if (row) {
+        row[i] = n_new;
+        row[nx + i] = u_new;
+      }
+      if (flux_traj) flux_traj[b * (int64_t)T * nx + (int64_t)t * nx + i] = F;
+    }
+    const float E_new = on ? poisson_cell(rho, s_c, i, nx) : 0.f;
+    if (on && row) row[2 * nx + i] = E_new;
+    n = n_new;
+    u = u_new;
+    E = E_new;
+    if (metrics) {
+      MetricAcc m;
+      m.init();
+      if (on) m.add(n, u, E);
+      m.wave_reduce();
+      if (i == 0) {
+        MetricAcc w;  // block_metrics' sum over the workgroup's 4 wave partials
+        w.init();
+        w.energy += m.energy;
+        w.charge += m.charge;
+        w.maxdev = m.maxdev > w.maxdev ? m.maxdev : w.maxdev;
+        w.finite &= m.finite;
+        for (int k = 1; k < kFvThreads / 64; ++k) {
+          w.energy += 0.0;
+          w.charge += 0.0;
+        }
+        w.store(metrics + b * ldM + (int64_t)(t + 1) * HF_NUM_METRICS, nx);
+      }
+    }
+  }
+  if (on) {
+    state_final[b * S + i] = n;
+    state_final[b * S + nx + i] = u;
+    state_final[b * S + 2 * nx + i] = E;
+  }
+}
+
 // hf_poisson at FFT sizes: one wave per pair of ICs, as above.
 template <int N>
 __global__ __launch_bounds__(64 * kFftWaves, 2) void poisson_fft_kernel(const float *__restrict__ n, int ld_n,
@@ -648,13 +724,20 @@ hipError_t fv_run_fft_launch(const float *state0, int64_t ld_s0, float *state_fi
   return hipGetLastError();
 }
 
-bool fv_run_fused(int nx) { return poisson_uses_fft(nx) && nx <= kFvRunMaxNx; }
+bool fv_run_fused(int nx) { return (poisson_uses_fft(nx) && nx <= kFvRunMaxNx) || (nx >= 1 && nx <= kFvSmallMaxNx); }
 
 hipError_t launch_fv_run(const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *pc, int B,
                          int nx, int T, float c, float dt, float nu, float dx2, float *flux_traj, float *metrics,
                          const float *ref, float *mse, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if ((ref == nullptr) != (mse == nullptr)) return hipErrorInvalidValue;
+  if (nx <= kFvSmallMaxNx) {  // contiguous states; no scoring at these nx (the fused hybrid kernel has its twin)
+    if (mse || ld_s0 != 3LL * nx || !state_final) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)((B + kFvThreads / 64 - 1) / (kFvThreads / 64));
+    hipLaunchKernelGGL(fv_run_small_kernel, dim3(grid), dim3(kFvThreads), 0, s, state0, state_final, traj, pc, nx, c,
+                       dt, nu, dx2, flux_traj, metrics, B, T);
+    return hipGetLastError();
+  }
   switch (fv_run_fused(nx) ? nx : 0) {
     case 256: return fv_run_fft_launch<256>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, s);
     case 512: return fv_run_fft_launch<512>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, s);

@@ -174,12 +174,13 @@ def test_classical_run_vs_reference(hf):
     close(r["traj"].cpu().numpy(), g["nx1024_states"], ROLL_ATOL, ROLL_RTOL)
 
 
-@pytest.mark.parametrize("nx", [256, 512, 1024, 2048])
+@pytest.mark.parametrize("nx", [13, 48, 64, 256, 512, 1024, 2048])
 def test_classical_run_fused_equals_steps(hf, nx):
-    """BaselineSolver.run at FFT sizes (src/baseline_solver.py:80-118): the
-    one-launch register-resident rollout (fv_run_fft_kernel, nx <= 1024; 2048
-    stays per-step) equals T per-step launches (hf_step) bit for bit, in every
-    output: trajectory, flux, metrics, final state; odd B leaves a half pair;
+    """BaselineSolver.run (src/baseline_solver.py:80-118): the one-launch
+    register-resident rollouts (fv_run_small_kernel for nx <= 64,
+    fv_run_fft_kernel for FFT nx <= 1024; 2048 stays per-step) equal T
+    per-step launches (hf_step) bit for bit, in every output: trajectory, flux,
+    metrics, final state; odd B leaves a half pair / a partial workgroup;
     state0 aliased with the final state."""
     from hybridflux import engine
     T, B = 12, 7
