@@ -256,7 +256,7 @@ int hf_step(hf_model_t model, const float *dev_state_in, float *dev_state_out,
  * dev_metrics [B][T+1][HF_NUM_METRICS] (may be NULL).
  * For nx in {16,32,48,64} with model != NULL the whole rollout is ONE
  * persistent kernel (state resident on-chip across steps); so is the classical
- * rollout (model == NULL) at nx in {256, 512, 1024}, bit-identical to T
+ * rollout (model == NULL) at nx <= 64 and nx in {256, 512, 1024}, bit-identical to T
  * hf_step calls (HF_FV_PERSIST=0 in the environment selects the per-step
  * launches, for A/B timing).  Otherwise, with
  * model != NULL and B*nx >= 2^21 cells, slices of the batch step on up to 3
