@@ -594,7 +594,7 @@ struct Scratch {
     if (need == 0) return HF_OK;
     if (ws) {
       if (ws_bytes < need)
-        return fail(HF_EINVAL, std::string(fn) + ": workspace smaller than hf_run_workspace_bytes");
+        return fail(HF_EINVAL, std::string(fn) + ": workspace smaller than hf_workspace_need");
       base = static_cast<char *>(ws);
       return HF_OK;
     }
@@ -684,24 +684,83 @@ bool fv_run_persistent() {
   return on;
 }
 
-// lane stream i (1..kMaxLanes-1) of the current device, created on first use
-hipError_t lane_stream(int i, hipStream_t *out) {
+int64_t up256(int64_t v) { return (v + 255) / 256 * 256; }
+
+// The scratch each path actually carves (hf_workspace_need): the fused
+// rollouts and the one-launch classical rollouts take none; the generic run
+// takes two state buffers unless the trajectory is the ping-pong, plus the
+// face flux of the hybrid step; the FFT compare one hybrid trajectory and the
+// flux; the generic compare both trajectories, a state and the flux.
+int64_t need_step(const hf_model *m, int B, int nx, bool has_ff) {
+  if (!m || fused_nx(nx) || has_ff) return 0;
+  return up256(4LL * B * nx);
+}
+int64_t need_run(const hf_model *m, int B, int nx, int T, bool has_traj) {
+  if (B == 0 || T == 0 || (m && fused_nx(nx))) return 0;
+  if (!m && hf::fv_run_fused(nx) && fv_run_persistent()) return 0;
+  return (has_traj ? 0 : 2 * up256(12LL * B * nx)) + (m ? up256(4LL * B * nx) : 0);
+}
+bool compare_fft_twin(int nx) { return hf::poisson_uses_fft(nx) && hf::fv_run_fused(nx) && fv_run_persistent(); }
+int64_t need_compare(int B, int nx, int T) {
+  if (B == 0 || fused_nx(nx)) return 0;
+  const int64_t traj = up256(12LL * B * (T + 1) * nx), flux = up256(4LL * B * nx);
+  if (compare_fft_twin(nx)) return traj + flux;
+  return 2 * traj + up256(12LL * B * nx) + flux;
+}
+
+// Lane streams belong to the caller's stream: lane i (1..kMaxLanes-1) of
+// (current device, caller stream), created on first use.  Calls on different
+// caller streams (other threads, other streams of one thread) therefore never
+// share a lane, so they do not serialise through each other's lanes, and a
+// graph capture of one caller stream pulls only that stream's own lanes into
+// capture mode.  Calls on one caller stream are ordered by that stream anyway.
+// At most kMaxLaneOwners caller streams get lanes; later ones run one lane.
+constexpr int kMaxLaneOwners = 256;
+
+struct LaneSet {
+  int dev;
+  hipStream_t owner;
+  hipStream_t lane[kMaxLanes];
+};
+
+hipError_t lane_streams(hipStream_t caller, int lanes, hipStream_t *out, bool *granted) {
   static std::mutex mu;
-  static hipStream_t streams[64][kMaxLanes] = {};
+  static std::vector<LaneSet> sets;
+  *granted = false;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lock(mu);
-  if (!streams[dev][i]) {
-    e = hipStreamCreateWithFlags(&streams[dev][i], hipStreamNonBlocking);
-    if (e != hipSuccess) return e;
+  LaneSet *ls = nullptr;
+  for (auto &x : sets)
+    if (x.dev == dev && x.owner == caller) ls = &x;
+  if (!ls) {
+    if ((int)sets.size() >= kMaxLaneOwners) return hipSuccess;
+    sets.push_back(LaneSet{dev, caller, {}});
+    ls = &sets.back();
   }
-  *out = streams[dev][i];
+  for (int i = 1; i < lanes; ++i) {
+    if (!ls->lane[i]) {
+      e = hipStreamCreateWithFlags(&ls->lane[i], hipStreamNonBlocking);
+      if (e != hipSuccess) return e;
+    }
+    out[i] = ls->lane[i];
+  }
+  *granted = true;
   return hipSuccess;
 }
 
 }  // namespace
+
+int64_t hf_workspace_need(hf_model_t m, int op, int B, int nx, int T, int flags) {
+  if (B < 0 || nx < 1 || T < 0 || op < HF_OP_STEP || op > HF_OP_COMPARE) return -1;
+  if (flags & ~(HF_WS_TRAJ | HF_WS_FLUX_FACE)) return -1;
+  switch (op) {
+    case HF_OP_STEP: return need_step(m, B, nx, flags & HF_WS_FLUX_FACE);
+    case HF_OP_RUN: return need_run(m, B, nx, T, flags & HF_WS_TRAJ);
+    default: return m ? need_compare(B, nx, T) : -1;
+  }
+}
 
 int hf_step(hf_model_t m, const float *in, float *out, const float *x, const double *pc, int B, int nx,
             float c, float dt, float nu, float dx2, float *ff, float *metrics, void *ws, int64_t ws_bytes,
@@ -727,7 +786,7 @@ int hf_step(hf_model_t m, const float *in, float *out, const float *x, const dou
     return HF_OK;
   }
   Scratch sc;
-  if (int rc = sc.init(ws, ws_bytes, ff ? 0 : hf_run_workspace_bytes(HF_OP_STEP, B, nx, 1), s, "hf_step"))
+  if (int rc = sc.init(ws, ws_bytes, need_step(m, B, nx, ff != nullptr), s, "hf_step"))
     return rc;
   float *F = ff ? ff : sc.take(sizeof(float) * (int64_t)B * nx);
   HF_CHECK_HIP(hf::launch_chain_flux(m->chain, nullptr, in, 3LL * nx, x, B, nx, nullptr, F, s), "hf_step(flux)");
@@ -778,7 +837,7 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   // scratch: two state buffers unless the trajectory is the ping-pong, the face flux for the hybrid step
   const int64_t sbytes = (sizeof(float) * B * S + 255) / 256 * 256, fbytes = (sizeof(float) * B * nx + 255) / 256 * 256;
   Scratch sc;
-  if (int rc = sc.init(ws, ws_bytes, (traj ? 0 : 2 * sbytes) + (m ? fbytes : 0), s, "hf_run")) return rc;
+  if (int rc = sc.init(ws, ws_bytes, need_run(m, B, nx, T, traj != nullptr), s, "hf_run")) return rc;
   float *buf0 = nullptr, *buf1 = nullptr;
   if (!traj) buf0 = sc.take(sbytes), buf1 = sc.take(sbytes);
   float *F = m ? sc.take(fbytes) : nullptr;
@@ -798,7 +857,14 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   }
   // lane i steps ICs [B*i/lanes, B*(i+1)/lanes); lane 0 on the caller's stream
   hipStream_t ls[kMaxLanes] = {s};
-  for (int i = 1; i < lanes; ++i) HF_CHECK_HIP(lane_stream(i, &ls[i]), "hf_run lane stream");
+  bool granted = false;
+  HF_CHECK_HIP(lane_streams(s, lanes, ls, &granted), "hf_run lane stream");
+  if (!granted) {
+    HF_CHECK_HIP(run_steps(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics, buf0,
+                           buf1, F, s),
+                 "hf_run");
+    return HF_OK;
+  }
   hipEvent_t fork = nullptr, join[kMaxLanes] = {};
   for (int i = 1; i < lanes; ++i) {
     hipError_t ce = hipEventCreateWithFlags(&join[i], hipEventDisableTiming);
@@ -856,13 +922,13 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
                  "hf_run_compare(fused)");
     return HF_OK;
   }
-  if (hf::poisson_uses_fft(nx) && hf::fv_run_fused(nx) && fv_run_persistent()) {
+  if (compare_fft_twin(nx)) {
     // FFT nx <= 1024: the hybrid rollout first, recording its trajectory; then
     // the classical twin as one launch from that trajectory's row 0 (state0,
     // also when state_final aliases it), scoring each step against the hybrid
     // row as it goes: no classical trajectory, no MSE pass.  Same bits as below.
     Scratch sc;
-    if (int rc = sc.init(ws, ws_bytes, hf_run_workspace_bytes(HF_OP_COMPARE, B, nx, T), s, "hf_run_compare"))
+    if (int rc = sc.init(ws, ws_bytes, need_compare(B, nx, T), s, "hf_run_compare"))
       return rc;
     const int64_t S = 3LL * nx, ldT = (T + 1) * S;
     float *th = sc.take(sizeof(float) * (int64_t)B * ldT);
@@ -882,7 +948,7 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
   // classical twin runs first: state_final may alias state0, and the hybrid
   // run is the one that writes it.
   Scratch sc;
-  if (int rc = sc.init(ws, ws_bytes, hf_run_workspace_bytes(HF_OP_COMPARE, B, nx, T), s, "hf_run_compare"))
+  if (int rc = sc.init(ws, ws_bytes, need_compare(B, nx, T), s, "hf_run_compare"))
     return rc;
   const int64_t traj_bytes = sizeof(float) * (int64_t)B * (T + 1) * 3 * nx;
   float *th = sc.take(traj_bytes), *tc = sc.take(traj_bytes), *fin_c = sc.take(sizeof(float) * (int64_t)B * 3 * nx);

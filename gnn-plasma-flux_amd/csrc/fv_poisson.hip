@@ -266,8 +266,10 @@ __device__ __forceinline__ void fv_finish_lane(float *__restrict__ so, const dou
   }
 }
 
+// N = 2048: the wave-private LDS (4 x 2176 double2, ~139 KB) admits one
+// workgroup per CU, so a min-blocks hint of 2 would only cap the VGPRs.
 template <bool HYBRID, int N>
-__global__ __launch_bounds__(64 * kFftWaves, 2) void fv_step_fft_kernel(
+__global__ __launch_bounds__(64 * kFftWaves, N >= 2048 ? 1 : 2) void fv_step_fft_kernel(
     const float *__restrict__ in, int64_t ld_in, float *__restrict__ out, int64_t ld_out,
     const float *__restrict__ face_flux, const double *__restrict__ pc, float c, float dt, float nu, float dx2,
     float *__restrict__ flux_out, int64_t ld_flux, float *__restrict__ metrics, int64_t ld_metrics, int B) {
@@ -570,7 +572,7 @@ __global__ __launch_bounds__(kFvThreads) void fv_run_small_kernel(const float *s
 
 // hf_poisson at FFT sizes: one wave per pair of ICs, as above.
 template <int N>
-__global__ __launch_bounds__(64 * kFftWaves, 2) void poisson_fft_kernel(const float *__restrict__ n, int ld_n,
+__global__ __launch_bounds__(64 * kFftWaves, N >= 2048 ? 1 : 2) void poisson_fft_kernel(const float *__restrict__ n, int ld_n,
                                                                      float *__restrict__ E, int ld_E,
                                                                      const double *__restrict__ pc, int B) {
   constexpr int V = N / 64;

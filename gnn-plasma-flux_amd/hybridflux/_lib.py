@@ -25,6 +25,8 @@ HF_NUM_SUMMARY = 8
 HF_OP_STEP = 0
 HF_OP_RUN = 1
 HF_OP_COMPARE = 2
+HF_WS_TRAJ = 1
+HF_WS_FLUX_FACE = 2
 
 # name -> (restype, argtypes); mirrors include/hybridflux.h exactly.
 SIGNATURES = {
@@ -59,6 +61,7 @@ SIGNATURES = {
     "hf_poisson_coeffs": (c_int, [c_int, c_double, c_void_p]),
     "hf_poisson": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p]),
     "hf_run_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int]),
+    "hf_workspace_need": (c_int64, [c_void_p, c_int, c_int, c_int, c_int, c_int]),
     "hf_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                         c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "hf_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,

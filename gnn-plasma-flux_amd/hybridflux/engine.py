@@ -136,12 +136,19 @@ def _state(t, nx):
     return t.contiguous()
 
 
-def workspace(op, B, nx, T, dev, given=None):
+def workspace(op, B, nx, T, dev, given=None, model=None, traj=False, flux_face=False):
     """Scratch for the generic (non-fused) sequencing of hf_step / hf_run /
     hf_run_compare: the caller's uint8 device tensor (checked), or one from
     torch's stream-ordered caching allocator, so no hipMalloc runs inside a
-    rollout.  Returns (tensor or None, bytes)."""
-    nbytes = int(lib().hf_run_workspace_bytes(op, B, nx, T))
+    rollout.  Sized by hf_workspace_need for this path: `model` is the
+    DeviceModel (None = classical), `traj` / `flux_face` whether the call gets
+    a trajectory / face-flux buffer.  Paths that need no scratch (the fused
+    rollouts, the one-launch classical rollouts) get None.  Returns (tensor or
+    None, bytes)."""
+    flags = (_lib.HF_WS_TRAJ if traj is not False and traj is not None else 0) | \
+            (_lib.HF_WS_FLUX_FACE if flux_face is not False and flux_face is not None else 0)
+    handle = model.handle if model is not None else None
+    nbytes = int(lib().hf_workspace_need(handle, op, B, nx, T, flags))
     if nbytes < 0:
         raise ValueError(f"bad workspace query (op={op}, B={B}, nx={nx}, T={T})")
     if given is not None:
@@ -161,7 +168,7 @@ def step(model, grid, state, flux_face=False, metrics=False, ws=None):
     F = torch.empty(B, grid.nx, device=dev) if flux_face else None
     M = torch.empty(B, HF_NUM_METRICS, device=dev) if metrics else None
     x, pc = grid.on(dev)
-    w, wb = workspace(HF_OP_STEP, B, grid.nx, 1, dev, ws)
+    w, wb = workspace(HF_OP_STEP, B, grid.nx, 1, dev, ws, model=model, flux_face=flux_face)
     with torch.cuda.device(dev):
         check(lib().hf_step(model.handle if model else None, ptr(state), ptr(out), ptr(x), ptr(pc), B,
                             grid.nx, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(F), ptr(M), ptr(w), wb,
@@ -191,7 +198,7 @@ def run(model, grid, state0, T, traj=True, flux=False, metrics=False, out=None, 
     fl = _buf(flux, flux, (B, T, grid.nx), dev)
     me = _buf(metrics, metrics, (B, T + 1, HF_NUM_METRICS), dev)
     x, pc = grid.on(dev)
-    w, wb = workspace(HF_OP_RUN, B, grid.nx, T, dev, ws)
+    w, wb = workspace(HF_OP_RUN, B, grid.nx, T, dev, ws, model=model, traj=tr)
     with torch.cuda.device(dev):
         check(lib().hf_run(model.handle if model else None, ptr(state0), ptr(final), ptr(x), ptr(pc), B,
                            grid.nx, T, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(tr), ptr(fl),
@@ -211,7 +218,7 @@ def run_compare(model, grid, state0, T, metrics=True, out=None, ws=None):
     me = torch.empty(B, T + 1, HF_NUM_METRICS, device=dev) if metrics else None
     mc = torch.empty(B, T + 1, HF_NUM_METRICS, device=dev) if metrics else None
     x, pc = grid.on(dev)
-    w, wb = workspace(HF_OP_COMPARE, B, grid.nx, T, dev, ws)
+    w, wb = workspace(HF_OP_COMPARE, B, grid.nx, T, dev, ws, model=model)
     with torch.cuda.device(dev):
         check(lib().hf_run_compare(model.handle, ptr(state0), ptr(final), ptr(x), ptr(pc), B, grid.nx, T,
                                    grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(mse), ptr(me), ptr(mc),

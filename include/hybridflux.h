@@ -214,7 +214,8 @@ int hf_poisson(const float *dev_n, int ld_n, float *dev_E, int ld_E,
 /*
  * Scratch of the generic (non-fused) sequencing.  hf_step, hf_run and
  * hf_run_compare take (dev_workspace, workspace_bytes): a device buffer of at
- * least hf_run_workspace_bytes(op, B, nx, T) bytes that the call may use as
+ * least hf_workspace_need(model, op, B, nx, T, flags) bytes (or the upper
+ * bound hf_run_workspace_bytes(op, B, nx, T)) that the call may use as
  * scratch until the work it enqueued has run; the caller keeps it alive and
  * unshared until then.  dev_workspace == NULL makes the call allocate its
  * scratch stream-ordered (hipMallocAsync / hipFreeAsync on `stream`).  The
@@ -223,7 +224,17 @@ int hf_poisson(const float *dev_n, int ld_n, float *dev_E, int ld_E,
 #define HF_OP_STEP 0
 #define HF_OP_RUN 1
 #define HF_OP_COMPARE 2
+/* An upper bound over every model, nx path and output choice of `op`. */
 int64_t hf_run_workspace_bytes(int op, int B, int nx, int T);
+/* The exact scratch the call will carve for this model (NULL = classical;
+ * HF_OP_COMPARE needs a model), nx path and outputs: flags HF_WS_TRAJ when the
+ * call is given dev_traj (hf_run), HF_WS_FLUX_FACE when given dev_flux_face
+ * (hf_step).  0 on every path that needs no scratch (the fused rollouts, the
+ * one-launch classical rollouts); -1 on bad arguments.  A dev_workspace of at
+ * least this many bytes is accepted by the call; a smaller one is HF_EINVAL. */
+#define HF_WS_TRAJ 1
+#define HF_WS_FLUX_FACE 2
+int64_t hf_workspace_need(hf_model_t model, int op, int B, int nx, int T, int flags);
 
 /*
  * One timestep for B ICs (state_in -> state_out, may not alias).
@@ -263,7 +274,9 @@ int hf_step(hf_model_t model, const float *dev_state_in, float *dev_state_out,
  * library-owned lane streams forked from and joined back into `stream` with
  * events (HF_RUN_LANES=1..4 in the environment overrides the count): the call
  * stays ordered on `stream` (and capturable), and every IC's result is
- * bit-identical to the one-stream sequencing.
+ * bit-identical to the one-stream sequencing.  The lane streams belong to
+ * (device, `stream`): calls on different streams or threads never share a
+ * lane, and capturing `stream` draws in only its own lanes.
  */
 int hf_run(hf_model_t model, const float *dev_state0, float *dev_state_final,
            const float *dev_x, const double *dev_c, int B, int nx, int T,
@@ -287,8 +300,10 @@ int hf_run(hf_model_t model, const float *dev_state0, float *dev_state_final,
  * For nx in {256, 512, 1024} (model not fused) the hybrid rollout runs first and
  * the classical twin is one launch that scores each step against the hybrid
  * trajectory as it goes; the results equal the recorded-trajectory path bit
- * for bit.  dev_workspace, if given, is sized by hf_run_workspace_bytes(
- * HF_OP_COMPARE, ...) for every nx.
+ * for bit.  dev_workspace, if given, is sized by hf_workspace_need(model,
+ * HF_OP_COMPARE, ...): 0 at the fused nx, one hybrid trajectory plus the face
+ * flux at nx in {256, 512, 1024}, two trajectories, a state and the flux
+ * otherwise.
  */
 int hf_run_compare(hf_model_t model, const float *dev_state0, float *dev_state_final,
                    const float *dev_x, const double *dev_c, int B, int nx, int T,

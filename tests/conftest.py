@@ -38,6 +38,42 @@ def pytest_sessionfinish(session, exitstatus):
             json.dump(_RECORDED, f, indent=1, sort_keys=True)
 
 
+_CTX = {"test": None, "n": 0}
+
+
+@pytest.fixture(autouse=True)
+def _parity_context(request):
+    """Names the running test for close()'s automatic error records."""
+    _CTX["test"] = request.node.nodeid.split("::", 1)[-1]
+    _CTX["n"] = 0
+    yield
+
+
+def close(a, b, atol, rtol=0.0, what=None):
+    """Assert |a - b| <= atol + rtol |b| elementwise (a finite), and record the
+    measured max |a - b| and its largest fraction of the tolerance under the
+    running test (the $HF_PARITY_RECORD file): every gated comparison carries
+    its margin.  Returns the max |a - b|."""
+    if hasattr(a, "detach"):
+        a = a.detach().cpu().numpy()
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = np.abs(a.astype(np.float64) - b)
+    lim = atol + rtol * np.abs(b)
+    _CTX["n"] += 1
+    key = what or f"check{_CTX['n']}"
+    if err.size and _CTX["test"]:
+        rec = _RECORDED.setdefault(_CTX["test"], {})
+        rec[f"{key}_max_abs"] = float(np.nanmax(err)) if np.isfinite(err).any() else float("nan")
+        with np.errstate(divide="ignore", invalid="ignore"):
+            frac = np.where(lim > 0, err / np.where(lim > 0, lim, 1), np.where(err > 0, np.inf, 0.0))
+        rec[f"{key}_frac_of_tol"] = float(np.nanmax(frac))
+        rec[f"{key}_tol"] = f"atol {atol:.1e} + rtol {rtol:.1e}"
+    assert np.isfinite(a).all()
+    assert (err <= lim).all(), f"max err {err.max():.3e} (limit {atol:.1e}+{rtol:.1e}|ref|)"
+    return float(err.max()) if err.size else 0.0
+
+
 def golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 

@@ -1,0 +1,69 @@
+"""One rank of the IC-sharded rollout on the HIP path (tests/test_gpu_distributed.py).
+
+Run as a plain process (one rank) or under torch.distributed.run (N ranks,
+backend gloo, every rank on cuda:0 of a one-GPU box).  Each rank takes its
+contiguous shard of the seeds (hybridflux.rollout.shard_seeds), runs it through
+the real HybridSolver (run_batch and compare_batch), and the shard results are
+exchanged exactly as bench.py does at N > 1 (gather_rollout: device summary
+kernel + all_gather of the metric series and summaries); the final states are
+gathered with gather_ic_rows.  Rank 0 writes everything to OUT.npz.
+The reference workload is scripts/evaluation/evaluate_multi_ic.py:106-138.
+
+    python tests/dist_rollout_worker.py OUT.npz
+    python -m torch.distributed.run --nproc-per-node 2 ... tests/dist_rollout_worker.py OUT.npz
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "gnn-plasma-flux_amd"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+# (label, n_total, nx, T, precision, weights): the fused nx = 64 rollout
+# (cfg5's per-rank kernel) and the generic two-launch sequencing (nx = 256)
+CASES = [("fused64_f32", 37, 64, 12, "f32", "W1_r2"),
+         ("generic256_bf16", 9, 256, 6, "bf16", "W1_r2")]
+
+
+def main(out):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("gloo")
+    from hybridflux import HybridSolver
+    from hybridflux.rollout import gather_ic_rows, gather_rollout, max_over_ranks, shard_seeds
+
+    res = {"world": np.int64(world)}
+    for label, n_total, nx, T, prec, w in CASES:
+        weights = dict(np.load(os.path.join(ROOT, "tests", "golden", f"weights_{w}.npz"), allow_pickle=False))
+        solver = HybridSolver(weights, radius=2, nx=nx, dt=5e-3 * 64.0 / nx, device=dev, precision=prec)
+        ics = solver.baseline.initial_conditions(shard_seeds(1000, n_total, world, rank), as_tensor=True)
+        run = solver.run_batch(ics, T, traj=False, metrics=True)
+        g = gather_rollout(run, n_total)
+        fin = gather_ic_rows(run["final"], n_total)
+        cmp = solver.compare_batch(ics, T)
+        gc = gather_rollout(cmp, n_total)
+        torch.cuda.synchronize(dev)
+        res[f"{label}/metrics"] = g["metrics"].cpu().numpy()
+        res[f"{label}/summary"] = g["summary"].cpu().numpy()
+        res[f"{label}/final"] = fin.cpu().numpy()
+        res[f"{label}/cmp_mse"] = gc["mse"].cpu().numpy()
+        res[f"{label}/cmp_summary"] = gc["summary"].cpu().numpy()
+        res[f"{label}/local_n"] = np.int64(ics.shape[0])
+    res["max_over_ranks"] = np.float64(max_over_ranks(float(rank + 1)))
+    if rank == 0:
+        np.savez(out, **res)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

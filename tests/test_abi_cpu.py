@@ -168,3 +168,20 @@ def test_training_entry_points_validate_before_device():
                                  None) == _lib.HF_EINVAL
     assert lib.hf_graph_forward_train(dummy, 4, 16, 2, dummy, 0, dummy, 4, 0, dummy, dummy, None) == _lib.HF_EINVAL
     assert P > 0
+
+
+def test_workspace_need_classical():
+    """hf_workspace_need is a host-side size query: exact per path, -1 on bad arguments."""
+    from hybridflux._lib import HF_OP_COMPARE, HF_OP_RUN, HF_OP_STEP
+    L = _lib.lib()
+    assert L.hf_workspace_need(None, HF_OP_RUN, 7, 64, 3, 0) == 0        # one-launch classical rollout
+    assert L.hf_workspace_need(None, HF_OP_RUN, 7, 1024, 3, 0) == 0
+    assert L.hf_workspace_need(None, HF_OP_RUN, 7, 100, 3, 0) == 2 * ((12 * 7 * 100 + 255) // 256 * 256)
+    assert L.hf_workspace_need(None, HF_OP_STEP, 7, 100, 1, 0) == 0
+    assert L.hf_workspace_need(None, HF_OP_COMPARE, 7, 100, 3, 0) == -1   # compare needs a model
+    assert L.hf_workspace_need(None, HF_OP_RUN, 7, 100, 3, 4) == -1       # unknown flag
+
+
+    assert L.hf_workspace_need(None, HF_OP_RUN, 7, 100, 0, 0) == 0          # T = 0 copies only
+    for op in (HF_OP_STEP, HF_OP_RUN, HF_OP_COMPARE):                         # the bound covers the exact need
+        assert L.hf_run_workspace_bytes(op, 7, 100, 3) >= max(L.hf_workspace_need(None, op, 7, 100, 3, 0), 0)

@@ -13,18 +13,11 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import close, golden
 from oracle import hybrid_oracle as O
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-
-
-def close(a, b, atol, rtol):
-    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
-    err = np.abs(a.astype(np.float64) - b)
-    lim = atol + rtol * np.abs(b)
-    assert (err <= lim).all(), float((err - lim).max())
 
 
 @pytest.fixture(scope="module")

@@ -1,0 +1,75 @@
+"""cfg5's data path with more than one rank, on the HIP kernels (BASELINE.json
+configs[4]; reference workload scripts/evaluation/evaluate_multi_ic.py:106-138).
+
+Two rank processes share the box's one GPU over gloo (RCCL needs a GPU per
+rank; the 8-GPU RCCL run is the driver's).  Each runs its IC shard through
+HybridSolver and the end-of-rollout exchange bench.py uses (gather_rollout:
+device summary kernel + all_gather).  The gathered metric series, summaries,
+final states and the compare path's MSE must equal a one-rank run of the same
+seeds bit for bit: IC sharding changes no arithmetic.  Then bench.py itself,
+launched plainly with --gpus 2, must start its two ranks and report them.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "dist_rollout_worker.py")
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def _run(cmd, timeout):
+    p = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    assert p.returncode == 0, f"{cmd}\nrc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    return p
+
+
+@pytest.mark.timeout(400)
+def test_two_ranks_equal_one_rank_bitwise(tmp_path):
+    one, two = tmp_path / "one.npz", tmp_path / "two.npz"
+    _run([sys.executable, WORKER, str(one)], 200)
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(two)], 300)
+    a, b = np.load(one), np.load(two)
+    assert int(a["world"]) == 1 and int(b["world"]) == 2
+    assert float(b["max_over_ranks"]) == 2.0
+    for label in ("fused64_f32", "generic256_bf16"):
+        for key in ("metrics", "summary", "final", "cmp_mse", "cmp_summary"):
+            x, y = a[f"{label}/{key}"], b[f"{label}/{key}"]
+            assert x.shape == y.shape, (label, key, x.shape, y.shape)
+            assert np.isfinite(x).all() or key.endswith("summary")
+            # bitwise (NaN-safe): the same ICs, the same kernels, gathered in global IC order
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (label, key)
+    # the ragged shards: rank 0 holds ceil(n/2) ICs
+    assert int(b["fused64_f32/local_n"]) == 19 and int(b["generic256_bf16/local_n"]) == 5
+
+
+@pytest.mark.timeout(400)
+def test_bench_self_launches_ranks():
+    """`python bench.py --gpus 2` without a launcher starts 2 ranks itself."""
+    p = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+              "--steps", "4", "--warmup", "2", "--no-cpu-baseline", "--no-other-configs", "--also", ""], 300)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_ics"] == 8192 and d["config"]["ics_per_gpu"] == 4096
+    assert d["finite_fraction"] == 1.0 and d["value"] > 0
+    assert "gloo" in d["config"]["collective"]

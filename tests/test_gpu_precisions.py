@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden, rand_sd
+from conftest import close, golden, rand_sd
 from oracle import hybrid_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -23,15 +23,6 @@ DEV = "cuda:0"
 def hf():
     import hybridflux
     return hybridflux
-
-
-def close(a, b, atol, rtol=0.0):
-    a, b = np.asarray(a), np.asarray(b)
-    assert a.shape == b.shape, (a.shape, b.shape)
-    err = np.abs(a.astype(np.float64) - b)
-    assert np.isfinite(a).all()
-    assert (err <= atol + rtol * np.abs(b)).all(), f"max err {err.max():.3e}"
-    return float(err.max())
 
 
 def weights(name):

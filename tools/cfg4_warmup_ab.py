@@ -26,7 +26,7 @@ def main():
     solver = HybridSolver(os.path.join(ROOT, "tests", "golden", "weights_W1_r2.npz"), radius=2, nx=nx, dt=dt,
                           device=dev, precision="bf16")
     ics = solver.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True)
-    ws, _ = engine.workspace(HF_OP_RUN, B, nx, T, dev)
+    ws, _ = engine.workspace(HF_OP_RUN, B, nx, T, dev, model=solver._dm())
     final = torch.empty_like(ics)
     met = torch.empty(B, T + 1, 4, device=dev)
     stream = torch.cuda.current_stream(dev)

@@ -10,7 +10,7 @@ dev = torch.device("cuda", 0)
 w = dict(np.load("tests/golden/weights_W1_r3.npz"))
 s = HybridSolver(w, radius=3, device=dev)
 ics = s.baseline.initial_conditions(range(1000, 1000 + 4096), as_tensor=True)
-ws, _ = engine.workspace(HF_OP_RUN, 4096, 64, 20, dev)
+ws, _ = engine.workspace(HF_OP_RUN, 4096, 64, 20, dev, model=s._dm(), traj=True)
 s.run_batch(ics, 5, traj=True, metrics=True, ws=ws)
 torch.cuda.synchronize()
 tr = torch.empty(4096, 21, 3, 64, device=dev); me = torch.empty(4096, 21, 4, device=dev); fin = torch.empty_like(ics)

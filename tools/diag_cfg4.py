@@ -38,7 +38,7 @@ def main():
                           device=dev, precision="bf16")
     s0 = solver.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True)
     grid = engine.Grid(nx, dt=dt)
-    ws, _ = engine.workspace(HF_OP_RUN, B, nx, T, dev)
+    ws, _ = engine.workspace(HF_OP_RUN, B, nx, T, dev, model=solver._dm())
     fin = torch.empty_like(s0)
     cells = B * nx * T
     out = {"build": version(), "T": T, "B": B}

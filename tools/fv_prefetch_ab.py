@@ -21,7 +21,7 @@ def main(nx=1024, B=4096, n=20):
     w = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r2.npz"), allow_pickle=False))
     s = HybridSolver(w, radius=2, nx=nx, dt=3.125e-4, device=dev, precision="bf16")
     st = s.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True).contiguous()
-    ws = engine.workspace(engine.HF_OP_STEP, B, nx, 1, dev)[0]
+    ws = engine.workspace(engine.HF_OP_STEP, B, nx, 1, dev, model=s._dm())[0]
     for _ in range(n):
         engine.step(s._dm(), s.grid, st, ws=ws)
         engine.step(None, s.grid, st, ws=ws)

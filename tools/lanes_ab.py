@@ -32,7 +32,7 @@ def main():
     for prec in os.environ.get("LANES_AB_PREC", "bf16,f32,f16x3").split(","):
         solver = HybridSolver(w, radius=2, nx=nx, dt=dt, device=dev, precision=prec)
         ics = solver.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True)
-        ws, _ = engine.workspace(HF_OP_RUN, B, nx, T, dev)
+        ws, _ = engine.workspace(HF_OP_RUN, B, nx, T, dev, model=solver._dm())
         final = torch.empty_like(ics)
         met = torch.empty(B, T + 1, 4, device=dev)
         solver.run_batch(ics, T, traj=False, metrics=met, out=final, ws=ws)

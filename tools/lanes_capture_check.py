@@ -13,7 +13,7 @@ solver = HybridSolver(w, radius=2, nx=nx, dt=3.125e-4, device=dev, precision="bf
 ics = solver.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True)
 ref = engine.run(m, grid, ics, T, traj=False)["final"].clone()
 out = torch.empty_like(ics)
-ws, _ = engine.workspace(1, B, nx, T, dev)
+ws, _ = engine.workspace(1, B, nx, T, dev, model=m)
 s = torch.cuda.Stream(dev)
 s.wait_stream(torch.cuda.current_stream(dev))
 with torch.cuda.stream(s):
