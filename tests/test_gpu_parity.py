@@ -2,11 +2,19 @@
 the reference and against the CPU oracle on the same seeded inputs.
 
 Tolerances (float32 everywhere; the kernels sum in a different order than
-the CPU BLAS, which the reference itself differs from fp64 by ~4e-7):
-  edge / face fluxes, one evaluation ............ atol 2e-6
-  Poisson E ..................................... atol 1e-7
-  classical FV update (n, u), one step ........... bit-exact
-  states after a 30-step rollout ................. atol 1e-5 + rtol 1e-5
+the CPU BLAS, which the reference itself differs from fp64 by ~4e-7).  Each
+gate is 2-5x the error measured on MI355X (every run records them through
+conftest.close into $HF_PARITY_RECORD; profiles/r03_*_parity_errors.json):
+  edge / face fluxes, one evaluation ..... atol 2e-6         (measured <= 5.1e-7)
+  Poisson E .............................. atol 1e-7         (measured <= 1.5e-8: the
+      gate is one float32 ulp at |E| ~ 1 (1.2e-7), below which a correctly
+      rounded value may still differ from the reference's by one ulp)
+  classical FV update (n, u), one step ... bit-exact
+  classical 30-step rollout .............. atol 5e-7         (measured <= 1.2e-7)
+  hybrid states, 12..30-step rollouts .... atol 2e-6 + rtol 2e-6 (measured <= 7.8e-7)
+  metrics of a rollout ................... energy atol 1e-8, charge atol 2e-7
+                                           (measured 1.9e-9, 5.6e-8)
+  per-step MSE vs the classical twin ..... rtol 2e-5         (measured <= 4.2e-6 relative)
 """
 import numpy as np
 import pytest
@@ -19,7 +27,8 @@ pytestmark = pytest.mark.gpu
 
 FLUX_ATOL = 2e-6
 E_ATOL = 1e-7
-ROLL_ATOL, ROLL_RTOL = 1e-5, 1e-5
+ROLL_ATOL, ROLL_RTOL = 2e-6, 2e-6
+CLASSICAL_ATOL = 5e-7
 DEV = "cuda:0"
 
 
@@ -156,13 +165,13 @@ def test_classical_run_vs_reference(hf):
     g = golden("classical.npz")
     s = hf.BaselineSolver(64, device=DEV)
     states, fluxes = s.run(g["seed0_states"][0], n_steps=30)    # config 1 path
-    close(states, g["seed0_states"], ROLL_ATOL, ROLL_RTOL)
-    close(fluxes, g["seed0_fluxes"], ROLL_ATOL, ROLL_RTOL)
+    close(states, g["seed0_states"], CLASSICAL_ATOL)
+    close(fluxes, g["seed0_fluxes"], CLASSICAL_ATOL)
     r = s.run_batch(g["b16_states"][:, 0], 30, flux=True)
-    close(r["traj"].cpu().numpy(), g["b16_states"], ROLL_ATOL, ROLL_RTOL)
+    close(r["traj"].cpu().numpy(), g["b16_states"], CLASSICAL_ATOL)
     s1k = hf.BaselineSolver(1024, dt=3.125e-4, device=DEV)
     r = s1k.run_batch(g["nx1024_states"][:, 0], 30)
-    close(r["traj"].cpu().numpy(), g["nx1024_states"], ROLL_ATOL, ROLL_RTOL)
+    close(r["traj"].cpu().numpy(), g["nx1024_states"], CLASSICAL_ATOL)
 
 
 @pytest.mark.parametrize("nx", [13, 48, 64, 256, 512, 1024, 2048])
@@ -205,11 +214,11 @@ def test_hybrid_rollout_vs_reference(hf, w):
     close(traj, h["states"], ROLL_ATOL, ROLL_RTOL)
     # flux of step t is the symmetrised GNN flux of the reference state t
     F_ref = 0.5 * (h["flux_edge"][..., :64] + h["flux_edge"][..., 64:]).astype(np.float32)
-    close(out["flux"].cpu().numpy(), F_ref, 5e-6, 1e-5)
+    close(out["flux"].cpu().numpy(), F_ref, FLUX_ATOL)
     energy, charge, finite = O.rollout_metrics(traj)
     m = out["metrics"].cpu().numpy()
-    close(m[..., 0], energy, 1e-6, 1e-6)
-    close(m[..., 1], charge, 1e-6, 1e-6)
+    close(m[..., 0], energy, 1e-8)
+    close(m[..., 1], charge, 2e-7)
     assert (m[..., 2] == finite).all()
 
 
@@ -218,7 +227,7 @@ def test_hybrid_numpy_api_step_and_run(hf):
     solver = hf.HybridSolver(weights("W1_r1"), radius=1, device=DEV)
     s1 = solver.step(h["states"][0, 0])
     assert s1.shape == (3, 64) and s1.dtype == np.float32
-    close(s1, h["states"][0, 1], 1e-6, 1e-6)
+    close(s1, h["states"][0, 1], 1e-7)  # one step: measured 1.5e-8
     traj = solver.run(h["states"][0, 0], n_steps=30)
     assert traj.shape == (31, 3, 64)
     close(traj, h["states"][0], ROLL_ATOL, ROLL_RTOL)
@@ -438,13 +447,13 @@ def test_compare_vs_oracle(hf, nx, precision):
     out = solver.compare_batch(ics, 20)
     got = out["mse"].cpu().numpy()
     assert got.shape == (3, 21, 3) and (got[:, 0] == 0).all()
-    close(got, want, 1e-9, 2e-3)
+    close(got, want, 1e-12, 2e-5)
     e, q, f = O.rollout_metrics(Sc)
     mc = out["metrics_classical"].cpu().numpy()
-    close(mc[..., 0], e, 1e-6, 1e-6)
-    close(mc[..., 1], q, 1e-6, 1e-6)
+    close(mc[..., 0], e, 1e-8)
+    close(mc[..., 1], q, 2e-7)
     per_ic = got.sum(-1).mean(-1)                                        # evaluate_multi_ic.py:91-94
-    close(per_ic, want.sum(-1).mean(-1), 1e-9, 2e-3)
+    close(per_ic, want.sum(-1).mean(-1), 1e-12, 2e-5)
 
 
 @pytest.mark.parametrize("nx", [256, 512, 1024])
@@ -482,9 +491,9 @@ def test_generate_dataset_vs_oracle(hf, tmp_path):
     assert sorted(d.files) == sorted(["state_t", "flux_t", "state_next", "x", "dt", "dx", "nu"])
     G = O.Grid(64)
     S, F = O.classical_run(G, np.stack([O.initial_condition(G, s) for s in range(3)]), 7)
-    close(d["state_t"], S[:, :-1].reshape(21, 3, 64), 1e-5, 1e-5)
-    close(d["state_next"], S[:, 1:].reshape(21, 3, 64), 1e-5, 1e-5)
-    close(d["flux_t"], F.reshape(21, 64), 1e-5, 1e-5)
+    close(d["state_t"], S[:, :-1].reshape(21, 3, 64), CLASSICAL_ATOL)
+    close(d["state_next"], S[:, 1:].reshape(21, 3, 64), CLASSICAL_ATOL)
+    close(d["flux_t"], F.reshape(21, 64), CLASSICAL_ATOL)
     assert np.array_equal(d["x"], G.x.astype(np.float32)) and float(d["dx"]) == G.dx
     # first step of every IC: F of step 0 and n of step 1 are bit-exact (u of step 1
     # carries dt*E of the IC, whose E is the device Poisson solve: within E_ATOL)
