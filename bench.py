@@ -229,6 +229,10 @@ def main():
     warm_met = torch.empty(B, Wr + 1, 4, device=dev)
     warm_final = torch.empty_like(ics)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if os.environ.get("HF_BENCH_TOUCH", "0") == "1":  # A/B only: first-touch the output buffers before the warmup
+        for t in (final, traj_buf, met_buf):
+            if t is not None:
+                t.zero_()
     torch.cuda.synchronize(dev)
 
     # warmup: one rollout of W steps (compiles nothing; faults the code objects
