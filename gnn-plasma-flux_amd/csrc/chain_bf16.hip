@@ -49,6 +49,19 @@ typedef unsigned u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f2{a, b}, b2));
 }
+// ReLU of two f32 values packed to bf16.  HF_EXP_IRELU (experiment): convert
+// first, then a signed 16-bit max with 0 on the bf16 bit patterns (one
+// v_pk_max_i16 for two values); equal to bf16(relu(z)) except that a
+// negative-signed NaN becomes +0.
+__device__ __forceinline__ unsigned pk_relu_bf16(float a, float b) {
+#ifdef HF_EXP_IRELU
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  const s2 v = __builtin_bit_cast(s2, pk_bf16(a, b));
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(v, s2{0, 0}));
+#else
+  return pk_bf16(relu(a), relu(b));
+#endif
+}
 __device__ __forceinline__ f4 mma(const u4 &a, const u4 &b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
 }
@@ -57,9 +70,14 @@ __device__ __forceinline__ f4 mma(const u4 &a, const u4 &b, f4 c) {
 // fragments, or the seam reads after a ring barrier), then one MFMA and up to
 // NV VALU (epilogue work of the previous pair) at a time.  The sched_barrier
 // keeps the next unit's reads from being picked for this unit's DS group.
+#ifndef HF_EXP_VFIRST
+#define HF_EXP_VFIRST 0
+#endif
 template <int NM, int NV, int ND = 4>
 __device__ __forceinline__ void interleave() {
   __builtin_amdgcn_sched_group_barrier(0x100, ND, 0);
+  // experiment: VALU issued between the fragment reads and the first MFMA
+  if constexpr (HF_EXP_VFIRST > 0 && NV > 0) __builtin_amdgcn_sched_group_barrier(0x002, HF_EXP_VFIRST, 0);
 #pragma unroll
   for (int i = 0; i < NM; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -273,7 +291,7 @@ struct CoreBF16 {
         for (int mt = 0; mt < MT; ++mt) z[rr][mt] = __fadd_rn(P.a[mt][t][r0 + rr], sm[mt]);
       }
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) nh[mt][K] = pk_bf16(relu(z[0][mt]), relu(z[1][mt]));
+      for (int mt = 0; mt < MT; ++mt) nh[mt][K] = pk_relu_bf16(z[0][mt], z[1][mt]);
     } else if constexpr (PART == 1) {
 #pragma unroll
       for (int mt = 1; mt < MT - 1; ++mt) {
@@ -283,7 +301,7 @@ struct CoreBF16 {
           const int r = r0 + rr;
           z[rr] = __fadd_rn(P.a[mt][t][r], __fadd_rn(P.g[mt - 1][t][r], P.g[mt + 1][t][r]));
         }
-        nh[mt][K] = pk_bf16(relu(z[0]), relu(z[1]));
+        nh[mt][K] = pk_relu_bf16(z[0], z[1]);
       }
     } else {
       float z0[2], z1[2];
@@ -310,8 +328,8 @@ struct CoreBF16 {
             : "v"(P.g[0][t][r]), "v"(P.g[MT - 2][t][r]));
         z1[rr] = __fadd_rn(P.a[MT - 1][t][r], sr);
       }
-      nh[0][K] = pk_bf16(relu(z0[0]), relu(z0[1]));
-      nh[MT - 1][K] = pk_bf16(relu(z1[0]), relu(z1[1]));
+      nh[0][K] = pk_relu_bf16(z0[0], z0[1]);
+      nh[MT - 1][K] = pk_relu_bf16(z1[0], z1[1]);
     }
   }
 
@@ -884,7 +902,7 @@ struct CellBF16T {
             const float gl = dpp_over<kRowShr1>(X.l[t][r], v), gr = dpp_over<kRowShl1>(X.r[t][r], v);
             z[rr] = __fadd_rn(acc[q].a[0][tt][r], __fadd_rn(gl, gr));
           }
-          A.h[0][q][K] = pk_bf16(relu(z[0]), relu(z[1]));
+          A.h[0][q][K] = pk_relu_bf16(z[0], z[1]);
         }
     }
     // edge readout, P/Q split (src/flux_gnn.py:62-66): all 8 tiles, then column
