@@ -565,7 +565,7 @@ int64_t graph_tape_bytes(const GraphW &w, int64_t N, int64_t E) {
   size_t b = align256(sizeof(int) * N) * 2 + align256(sizeof(int) * (N + 1)) + align256(sizeof(int) * E);
   b += (size_t)(2 * w.layers + 1) * align256(sizeof(float) * N * H);
   b += align256(sizeof(float) * E * H);
-  return (int64_t)b;
+  return std::max((int64_t)b, chain_tape_bytes(w, N));  // either path (tagged chains: train_chain.hip)
 }
 
 int64_t graph_backward_ws_bytes(const GraphW &w, int64_t N, int64_t E) {
@@ -575,14 +575,15 @@ int64_t graph_backward_ws_bytes(const GraphW &w, int64_t N, int64_t E) {
   b += align256(sizeof(float) * N * 2 * H);                      // dX
   b += align256(sizeof(float) * wgrad_part_floats(w, N, E));     // split-K partials
   b += align256(sizeof(int) * N) * 2 + align256(sizeof(int) * (N + 1)) + align256(sizeof(int) * E);  // CSR by col
-  return (int64_t)b;
+  return std::max((int64_t)b, chain_backward_ws_bytes(w, N));
 }
 
 hipError_t launch_graph_forward_train(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
                                       int chain_nx, float *flux, void *tape, hipStream_t s) {
+  if (E <= 0) return hipSuccess;  // no flux to compute; the backward returns zeros
+  if (chain_train_ok(w, chain_nx)) return launch_chain_forward_train(w, nf, N, chain_nx, flux, tape, s);
   Tape t = carve_tape(w, N, E, tape);
   hipError_t err;
-  if (E <= 0) return hipSuccess;  // no flux to compute; the backward returns zeros
   if ((err = build_csr(ei, E, N, t.deg, t.off, t.cur, t.perm, s, chain_nx, false))) return err;
   return forward_core(w, nf, N, ei, E, t.off, t.perm, t.h, t.agg, true, t.z, flux, s);
 }
@@ -606,6 +607,8 @@ hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, co
     if (grad_nf && (err = hipMemsetAsync(grad_nf, 0, sizeof(float) * N * w.in_dim, s))) return err;
     return hipSuccess;
   }
+  if (chain_train_ok(w, chain_nx))
+    return launch_chain_backward(w, nf, N, chain_nx, tape, grad_flux, grad_params, grad_nf, ws, s);
   Carve c{static_cast<char *>(ws)};
   float *dz = c.take<float>(E * H);
   float *buf[3] = {c.take<float>(N * H), c.take<float>(N * H), c.take<float>(N * H)};

@@ -198,6 +198,15 @@ hipError_t launch_graph_forward_train(const GraphW &w, const float *nf, int64_t 
 hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
                                  int chain_nx, const void *tape, const float *grad_flux, float *grad_params, float *grad_nf,
                                  void *ws, hipStream_t s);
+// Chain-specialised training path (train_chain.hip): tagged chain graphs
+// (chain_nx > 0) with hidden % 4 == 0, hidden <= 512, in_dim <= 8.
+bool chain_train_ok(const GraphW &w, int chain_nx);
+int64_t chain_tape_bytes(const GraphW &w, int64_t N);
+int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N);
+hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t N, int nx, float *flux, void *tape,
+                                      hipStream_t s);
+hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, int nx, const void *tape,
+                                 const float *grad_flux, float *grad_params, float *grad_nf, void *ws, hipStream_t s);
 hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei,
                              int64_t E, float *flux, void *ws, hipStream_t s);
 
