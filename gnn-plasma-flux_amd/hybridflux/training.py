@@ -101,19 +101,80 @@ class FluxDataset:
         return self.state_t[idx], self.flux_t[idx], self.state_next[idx]
 
 
-def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid):
+class GraphedStep:
+    """One optimizer step of the reference trainer's loop (ablation_loss ->
+    backward -> optimizer step, train_ablation.py:107-210) on a fixed batch
+    size, captured once as a HIP graph (torch.cuda.graph) and replayed per
+    batch: the step's ~100 small launches (loss terms, FV updates, Poisson,
+    FluxGNN forward/backward kernels, Adam) become one graph launch.  The
+    batch indices are a static device tensor gathered inside the graph.  The
+    optimizer must be capturable (torch.optim.Adam(..., capturable=True)).
+    The warmup steps that precede the capture are ordinary eager steps on the
+    first batches, so a pass makes exactly the eager loop's updates."""
+
+    def __init__(self, model, opt, data, batch_size, x, dt, dx, cfg, grid):
+        self.args = (model, opt, data, x, dt, dx, cfg, grid)
+        dev = data.state_t.device
+        self.idx = torch.zeros(batch_size, dtype=torch.long, device=dev)
+        self.graph = None
+        self.out = None
+
+    def _body(self):
+        model, opt, data, x, dt, dx, cfg, grid = self.args
+        st, ft, sn = data.batch(self.idx)
+        loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss.detach(), flux_loss.detach()
+
+    def capture(self):
+        self.args[1].zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = self._body()
+
+    def __call__(self, idx):
+        """Step on batch idx (a device index tensor of the captured size):
+        (loss, flux_loss) as fresh device scalars."""
+        self.idx.copy_(idx)
+        if self.graph is None:
+            return self._body()
+        self.graph.replay()
+        return self.out[0].clone(), self.out[1].clone()
+
+
+def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid, graphed=None, warmup=3):
     """One pass over `order` (sample indices) in batches; returns (sum of
-    losses, sum of flux losses) weighted by batch size, and the step count."""
+    losses, sum of flux losses) weighted by batch size, and the step count.
+    graphed: a GraphedStep of this batch size (created by the caller and kept
+    across passes); its first `warmup` steps run eagerly on a side stream, then
+    it is captured and every further full batch replays the graph."""
     tot, tot_flux, steps = 0.0, 0.0, 0
     losses = []
     for b0 in range(0, len(order), batch_size):
         idx = order[b0:b0 + batch_size]
-        st, ft, sn = data.batch(idx)
-        loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid)
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
-        losses.append((loss.detach(), flux_loss.detach(), len(idx)))
+        if graphed is not None and len(idx) == batch_size:
+            if graphed.graph is None and getattr(graphed, "_warm", 0) >= warmup:
+                torch.cuda.synchronize()
+                graphed.capture()
+            if graphed.graph is None:
+                graphed._warm = getattr(graphed, "_warm", 0) + 1
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    loss, flux_loss = graphed(idx)
+                torch.cuda.current_stream().wait_stream(side)
+            else:
+                loss, flux_loss = graphed(idx)
+        else:
+            st, ft, sn = data.batch(idx)
+            loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            loss, flux_loss = loss.detach(), flux_loss.detach()
+        losses.append((loss, flux_loss, len(idx)))
         steps += 1
     for l, f, n in losses:  # one host sync per pass, not per step
         tot += float(l) * n

@@ -100,21 +100,39 @@ def test_backward_deterministic_and_chain_batch_vs_oracle(hf):
         grads_close(runs[2][k], v.grad.numpy())
 
 
-@pytest.mark.parametrize("nx,B,layers,hidden", [(64, 5, 4, 128), (1, 3, 2, 128), (2, 4, 1, 64), (7, 6, 0, 32),
-                                                 (100, 3, 3, 128), (64, 300, 4, 128)])
-def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden):
+@pytest.mark.parametrize("nx,B,layers,hidden,kinkfree", [(64, 5, 4, 128, False), (1, 3, 2, 128, False),
+                                                          (2, 4, 1, 64, False), (7, 6, 0, 32, False),
+                                                          (100, 3, 3, 128, False), (64, 300, 4, 128, True)])
+def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden, kinkfree):
     """The chain training path (train_chain.hip: stencil-loader GEMMs, P/Q
     readout, split-K weight gradients) on tagged chains of any nx, layer count
     and width: flux, parameter and node-feature gradients vs torch-CPU autograd
-    of the oracle (src/flux_gnn.py:40-67).  B=300 x 64 cells spans several
-    GEMM row tiles and weight-gradient splits."""
+    of the oracle (src/flux_gnn.py:40-67).
+
+    A pre-activation within rounding of 0 (the P/Q split and the GEMM order
+    round differently from the reference) would flip one ReLU derivative and
+    move a gradient by O(g w) -- at 300 chains x 64 cells x 128 features per
+    layer a few such kinks are expected.  The large case (several GEMM row
+    tiles and weight-gradient splits) therefore uses weights whose every
+    pre-activation is bounded away from 0 (positive biases of 4 against
+    products below 3), so its ReLU derivatives are unambiguous and the gate
+    stays the gradient gate; the small cases exercise the masks."""
     rng = np.random.default_rng(nx * 100 + layers)
-    sd = {"input_mlp.0.weight": rng.normal(0, 0.5, (hidden, 4)), "input_mlp.0.bias": rng.normal(0, 0.1, hidden)}
-    for l in range(layers):
-        sd[f"update_mlps.{l}.0.weight"] = rng.normal(0, 1.5 / np.sqrt(2 * hidden), (hidden, 2 * hidden))
-        sd[f"update_mlps.{l}.0.bias"] = rng.normal(0, 0.1, hidden)
-    sd["edge_mlp.0.weight"] = rng.normal(0, 1.5 / np.sqrt(2 * hidden), (hidden, 2 * hidden))
-    sd["edge_mlp.0.bias"] = rng.normal(0, 0.1, hidden)
+    if kinkfree:
+        u = lambda a, shape: rng.uniform(-a, a, shape)  # noqa: E731
+        sd = {"input_mlp.0.weight": u(0.1, (hidden, 4)), "input_mlp.0.bias": np.full(hidden, 4.0)}
+        for l in range(layers):
+            sd[f"update_mlps.{l}.0.weight"] = u(0.002, (hidden, 2 * hidden))
+            sd[f"update_mlps.{l}.0.bias"] = np.full(hidden, 4.0)
+        sd["edge_mlp.0.weight"] = u(0.002, (hidden, 2 * hidden))
+        sd["edge_mlp.0.bias"] = np.full(hidden, 4.0)
+    else:
+        sd = {"input_mlp.0.weight": rng.normal(0, 0.5, (hidden, 4)), "input_mlp.0.bias": rng.normal(0, 0.1, hidden)}
+        for l in range(layers):
+            sd[f"update_mlps.{l}.0.weight"] = rng.normal(0, 1.5 / np.sqrt(2 * hidden), (hidden, 2 * hidden))
+            sd[f"update_mlps.{l}.0.bias"] = rng.normal(0, 0.1, hidden)
+        sd["edge_mlp.0.weight"] = rng.normal(0, 1.5 / np.sqrt(2 * hidden), (hidden, 2 * hidden))
+        sd["edge_mlp.0.bias"] = rng.normal(0, 0.1, hidden)
     sd["edge_mlp.2.weight"] = rng.normal(0, 1 / np.sqrt(hidden), (1, hidden))
     sd["edge_mlp.2.bias"] = rng.normal(0, 0.1, 1)
     sd = {k: np.asarray(v, np.float32) for k, v in sd.items()}
@@ -241,3 +259,31 @@ def test_train_model_smoke(hf, tmp_path):
     solver = hf.HybridSolver(str(tmp_path / "hybrid_physics_r2.pt"), radius=2, device=DEV)
     out = solver.run(st[0], 5)
     assert out.shape == (6, 3, 64) and np.isfinite(out).all()
+
+
+def test_graphed_steps_equal_eager(hf):
+    """train_steps with a captured step (GraphedStep: HIP-graph replay of the
+    loss + backward + Adam step) makes the eager loop's updates: same losses
+    and weights after 8 batches of 16 ('full' config: the rollout loss runs
+    the model on 4 states per sample), to float32 rounding of Adam's
+    capturable arithmetic."""
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import FluxDataset, GraphedStep, train_steps
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=4, steps_per_ic=32, out_path=None, device=DEV)
+    data = FluxDataset(st, ft, sn, DEV)
+    solver = hf.BaselineSolver(64, device=DEV)
+    xd = torch.as_tensor(x, device=DEV)
+    cfg = hf.ABLATION_CONFIGS["full"]
+    order = torch.randperm(len(data), generator=torch.Generator().manual_seed(5))[:128].to(DEV)
+    res = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        m = hf.FluxGNN(4, 128, 4).to(DEV)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=graphed)
+        gs = GraphedStep(m, opt, data, 16, xd, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
+        tot, _, steps = train_steps(m, opt, data, order, 16, xd, solver.dt, solver.dx, cfg, solver.grid, graphed=gs)
+        assert steps == 8 and (gs is None or gs.graph is not None)
+        res.append((tot, {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}))
+    assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[0][0])
+    for k in res[0][1]:
+        assert np.abs(res[0][1][k] - res[1][1][k]).max() <= 1e-5, k

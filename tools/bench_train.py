@@ -25,19 +25,39 @@ sys.path.insert(0, os.path.join(ROOT, "gnn-plasma-flux_amd"))
 sys.path.insert(0, ROOT)
 
 
-def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver):
-    from hybridflux.training import train_steps
+def flop_per_sample(cfg_name, nx=64, H=128, L=4, F=4):
+    """Algorithmic FLOPs of one sample's FluxGNN forward + backward in the
+    training step (P/Q-split readout, as the inference count of SURVEY.md 8d):
+    forward 329,216 per cell (input 2FH, layers L*2*2H*H, readout 2*H*2H +
+    2 edges * 2H), backward = data gradients (layers L*2*2H*H, readout 2*2H*H)
+    + weight gradients (the same GEMM sizes, plus the input layer's 2FH).  The
+    'full' and 'rollout_only' configs run the model on rollout_steps more
+    states per sample, each with its backward.  The loss terms' elementwise FV
+    updates and the detached Poisson solves are not counted."""
+    from hybridflux.config import ABLATION_CONFIGS
+    fwd = 2 * F * H + L * 2 * 2 * H * H + 2 * H * 2 * H + 2 * 2 * H
+    bwd = (L * 2 * 2 * H * H + 2 * 2 * H * H) * 2 + 2 * F * H
+    cfg = ABLATION_CONFIGS[cfg_name]
+    evals = 1 + (cfg["rollout_steps"] if cfg["lambda_energy_multi"] > 0 else 0)
+    return evals * (fwd + bwd) * nx
+
+
+def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False):
+    """samples/s of `steps` optimizer steps at `batch` samples each (eager, or
+    replaying the captured step: hybridflux.training.GraphedStep)."""
+    from hybridflux.training import GraphedStep, train_steps
     torch.manual_seed(0)
     m = hf.FluxGNN(4, 128, 4).to("cuda")
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=graphed)
     cfg = hf.ABLATION_CONFIGS[cfg_name]
     gen = torch.Generator().manual_seed(1)
+    gs = GraphedStep(m, opt, data, batch, x, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
 
     def run(n):
         order = torch.randint(0, len(data), (n * batch,), generator=gen).to("cuda")
-        return train_steps(m, opt, data, order, batch, x, solver.dt, solver.dx, cfg, solver.grid)
+        return train_steps(m, opt, data, order, batch, x, solver.dt, solver.dx, cfg, solver.grid, graphed=gs)
 
-    run(warmup)
+    run(warmup + (4 if graphed else 0))  # graphed: 3 eager warmup steps, the capture, then replays
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(steps)
@@ -85,18 +105,27 @@ def main():
     for b in [int(v) for v in args.batches.split(",") if v]:
         steps = max(2, args.steps if b > 1 else args.steps * 5)
         r, ms = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver)
-        rates[str(b)] = {"samples_per_s": round(r, 1), "ms_per_step": round(ms, 3), "steps": steps}
-        print(f"batch {b}: {r:.1f} samples/s, {ms:.3f} ms/step", file=sys.stderr, flush=True)
+        rg, msg = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, graphed=True)
+        rates[str(b)] = {"samples_per_s": round(rg, 1), "ms_per_step": round(msg, 3), "steps": steps,
+                         "eager_samples_per_s": round(r, 1), "eager_ms_per_step": round(ms, 3)}
+        print(f"batch {b}: {r:.1f} samples/s eager ({ms:.3f} ms/step), {rg:.1f} graphed ({msg:.3f} ms/step)",
+              file=sys.stderr, flush=True)
     cpu = None
     if args.cpu_samples > 0:
         cpu = {"value": round(cpu_rate(args.config, args.cpu_samples, st, ft, sn), 2), "unit": "samples/s",
                "cores": 16, "kind": "port",
                "sample": f"{args.cpu_samples} samples, batch size 1, oracle ablation_loss + torch-CPU autograd + Adam "
                          "(the reference trainer's loop)"}
+    fps = flop_per_sample(args.config)
+    top = max(rates, key=lambda k: int(k))
+    achieved = rates[top]["samples_per_s"] * fps / 1e12
+    roof = {"bound": "mfma", "batch": int(top), "flop_per_sample": fps, "achieved": round(achieved, 2),
+            "peak": 157.3, "unit": "TFLOP/s", "frac": round(achieved / 157.3, 4),
+            "note": "whole optimizer step (loss, FV terms, Adam included; HIP-graph replay) timed; FLOPs = FluxGNN forward+backward only"}
     print(json.dumps({"metric": f"FluxGNN training samples/s ('{args.config}' ablation loss, Adam)",
                       "unit": "samples/s", "config": {"dataset": "DATASET_CONFIG: 50 ICs x 40 steps, nx=64",
                                                        "model": "FluxGNN(4,128,4) f32"},
-                      "gpu": rates, "cpu_baseline": cpu}))
+                      "gpu": rates, "roofline": roof, "cpu_baseline": cpu}))
 
 
 if __name__ == "__main__":
