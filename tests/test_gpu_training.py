@@ -265,8 +265,10 @@ def test_graphed_steps_equal_eager(hf):
     """train_steps with a captured step (GraphedStep: HIP-graph replay of the
     loss + backward + Adam step) makes the eager loop's updates: same losses
     and weights after 8 batches of 16 ('full' config: the rollout loss runs
-    the model on 4 states per sample), to float32 rounding of Adam's
-    capturable arithmetic."""
+    the model on 4 states per sample).  Both arms use the capturable Adam (its
+    device-side bias corrections round differently from the host-side ones of
+    the default Adam, which after a few steps moves near-zero-gradient weights
+    by O(lr) differently, as test_adam_steps_vs_reference notes)."""
     from hybridflux.datagen import generate_dataset
     from hybridflux.training import FluxDataset, GraphedStep, train_steps
     st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=4, steps_per_ic=32, out_path=None, device=DEV)
@@ -279,11 +281,11 @@ def test_graphed_steps_equal_eager(hf):
     for graphed in (False, True):
         torch.manual_seed(0)
         m = hf.FluxGNN(4, 128, 4).to(DEV)
-        opt = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=graphed)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True)  # same Adam arithmetic in both arms
         gs = GraphedStep(m, opt, data, 16, xd, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
         tot, _, steps = train_steps(m, opt, data, order, 16, xd, solver.dt, solver.dx, cfg, solver.grid, graphed=gs)
         assert steps == 8 and (gs is None or gs.graph is not None)
         res.append((tot, {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}))
-    assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[0][0])
+    assert abs(res[0][0] - res[1][0]) <= 1e-6 * abs(res[0][0])
     for k in res[0][1]:
-        assert np.abs(res[0][1][k] - res[1][1][k]).max() <= 1e-5, k
+        assert np.abs(res[0][1][k] - res[1][1][k]).max() <= 1e-6, k
