@@ -41,28 +41,35 @@ constexpr int kStrRM = kBM + 8;   // [r][i] tile rows: 136 floats (the two lane 
 constexpr int kTileF = (kBM * kStrIM > kKC * kStrRM) ? kBM * kStrIM : kKC * kStrRM;
 
 __device__ __forceinline__ int64_t chain_prev(int64_t m, int nx) {
-  const int i = (int)(m % nx);
-  return m - i + (i == 0 ? nx - 1 : i - 1);
+  const int i = (int)((unsigned)m % (unsigned)nx);
+  return m + (i == 0 ? nx - 1 : -1);
 }
 __device__ __forceinline__ int64_t chain_next(int64_t m, int nx) {
-  const int i = (int)(m % nx);
-  return m - i + (i == nx - 1 ? 0 : i + 1);
+  const int i = (int)((unsigned)m % (unsigned)nx);
+  return m + (i == nx - 1 ? 1 - nx : 1);
 }
 
 // Row-major matrix views (element (row, col) of a logical [rows][cols] matrix).
-// Plain: rows in blocks of hrows; row r at p + (r % hrows) * ld + (r / hrows) * hoff
-// (a split weight like [W_a ; W_b] read out of nn.Linear's [H][2H]).
+// Plain: rows in blocks of 2^hshift; row r at p + (r & (2^hshift - 1)) * ld +
+// (r >> hshift) * hoff (a split weight like [W_a ; W_b] read out of
+// nn.Linear's [H][2H]; hshift = 62 for an ordinary matrix).  No 64-bit
+// division on the load path.
 struct VPlain {
   const float *p;
-  int64_t ld, rows, hrows, hoff;
+  int64_t ld, rows;
+  int hshift;
+  int64_t hoff;
   int cols;
   __device__ f4 load4(int64_t r, int c) const {
     if (r >= rows || c >= cols) return f4{0.f, 0.f, 0.f, 0.f};
-    return *reinterpret_cast<const f4 *>(p + (r % hrows) * ld + (r / hrows) * hoff + c);
+    const int64_t lo = r & ((int64_t(1) << hshift) - 1), hi = r >> hshift;
+    return *reinterpret_cast<const f4 *>(p + lo * ld + hi * hoff + c);
   }
 };
+constexpr int kNoSplit = 62;
 // [X ; agg X] of X [rows][C] on chains of nx rows: cols [0, C) are X, [C, 2C)
-// are (X[prev] + X[next]) * 0.5 (src/flux_gnn.py:53-59 on the chain).
+// are (X[prev] + X[next]) * 0.5 (src/flux_gnn.py:53-59 on the chain).  The
+// chain position is one 32-bit remainder (rows < 2^31).
 struct VStencil {
   const float *X;
   int64_t rows;
@@ -70,8 +77,10 @@ struct VStencil {
   __device__ f4 load4(int64_t r, int c) const {
     if (r >= rows || c >= 2 * C) return f4{0.f, 0.f, 0.f, 0.f};
     if (c < C) return *reinterpret_cast<const f4 *>(X + r * C + c);
-    const f4 a = *reinterpret_cast<const f4 *>(X + chain_next(r, nx) * C + (c - C));
-    const f4 b = *reinterpret_cast<const f4 *>(X + chain_prev(r, nx) * C + (c - C));
+    const int i = (int)((unsigned)r % (unsigned)nx);
+    const int64_t nr = r + (i == nx - 1 ? 1 - nx : 1), pr = r + (i == 0 ? nx - 1 : -1);
+    const f4 a = *reinterpret_cast<const f4 *>(X + nr * C + (c - C));
+    const f4 b = *reinterpret_cast<const f4 *>(X + pr * C + (c - C));
     return (a + b) * 0.5f;
   }
 };
@@ -255,36 +264,65 @@ inline int64_t tgemm_splits(int64_t R, int splits) {
   return R > 0 ? (R + rsplit - 1) / rsplit : 1;
 }
 
-// out[(i % ih) * ld + (i / ih) * hoff + j] = sum_s part[s][i][j] (s in order);
-// bias[i] = sum_s bias_part[s][i] for i < nbias.
-__global__ void part_reduce_kernel(const float *__restrict__ part, int S, int64_t I, int64_t J, float *out,
-                                   int64_t ih, int64_t ld, int64_t hoff, const float *__restrict__ bias_part,
-                                   int64_t nbias, float *bias) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < I * J) {
-    const int64_t i = t / J, j = t - i * J;
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v = __fadd_rn(v, part[(int64_t)s * I * J + t]);
-    out[(i % ih) * ld + (i / ih) * hoff + j] = v;
+// out[(i & (2^ish - 1)) * ld + (i >> ish) * hoff + j] = sum_s part[s][i][j] and
+// bias[i] = sum_s bias_part[s][i] (i < nbias).  Block of 256 threads = 64
+// outputs x 4 split quarters: quarter q sums splits [qS/4, (q+1)S/4) in order,
+// then the 4 quarter sums are added in order (deterministic).
+__global__ __launch_bounds__(256) void part_reduce_kernel(const float *__restrict__ part, int S, int64_t I, int64_t J,
+                                                          float *out, int ish, int64_t ld, int64_t hoff,
+                                                          const float *__restrict__ bias_part, int64_t nbias,
+                                                          float *bias) {
+  __shared__ float s_q[4][64];
+  const int o = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t n = I * J, t = (int64_t)blockIdx.x * 64 + o;
+  const bool is_w = t < n;
+  const int64_t tb = t - ((n + 63) / 64) * 64;  // bias outputs follow the weight outputs' blocks
+  const bool is_b = !is_w && bias && tb >= 0 && tb < nbias;
+  const int s0 = (int)((int64_t)S * q / 4), s1 = (int)((int64_t)S * (q + 1) / 4);
+  float v = 0.f;
+  if (is_w) {
+#pragma unroll 8
+    for (int s = s0; s < s1; ++s) v = __fadd_rn(v, part[(int64_t)s * n + t]);
+  } else if (is_b) {
+#pragma unroll 8
+    for (int s = s0; s < s1; ++s) v = __fadd_rn(v, bias_part[(int64_t)s * I + tb]);
   }
-  if (bias && t < nbias) {
-    float v = 0.f;
-    for (int s = 0; s < S; ++s) v = __fadd_rn(v, bias_part[(int64_t)s * I + t]);
-    bias[t] = v;
+  s_q[q][o] = v;
+  __syncthreads();
+  if (q == 0 && (is_w || is_b)) {
+    const float r = __fadd_rn(__fadd_rn(s_q[0][o], s_q[1][o]), __fadd_rn(s_q[2][o], s_q[3][o]));
+    if (is_w) {
+      const int64_t i = t / J, j = t - i * J;
+      out[(i & ((int64_t(1) << ish) - 1)) * ld + (i >> ish) * hoff + j] = r;
+    } else {
+      bias[tb] = r;
+    }
   }
+}
+inline unsigned part_reduce_blocks(int64_t I, int64_t J, int64_t nbias) {
+  return (unsigned)((I * J + 63) / 64 + (nbias + 63) / 64);
 }
 
 // h0[m][o] = ReLU(b_in[o] + sum_c W_in[o][c] nf[m][c])           (src/flux_gnn.py:49)
+// Thread = one row m and 4 consecutive o (H % 4 == 0, F <= 8).
 __global__ void input_forward_kernel(const float *__restrict__ nf, int F, const float *__restrict__ W,
                                      const float *__restrict__ b, int H, int64_t N, float *__restrict__ h0) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N * H) return;
-  const int64_t m = t / H;
-  const int o = (int)(t - m * H);
-  float v = 0.f;
-  for (int c = 0; c < F; ++c) v = fmaf(W[o * F + c], nf[m * F + c], v);
-  v = __fadd_rn(v, b[o]);
-  h0[t] = v > 0.f ? v : (v == v ? 0.f : v);
+  const int H4 = H / 4;
+  if (t >= N * H4) return;
+  const int64_t m = t / H4;
+  const int o0 = 4 * (int)(t - m * H4);
+  float x[8];
+  for (int c = 0; c < F; ++c) x[c] = nf[m * F + c];
+  f4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float v = 0.f;
+    for (int c = 0; c < F; ++c) v = fmaf(W[(o0 + e) * F + c], x[c], v);
+    v = __fadd_rn(v, b[o0 + e]);
+    r[e] = v > 0.f ? v : (v == v ? 0.f : v);
+  }
+  *reinterpret_cast<f4 *>(h0 + m * H + o0) = r;
 }
 
 // One wave per cell: flux of edge (i -> i+1) and (i+1 -> i) of its chain   (:62-66)
@@ -367,33 +405,59 @@ __global__ __launch_bounds__(256) void edge_backward_kernel(const float *__restr
     partial[(int64_t)blockIdx.x * (H + 1) + H] = __fadd_rn(__fadd_rn(s_b2[0], s_b2[1]), __fadd_rn(s_b2[2], s_b2[3]));
 }
 
-// gw2[c] = sum_b partial[b][c] (c < H), gb2 = sum_b partial[b][H], in block order
-__global__ void edge_partial_reduce_kernel(const float *__restrict__ partial, int nb, int H, float *gw2,
-                                           float *gb2) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c > H) return;
+// gw2[c] = sum_b partial[b][c] (c < H), gb2 = sum_b partial[b][H]: block c,
+// thread k sums blocks k, k + 256, ... in order, then a fixed-order LDS tree.
+__global__ __launch_bounds__(256) void edge_partial_reduce_kernel(const float *__restrict__ partial, int nb, int H,
+                                                                  float *gw2, float *gb2) {
+  __shared__ float s_v[256];
+  const int c = blockIdx.x, k = threadIdx.x;
   float v = 0.f;
-  for (int b = 0; b < nb; ++b) v = __fadd_rn(v, partial[(int64_t)b * (H + 1) + c]);
-  if (c < H) gw2[c] = v;
-  else *gb2 = v;
+  for (int b = k; b < nb; b += 256) v = __fadd_rn(v, partial[(int64_t)b * (H + 1) + c]);
+  s_v[k] = v;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (k < w) s_v[k] = __fadd_rn(s_v[k], s_v[k + w]);
+    __syncthreads();
+  }
+  if (k == 0) {
+    if (c < H) gw2[c] = s_v[0];
+    else *gb2 = s_v[0];
+  }
 }
 
 // Input-layer weight gradient partials: part[s][o][c] = sum_{m in split} d[m][o] nf[m][c],
-// bpart[s][o] = sum d[m][o].  Block s, thread o (+256k).
-__global__ void input_wgrad_kernel(const float *__restrict__ d, const float *__restrict__ nf, int F, int H,
-                                   int64_t N, int64_t rows, float *__restrict__ part, float *__restrict__ bpart) {
+// bpart[s][o] = sum d[m][o].  Block s: thread (lane k = t / H, o = t % H) sums
+// rows m0 + k, m0 + k + K, ... (K = 256 / H row lanes), then the K lanes are
+// added in order.
+__global__ __launch_bounds__(256) void input_wgrad_kernel(const float *__restrict__ d, const float *__restrict__ nf,
+                                                          int F, int H, int64_t N, int64_t rows,
+                                                          float *__restrict__ part, float *__restrict__ bpart) {
+  __shared__ float s_w[256][9];
+  const int K = 256 / H, k = threadIdx.x / H, o = threadIdx.x - k * H;
   const int64_t m0 = (int64_t)blockIdx.x * rows;
   const int64_t m1 = m0 + rows < N ? m0 + rows : N;
-  for (int o = threadIdx.x; o < H; o += blockDim.x) {
-    float w[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float bs = 0.f;
-    for (int64_t m = m0; m < m1; ++m) {
+  float w[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float bs = 0.f;
+  if (k < K) {
+#pragma unroll 4
+    for (int64_t m = m0 + k; m < m1; m += K) {
       const float dv = d[m * H + o];
       bs = __fadd_rn(bs, dv);
-      for (int c = 0; c < F && c < 8; ++c) w[c] = fmaf(dv, nf[m * F + c], w[c]);
+      for (int c = 0; c < F; ++c) w[c] = fmaf(dv, nf[m * F + c], w[c]);
     }
-    for (int c = 0; c < F && c < 8; ++c) part[((int64_t)blockIdx.x * H + o) * F + c] = w[c];
-    bpart[(int64_t)blockIdx.x * H + o] = bs;
+  }
+  for (int c = 0; c < F; ++c) s_w[threadIdx.x][c] = w[c];
+  s_w[threadIdx.x][8] = bs;
+  __syncthreads();
+  if (k == 0) {
+    for (int c = 0; c < F; ++c) {
+      float v = s_w[o][c];
+      for (int kk = 1; kk < K; ++kk) v = __fadd_rn(v, s_w[kk * H + o][c]);
+      part[((int64_t)blockIdx.x * H + o) * F + c] = v;
+    }
+    float v = s_w[o][8];
+    for (int kk = 1; kk < K; ++kk) v = __fadd_rn(v, s_w[kk * H + o][8]);
+    bpart[(int64_t)blockIdx.x * H + o] = v;
   }
 }
 
@@ -410,7 +474,7 @@ __global__ void input_dgrad_kernel(const float *__restrict__ d, const float *__r
 }
 
 constexpr int kWgradSplits = 256;
-constexpr int kInputSplits = 256;
+constexpr int kInputSplits = 1024;
 
 inline size_t al256(size_t v) { return (v + 255) & ~size_t(255); }
 
@@ -432,7 +496,8 @@ ChainTape carve_chain_tape(const GraphW &w, int64_t N, void *base) {
 }  // namespace
 
 bool chain_train_ok(const GraphW &w, int chain_nx) {
-  return chain_nx > 0 && w.hidden % 4 == 0 && w.hidden <= 512 && w.in_dim <= 8;
+  const int H = w.hidden;  // power of two in [4, 256] (split weight views, input-gradient lanes), in_dim <= 8
+  return chain_nx > 0 && H >= 4 && H <= 256 && (H & (H - 1)) == 0 && w.in_dim >= 1 && w.in_dim <= 8;
 }
 
 int64_t chain_tape_bytes(const GraphW &w, int64_t N) {
@@ -453,22 +518,22 @@ int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
 
 hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t N, int nx, float *flux, void *tape,
                                       hipStream_t s) {
-  const int H = w.hidden, L = w.layers;
+  const int H = w.hidden, L = w.layers, hsh = __builtin_ctz(H);
   const ChainTape t = carve_chain_tape(w, N, tape);
-  hipLaunchKernelGGL(input_forward_kernel, dim3((unsigned)((N * H + 255) / 256)), dim3(256), 0, s, nf, w.in_dim,
+  hipLaunchKernelGGL(input_forward_kernel, dim3((unsigned)((N * (H / 4) + 255) / 256)), dim3(256), 0, s, nf, w.in_dim,
                      w.w_in, w.b_in, H, N, t.h[0]);
   hipError_t e;
   for (int l = 0; l < L; ++l) {  // h[l+1] = ReLU(b_l + W_l [h[l] ; agg h[l]])               (:53-60)
     const VStencil A{t.h[l], N, H, nx};
-    const VPlain B{w.w_l + l * w.lsw, 2LL * H, H, INT64_MAX, 0, 2 * H};
+    const VPlain B{w.w_l + l * w.lsw, 2LL * H, H, kNoSplit, 0, 2 * H};
     if ((e = tgemm<VStencil, false, VPlain, false>(A, B, EpiAct{t.h[l + 1], H, w.b_l + l * w.lsb, H, true}, N, H,
                                                    2 * H, 1, s)))
       return e;
   }
   // PQ[m][c] = sum_k [W_a ; W_b][c][k] h[L][m][k] (+ b_e, c < H): row c of [W_a ; W_b] is
   // edge_mlp.0.weight[c % H][(c / H) * H ...]
-  const VPlain A{t.h[L], H, N, INT64_MAX, 0, H};
-  const VPlain B{w.w_e, 2LL * H, 2LL * H, H, H, H};
+  const VPlain A{t.h[L], H, N, kNoSplit, 0, H};
+  const VPlain B{w.w_e, 2LL * H, 2LL * H, hsh, H, H};
   if ((e = tgemm<VPlain, false, VPlain, false>(A, B, EpiAct{t.pq, 2LL * H, w.b_e, H, false}, N, 2 * H, H, 1, s)))
     return e;
   hipLaunchKernelGGL(edge_forward_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, t.pq, H, N, nx, w.w_2,
@@ -478,7 +543,7 @@ hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t 
 
 hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, int nx, const void *tape,
                                  const float *grad_flux, float *grad_params, float *grad_nf, void *ws, hipStream_t s) {
-  const int H = w.hidden, L = w.layers, F = w.in_dim;
+  const int H = w.hidden, L = w.layers, F = w.in_dim, hsh = __builtin_ctz(H);
   const ChainTape t = carve_chain_tape(w, N, const_cast<void *>(tape));
   const GraphW g = graph_view_state_dict(grad_params, F, H, L);
   char *p = static_cast<char *>(ws);
@@ -495,43 +560,42 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   float *epart = take(sizeof(float) * kEdgeBlocks * (H + 1));
   float *ipart = take(sizeof(float) * kInputSplits * H * (F + 1));
   hipError_t e;
-  auto reduce = [&](int64_t I, int64_t J, float *out, int64_t ih, int64_t ld, int64_t hoff, int64_t nbias,
+  auto reduce = [&](int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff, int64_t nbias,
                     float *bias) {
-    const int64_t n = std::max(I * J, nbias);
-    hipLaunchKernelGGL(part_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, (int)S, I, J,
-                       out, ih, ld, hoff, bpart, nbias, bias);
+    hipLaunchKernelGGL(part_reduce_kernel, dim3(part_reduce_blocks(I, J, nbias)), dim3(256), 0, s, part, (int)S, I, J,
+                       out, ish, ld, hoff, bpart, nbias, bias);
     return hipGetLastError();
   };
   // readout: dPQ, dw2, db2                                                          (:62-66)
   hipLaunchKernelGGL(edge_backward_kernel, dim3(kEdgeBlocks), dim3(256), 0, s, t.pq, H, N, nx, w.w_2, grad_flux, dPQ,
                      epart);
-  hipLaunchKernelGGL(edge_partial_reduce_kernel, dim3((unsigned)((H + 1 + 255) / 256)), dim3(256), 0, s, epart,
+  hipLaunchKernelGGL(edge_partial_reduce_kernel, dim3((unsigned)(H + 1)), dim3(256), 0, s, epart,
                      kEdgeBlocks, H, const_cast<float *>(g.w_2), const_cast<float *>(g.b_2));
   // dW_e[c % H][(c / H) H + k] = sum_m dPQ[m][c] h[L][m][k]; db_e = column sums of dP
   {
-    const VPlain A{dPQ, 2LL * H, N, INT64_MAX, 0, 2 * H};
-    const VPlain B{t.h[L], H, N, INT64_MAX, 0, H};
+    const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
+    const VPlain B{t.h[L], H, N, kNoSplit, 0, H};
     if ((e = tgemm<VPlain, true, VPlain, true, EpiPart, true>(A, B, EpiPart{part, 2LL * H, H}, 2 * H, H, N,
                                                                kWgradSplits, s, bpart)))
       return e;
-    if ((e = reduce(2 * H, H, const_cast<float *>(g.w_e), H, 2LL * H, H, H, const_cast<float *>(g.b_e)))) return e;
+    if ((e = reduce(2 * H, H, const_cast<float *>(g.w_e), hsh, 2LL * H, H, H, const_cast<float *>(g.b_e)))) return e;
   }
   // dh[L] = [W_a ; W_b]^T dPQ, masked by ReLU'(h[L])
   int cur = 0;
   {
-    const VPlain A{dPQ, 2LL * H, N, INT64_MAX, 0, 2 * H};
-    const VPlain B{w.w_e, 2LL * H, 2LL * H, H, H, H};  // B(r = c, j = k) = [W_a ; W_b][c][k]
+    const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
+    const VPlain B{w.w_e, 2LL * H, 2LL * H, hsh, H, H};  // B(r = c, j = k) = [W_a ; W_b][c][k]
     if ((e = tgemm<VPlain, false, VPlain, true>(A, B, EpiMask{dl[cur], H, t.h[L], H}, N, H, 2 * H, 1, s))) return e;
   }
   for (int l = L - 1; l >= 0; --l) {  // update layers, last to first                      (:53-60)
     // dW_l[o][k] = sum_m delta[m][o] [h[l] ; agg h[l]][m][k], db_l = column sums of delta
     {
-      const VPlain A{dl[cur], H, N, INT64_MAX, 0, H};
+      const VPlain A{dl[cur], H, N, kNoSplit, 0, H};
       const VStencil B{t.h[l], N, H, nx};
       if ((e = tgemm<VPlain, true, VStencil, true, EpiPart, true>(A, B, EpiPart{part, H, 2LL * H}, H, 2 * H, N,
                                                                   kWgradSplits, s, bpart)))
         return e;
-      if ((e = reduce(H, 2 * H, const_cast<float *>(g.w_l + l * g.lsw), INT64_MAX, 2LL * H, 0, H,
+      if ((e = reduce(H, 2 * H, const_cast<float *>(g.w_l + l * g.lsw), kNoSplit, 2LL * H, 0, H,
                       const_cast<float *>(g.b_l + l * g.lsb))))
         return e;
     }
@@ -539,7 +603,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
     // chain), masked by ReLU'(h[l]): B(r, j) = W_l[r % H][(r / H) H + j]
     {
       const VStencil A{dl[cur], N, H, nx};
-      const VPlain B{w.w_l + l * w.lsw, 2LL * H, 2LL * H, H, H, H};
+      const VPlain B{w.w_l + l * w.lsw, 2LL * H, 2LL * H, hsh, H, H};
       if ((e = tgemm<VStencil, false, VPlain, true>(A, B, EpiMask{dl[cur ^ 1], H, t.h[l], H}, N, H, 2 * H, 1, s)))
         return e;
       cur ^= 1;
@@ -551,12 +615,9 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   const int nsp = (int)((N + rows - 1) / rows);
   float *ipb = ipart + (int64_t)kInputSplits * H * F;
   hipLaunchKernelGGL(input_wgrad_kernel, dim3((unsigned)nsp), dim3(256), 0, s, d0, nf, F, H, N, rows, ipart, ipb);
-  {
-    const int64_t n = std::max((int64_t)H * F, (int64_t)H);
-    hipLaunchKernelGGL(part_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ipart, nsp, (int64_t)H,
-                       (int64_t)F, const_cast<float *>(g.w_in), INT64_MAX, (int64_t)F, 0, ipb, (int64_t)H,
-                       const_cast<float *>(g.b_in));
-  }
+  hipLaunchKernelGGL(part_reduce_kernel, dim3(part_reduce_blocks(H, F, H)), dim3(256), 0, s, ipart, nsp, (int64_t)H,
+                     (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F, (int64_t)0, ipb, (int64_t)H,
+                     const_cast<float *>(g.b_in));
   if (grad_nf)
     hipLaunchKernelGGL(input_dgrad_kernel, dim3((unsigned)((N * F + 255) / 256)), dim3(256), 0, s, d0, w.w_in, F, H, N,
                        grad_nf);

@@ -106,8 +106,9 @@ def main():
         steps = max(2, args.steps if b > 1 else args.steps * 5)
         r, ms = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver)
         rg, msg = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, graphed=True)
-        rates[str(b)] = {"samples_per_s": round(rg, 1), "ms_per_step": round(msg, 3), "steps": steps,
-                         "eager_samples_per_s": round(r, 1), "eager_ms_per_step": round(ms, 3)}
+        best = max(r, rg)
+        rates[str(b)] = {"samples_per_s": round(best, 1), "ms_per_step": round(b / best * 1e3, 3), "steps": steps,
+                         "eager_samples_per_s": round(r, 1), "graphed_samples_per_s": round(rg, 1)}
         print(f"batch {b}: {r:.1f} samples/s eager ({ms:.3f} ms/step), {rg:.1f} graphed ({msg:.3f} ms/step)",
               file=sys.stderr, flush=True)
     cpu = None
@@ -121,7 +122,7 @@ def main():
     achieved = rates[top]["samples_per_s"] * fps / 1e12
     roof = {"bound": "mfma", "batch": int(top), "flop_per_sample": fps, "achieved": round(achieved, 2),
             "peak": 157.3, "unit": "TFLOP/s", "frac": round(achieved / 157.3, 4),
-            "note": "whole optimizer step (loss, FV terms, Adam included; HIP-graph replay) timed; FLOPs = FluxGNN forward+backward only"}
+            "note": "whole optimizer step (loss, FV terms, Adam included; the faster of eager and HIP-graph replay) timed; FLOPs = FluxGNN forward+backward only"}
     print(json.dumps({"metric": f"FluxGNN training samples/s ('{args.config}' ablation loss, Adam)",
                       "unit": "samples/s", "config": {"dataset": "DATASET_CONFIG: 50 ICs x 40 steps, nx=64",
                                                        "model": "FluxGNN(4,128,4) f32"},
