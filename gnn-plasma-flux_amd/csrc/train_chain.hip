@@ -60,27 +60,42 @@ struct VPlain {
   int hshift;
   int64_t hoff;
   int cols;
-  __device__ f4 load4(int64_t r, int c) const {
-    if (r >= rows || c >= cols) return f4{0.f, 0.f, 0.f, 0.f};
+  struct Row {
+    const float *ptr;  // nullptr: outside the matrix
+  };
+  __device__ Row row(int64_t r) const {
+    if (r >= rows) return Row{nullptr};
     const int64_t lo = r & ((int64_t(1) << hshift) - 1), hi = r >> hshift;
-    return *reinterpret_cast<const f4 *>(p + lo * ld + hi * hoff + c);
+    return Row{p + lo * ld + hi * hoff};
+  }
+  __device__ f4 load4(const Row &w, int c) const {
+    if (!w.ptr || c >= cols) return f4{0.f, 0.f, 0.f, 0.f};
+    return *reinterpret_cast<const f4 *>(w.ptr + c);
   }
 };
 constexpr int kNoSplit = 62;
 // [X ; agg X] of X [rows][C] on chains of nx rows: cols [0, C) are X, [C, 2C)
 // are (X[prev] + X[next]) * 0.5 (src/flux_gnn.py:53-59 on the chain).  The
-// chain position is one 32-bit remainder (rows < 2^31).
+// row handle holds the three row pointers (one 32-bit remainder per row, rows
+// < 2^31), computed once per row rather than per load.
 struct VStencil {
   const float *X;
   int64_t rows;
   int C, nx;
-  __device__ f4 load4(int64_t r, int c) const {
-    if (r >= rows || c >= 2 * C) return f4{0.f, 0.f, 0.f, 0.f};
-    if (c < C) return *reinterpret_cast<const f4 *>(X + r * C + c);
+  struct Row {
+    const float *self, *nxt, *prv;  // self == nullptr: outside the matrix
+  };
+  __device__ Row row(int64_t r) const {
+    if (r >= rows) return Row{nullptr, nullptr, nullptr};
     const int i = (int)((unsigned)r % (unsigned)nx);
     const int64_t nr = r + (i == nx - 1 ? 1 - nx : 1), pr = r + (i == 0 ? nx - 1 : -1);
-    const f4 a = *reinterpret_cast<const f4 *>(X + nr * C + (c - C));
-    const f4 b = *reinterpret_cast<const f4 *>(X + pr * C + (c - C));
+    return Row{X + r * C, X + nr * C - C, X + pr * C - C};
+  }
+  __device__ f4 load4(const Row &w, int c) const {
+    if (!w.self || c >= 2 * C) return f4{0.f, 0.f, 0.f, 0.f};
+    if (c < C) return *reinterpret_cast<const f4 *>(w.self + c);
+    const f4 a = *reinterpret_cast<const f4 *>(w.nxt + c);
+    const f4 b = *reinterpret_cast<const f4 *>(w.prv + c);
     return (a + b) * 0.5f;
   }
 };
@@ -137,15 +152,26 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
   f4 ra[4], rbv[4], csum = f4{0.f, 0.f, 0.f, 0.f};
-  // thread -> (global row, col) of its 4 float4 per operand per stage
+  // thread -> (global row, col) of its 4 float4 per operand per stage.  The
+  // rows of an [i][r] operand are the same every stage: their handles are made once.
+  typename LA::Row rowa[4];
+  typename LB::Row rowb[4];
+  if (!ARM) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rowa[q] = ga.row(i0 + ((t + 256 * q) >> 3));
+  }
+  if (!BRM) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rowb[q] = gb.row(j0 + ((t + 256 * q) >> 3));
+  }
   auto gload = [&](int64_t r0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int idx = t + 256 * q;
-      if (ARM) ra[q] = ga.load4(r0 + (idx >> 5), (int)(i0 + 4 * (idx & 31)));
-      else ra[q] = (r0 + 4 * (idx & 7) < re) ? ga.load4(i0 + (idx >> 3), (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
-      if (BRM) rbv[q] = gb.load4(r0 + (idx >> 5), (int)(j0 + 4 * (idx & 31)));
-      else rbv[q] = (r0 + 4 * (idx & 7) < re) ? gb.load4(j0 + (idx >> 3), (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
+      if (ARM) ra[q] = ga.load4(ga.row(r0 + (idx >> 5)), (int)(i0 + 4 * (idx & 31)));
+      else ra[q] = (r0 + 4 * (idx & 7) < re) ? ga.load4(rowa[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
+      if (BRM) rbv[q] = gb.load4(gb.row(r0 + (idx >> 5)), (int)(j0 + 4 * (idx & 31)));
+      else rbv[q] = (r0 + 4 * (idx & 7) < re) ? gb.load4(rowb[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
     }
     if (ARM) {  // rows past this split's end belong to the next split
 #pragma unroll
@@ -304,20 +330,24 @@ inline unsigned part_reduce_blocks(int64_t I, int64_t J, int64_t nbias) {
 }
 
 // h0[m][o] = ReLU(b_in[o] + sum_c W_in[o][c] nf[m][c])           (src/flux_gnn.py:49)
-// Thread = one row m and 4 consecutive o (H % 4 == 0, F <= 8).
-__global__ void input_forward_kernel(const float *__restrict__ nf, int F, const float *__restrict__ W,
+// Thread = one row m and 4 consecutive o (H % 4 == 0); F is a template
+// argument so the row and the weights stay in registers.
+template <int F>
+__global__ void input_forward_kernel(const float *__restrict__ nf, const float *__restrict__ W,
                                      const float *__restrict__ b, int H, int64_t N, float *__restrict__ h0) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int H4 = H / 4;
   if (t >= N * H4) return;
   const int64_t m = t / H4;
   const int o0 = 4 * (int)(t - m * H4);
-  float x[8];
+  float x[F];
+#pragma unroll
   for (int c = 0; c < F; ++c) x[c] = nf[m * F + c];
   f4 r;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float v = 0.f;
+#pragma unroll
     for (int c = 0; c < F; ++c) v = fmaf(W[(o0 + e) * F + c], x[c], v);
     v = __fadd_rn(v, b[o0 + e]);
     r[e] = v > 0.f ? v : (v == v ? 0.f : v);
@@ -429,37 +459,54 @@ __global__ __launch_bounds__(256) void edge_partial_reduce_kernel(const float *_
 // bpart[s][o] = sum d[m][o].  Block s: thread (lane k = t / H, o = t % H) sums
 // rows m0 + k, m0 + k + K, ... (K = 256 / H row lanes), then the K lanes are
 // added in order.
+template <int F>
 __global__ __launch_bounds__(256) void input_wgrad_kernel(const float *__restrict__ d, const float *__restrict__ nf,
-                                                          int F, int H, int64_t N, int64_t rows,
-                                                          float *__restrict__ part, float *__restrict__ bpart) {
-  __shared__ float s_w[256][9];
+                                                          int H, int64_t N, int64_t rows, float *__restrict__ part,
+                                                          float *__restrict__ bpart) {
+  __shared__ float s_w[256][F + 1];
   const int K = 256 / H, k = threadIdx.x / H, o = threadIdx.x - k * H;
   const int64_t m0 = (int64_t)blockIdx.x * rows;
   const int64_t m1 = m0 + rows < N ? m0 + rows : N;
-  float w[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float w[F];
+#pragma unroll
+  for (int c = 0; c < F; ++c) w[c] = 0.f;
   float bs = 0.f;
   if (k < K) {
 #pragma unroll 4
     for (int64_t m = m0 + k; m < m1; m += K) {
       const float dv = d[m * H + o];
       bs = __fadd_rn(bs, dv);
+#pragma unroll
       for (int c = 0; c < F; ++c) w[c] = fmaf(dv, nf[m * F + c], w[c]);
     }
   }
+#pragma unroll
   for (int c = 0; c < F; ++c) s_w[threadIdx.x][c] = w[c];
-  s_w[threadIdx.x][8] = bs;
+  s_w[threadIdx.x][F] = bs;
   __syncthreads();
   if (k == 0) {
-    for (int c = 0; c < F; ++c) {
+#pragma unroll
+    for (int c = 0; c <= F; ++c) {
       float v = s_w[o][c];
       for (int kk = 1; kk < K; ++kk) v = __fadd_rn(v, s_w[kk * H + o][c]);
-      part[((int64_t)blockIdx.x * H + o) * F + c] = v;
+      if (c < F) part[((int64_t)blockIdx.x * H + o) * F + c] = v;
+      else bpart[(int64_t)blockIdx.x * H + o] = v;
     }
-    float v = s_w[o][8];
-    for (int kk = 1; kk < K; ++kk) v = __fadd_rn(v, s_w[kk * H + o][8]);
-    bpart[(int64_t)blockIdx.x * H + o] = v;
   }
 }
+
+// the kernels above for in_dim F = 1..8
+#define HF_INPUT_DISPATCH(F, CALL) \
+  switch (F) {                     \
+    case 1: CALL(1); break;        \
+    case 2: CALL(2); break;        \
+    case 3: CALL(3); break;        \
+    case 4: CALL(4); break;        \
+    case 5: CALL(5); break;        \
+    case 6: CALL(6); break;        \
+    case 7: CALL(7); break;        \
+    default: CALL(8); break;       \
+  }
 
 // grad_nf[m][c] = sum_o d[m][o] W_in[o][c]
 __global__ void input_dgrad_kernel(const float *__restrict__ d, const float *__restrict__ W, int F, int H, int64_t N,
@@ -520,8 +567,11 @@ hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t 
                                       hipStream_t s) {
   const int H = w.hidden, L = w.layers, hsh = __builtin_ctz(H);
   const ChainTape t = carve_chain_tape(w, N, tape);
-  hipLaunchKernelGGL(input_forward_kernel, dim3((unsigned)((N * (H / 4) + 255) / 256)), dim3(256), 0, s, nf, w.in_dim,
-                     w.w_in, w.b_in, H, N, t.h[0]);
+#define HF_IN_FWD(FF)                                                                                      \
+  hipLaunchKernelGGL(input_forward_kernel<FF>, dim3((unsigned)((N * (H / 4) + 255) / 256)), dim3(256), 0, s, nf, \
+                     w.w_in, w.b_in, H, N, t.h[0])
+  HF_INPUT_DISPATCH(w.in_dim, HF_IN_FWD)
+#undef HF_IN_FWD
   hipError_t e;
   for (int l = 0; l < L; ++l) {  // h[l+1] = ReLU(b_l + W_l [h[l] ; agg h[l]])               (:53-60)
     const VStencil A{t.h[l], N, H, nx};
@@ -614,7 +664,10 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   const int64_t rows = (N + kInputSplits - 1) / kInputSplits;
   const int nsp = (int)((N + rows - 1) / rows);
   float *ipb = ipart + (int64_t)kInputSplits * H * F;
-  hipLaunchKernelGGL(input_wgrad_kernel, dim3((unsigned)nsp), dim3(256), 0, s, d0, nf, F, H, N, rows, ipart, ipb);
+#define HF_IN_WG(FF) \
+  hipLaunchKernelGGL(input_wgrad_kernel<FF>, dim3((unsigned)nsp), dim3(256), 0, s, d0, nf, H, N, rows, ipart, ipb)
+  HF_INPUT_DISPATCH(F, HF_IN_WG)
+#undef HF_IN_WG
   hipLaunchKernelGGL(part_reduce_kernel, dim3(part_reduce_blocks(H, F, H)), dim3(256), 0, s, ipart, nsp, (int64_t)H,
                      (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F, (int64_t)0, ipb, (int64_t)H,
                      const_cast<float *>(g.b_in));
