@@ -441,6 +441,25 @@ int hf_graph_backward(const float *params, int in_dim, int hidden, int layers, c
   return HF_OK;
 }
 
+int64_t hf_ablation_loss_workspace_bytes(int B, int nx) {
+  if (B < 0 || nx < 1) return -1;
+  return hf::ablation_loss_ws_bytes(B, nx);
+}
+
+int hf_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx, float c,
+                     float dx, const float *lam, const double *pc, float *loss, float *flux_loss, float *dfe, void *ws,
+                     int64_t ws_bytes, void *stream) {
+  if (B < 1 || nx < 1) return fail(HF_EINVAL, "hf_ablation_loss: need B >= 1, nx >= 1");
+  if (!fe || !st || !ft || !sn || !lam || !pc || !loss || !flux_loss || !dfe || !ws)
+    return fail(HF_EINVAL, "hf_ablation_loss: NULL pointer");
+  if (ws_bytes < hf::ablation_loss_ws_bytes(B, nx))
+    return fail(HF_EINVAL, "hf_ablation_loss: workspace smaller than hf_ablation_loss_workspace_bytes");
+  HF_CHECK_HIP(hf::launch_ablation_loss(fe, st, ft, sn, B, nx, c, dx, lam, pc, loss, flux_loss, dfe, ws,
+                                        as_stream(stream)),
+               "hf_ablation_loss");
+  return HF_OK;
+}
+
 // ------------------------------------------------------- PureGNN / PINN
 int64_t hf_pure_gnn_param_count(int in_dim, int hidden, int layers) {
   if (in_dim < 1 || hidden < 1 || layers < 0) return -1;

@@ -207,6 +207,11 @@ hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t 
                                       hipStream_t s);
 hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, int nx, const void *tape,
                                  const float *grad_flux, float *grad_params, float *grad_nf, void *ws, hipStream_t s);
+// The ablation loss's single-step terms and d loss / d flux_edge (train_chain.hip).
+int64_t ablation_loss_ws_bytes(int B, int nx);
+hipError_t launch_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx,
+                                float c, float dx, const float *lam, const double *pc, float *loss, float *flux_loss,
+                                float *dfe, void *ws, hipStream_t s);
 hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei,
                              int64_t E, float *flux, void *ws, hipStream_t s);
 

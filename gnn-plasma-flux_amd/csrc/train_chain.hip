@@ -520,6 +520,113 @@ __global__ void input_dgrad_kernel(const float *__restrict__ d, const float *__r
   gnf[t] = v;
 }
 
+
+// ------------------------------------------------------------------ loss
+// The single-step terms of the reference trainer's ablation loss
+// (scripts/training/train_ablation.py:120-170), batched: one block per sample.
+// F = 0.5 (f_fwd + f_bwd) (:124-126), n' = n - c (F - roll(F, 1)) (:134-135),
+// in the reference's float32 operation order.
+__device__ __forceinline__ float face_of(const float *fe, int nx, int i) {
+  return __fmul_rn(0.5f, __fadd_rn(fe[i], fe[nx + i]));
+}
+__global__ __launch_bounds__(256) void loss_update_kernel(const float *__restrict__ fe, const float *__restrict__ st,
+                                                          int nx, float c, float *__restrict__ nn) {
+  const int b = blockIdx.x;
+  const float *f = fe + (int64_t)b * 2 * nx, *n = st + (int64_t)b * 3 * nx;
+  for (int i = threadIdx.x; i < nx; i += blockDim.x) {
+    const float Fi = face_of(f, nx, i), Fl = face_of(f, nx, i == 0 ? nx - 1 : i - 1);
+    nn[(int64_t)b * nx + i] = __fsub_rn(n[i], __fmul_rn(c, __fsub_rn(Fi, Fl)));
+  }
+}
+
+// fixed-order block sum of 256 per-thread values (thread 0 returns it)
+__device__ __forceinline__ float block_sum256(float v, float *sh) {
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int w = 128; w >= 1; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] = __fadd_rn(sh[threadIdx.x], sh[threadIdx.x + w]);
+    __syncthreads();
+  }
+  const float r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// Per-sample sums part[b][0..6] = sum (F - F_t)^2, sum (n' - n'_t)^2,
+// sum (E' - E'_t)^2, sum (n - 1), sum (n' - 1), sum (u'_t^2 + E'^2),
+// sum (u'_t^2 + E'_t^2); and d loss / d flux_edge: with r = n' - n'_t and
+// N = B nx, dL/dF_i = 2 (F_i - F_t,i) / N + lam_s 2 c (r_{i+1} - r_i) / N
+// (the continuity update's adjoint), half of it to each edge of face i.
+__global__ __launch_bounds__(256) void loss_terms_kernel(const float *__restrict__ fe, const float *__restrict__ st,
+                                                         const float *__restrict__ ft, const float *__restrict__ sn,
+                                                         const float *__restrict__ nn, const float *__restrict__ En,
+                                                         int B, int nx, float c, float lam_s, float *__restrict__ part,
+                                                         float *__restrict__ dfe) {
+  __shared__ float sh[256];
+  const int b = blockIdx.x;
+  const float *f = fe + (int64_t)b * 2 * nx, *n = st + (int64_t)b * 3 * nx, *F_t = ft + (int64_t)b * nx;
+  const float *nt = sn + (int64_t)b * 3 * nx, *ut = nt + nx, *Et = nt + 2 * nx;
+  const float *np = nn + (int64_t)b * nx, *Ep = En + (int64_t)b * nx;
+  const float inv = 2.0f / ((float)B * (float)nx);
+  float s[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = threadIdx.x; i < nx; i += blockDim.x) {
+    const float Fi = face_of(f, nx, i), dF = __fsub_rn(Fi, F_t[i]);
+    const float r = __fsub_rn(np[i], nt[i]);
+    const int ip = i == nx - 1 ? 0 : i + 1;
+    const float rn = __fsub_rn(np[ip], nt[ip]);
+    const float dE = __fsub_rn(Ep[i], Et[i]);
+    s[0] = fmaf(dF, dF, s[0]);
+    s[1] = fmaf(r, r, s[1]);
+    s[2] = fmaf(dE, dE, s[2]);
+    s[3] = __fadd_rn(s[3], __fsub_rn(n[i], 1.0f));
+    s[4] = __fadd_rn(s[4], __fsub_rn(np[i], 1.0f));
+    s[5] = __fadd_rn(s[5], __fadd_rn(__fmul_rn(ut[i], ut[i]), __fmul_rn(Ep[i], Ep[i])));
+    s[6] = __fadd_rn(s[6], __fadd_rn(__fmul_rn(ut[i], ut[i]), __fmul_rn(Et[i], Et[i])));
+    const float g = __fadd_rn(__fmul_rn(inv, dF), __fmul_rn(lam_s, __fmul_rn(__fmul_rn(inv, c), __fsub_rn(rn, r))));
+    const float h = __fmul_rn(0.5f, g);
+    dfe[(int64_t)b * 2 * nx + i] = h;
+    dfe[(int64_t)b * 2 * nx + nx + i] = h;
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const float v = block_sum256(s[k], sh);
+    if (threadIdx.x == 0) part[(int64_t)b * 7 + k] = v;
+  }
+}
+
+// loss = flux MSE + lam_s state MSE + lam_p Poisson MSE + lam_c charge + lam_e energy
+// (terms with lambda 0 are left out, as the reference does), one block, fixed order.
+__global__ __launch_bounds__(256) void loss_final_kernel(const float *__restrict__ part, int B, int nx, float dx,
+                                                         float lam_s, float lam_p, float lam_c, float lam_e,
+                                                         float *loss, float *flux_loss) {
+  __shared__ float sh[256];
+  float a[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float *p = part + (int64_t)b * 7;
+    a[0] = __fadd_rn(a[0], p[0]);
+    a[1] = __fadd_rn(a[1], p[1]);
+    a[2] = __fadd_rn(a[2], p[2]);
+    const float dq = __fsub_rn(__fmul_rn(p[4], dx), __fmul_rn(p[3], dx));          // charge_next - charge_t
+    a[3] = fmaf(dq, dq, a[3]);
+    const float de = __fsub_rn(__fmul_rn(0.5f, __fdiv_rn(p[5], (float)nx)), __fmul_rn(0.5f, __fdiv_rn(p[6], (float)nx)));
+    a[4] = fmaf(de, de, a[4]);
+  }
+  float t[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) t[k] = block_sum256(a[k], sh);
+  if (threadIdx.x == 0) {
+    const float N = (float)B * (float)nx;
+    const float fl = __fdiv_rn(t[0], N);
+    float L = fl;
+    if (lam_s > 0.f) L = __fadd_rn(L, __fmul_rn(lam_s, __fdiv_rn(t[1], N)));
+    if (lam_p > 0.f) L = __fadd_rn(L, __fmul_rn(lam_p, __fdiv_rn(t[2], N)));
+    if (lam_c > 0.f) L = __fadd_rn(L, __fmul_rn(lam_c, __fdiv_rn(t[3], (float)B)));
+    if (lam_e > 0.f) L = __fadd_rn(L, __fmul_rn(lam_e, __fdiv_rn(t[4], (float)B)));
+    *loss = L;
+    *flux_loss = fl;
+  }
+}
+
 constexpr int kWgradSplits = 256;
 constexpr int kInputSplits = 1024;
 
@@ -674,6 +781,27 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   if (grad_nf)
     hipLaunchKernelGGL(input_dgrad_kernel, dim3((unsigned)((N * F + 255) / 256)), dim3(256), 0, s, d0, w.w_in, F, H, N,
                        grad_nf);
+  return hipGetLastError();
+}
+
+int64_t ablation_loss_ws_bytes(int B, int nx) {
+  return (int64_t)(2 * al256(sizeof(float) * (size_t)B * nx) + al256(sizeof(float) * (size_t)B * 7));
+}
+
+hipError_t launch_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx,
+                                float c, float dx, const float *lam, const double *pc, float *loss, float *flux_loss,
+                                float *dfe, void *ws, hipStream_t s) {
+  char *p = static_cast<char *>(ws);
+  float *nn = reinterpret_cast<float *>(p);
+  float *En = reinterpret_cast<float *>(p + al256(sizeof(float) * (size_t)B * nx));
+  float *part = reinterpret_cast<float *>(p + 2 * al256(sizeof(float) * (size_t)B * nx));
+  hipLaunchKernelGGL(loss_update_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, nx, c, nn);
+  hipError_t e = launch_poisson(nn, nx, En, nx, pc, B, nx, s);  // detached E' (:138-145)
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(loss_terms_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, ft, sn, nn, En, B, nx, c, lam[0],
+                     part, dfe);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, s, part, B, nx, dx, lam[0], lam[1], lam[2], lam[3],
+                     loss, flux_loss);
   return hipGetLastError();
 }
 

@@ -375,3 +375,30 @@ def rollout_summary(metrics, mse=None, metrics_ref=None, drift=False):
         check(lib().hf_rollout_summary(ptr(metrics), ptr(mse), ptr(metrics_ref), B, T1 - 1, ptr(summ), ptr(dr),
                                        stream_of(dev)))
     return summ, dr
+
+
+def ablation_loss_terms(grid, flux_edge, st, ft, sn, lam):
+    """hf_ablation_loss: the single-step terms of the reference trainer's loss
+    (scripts/training/train_ablation.py:120-170) for B samples.  flux_edge
+    [B, 2nx], st / sn [B,3,nx], ft [B,nx] device tensors; lam = (lambda_state,
+    lambda_poisson, lambda_charge, lambda_energy_one).  Returns (loss, flux
+    MSE, d loss / d flux_edge [B, 2nx])."""
+    for t, what in ((flux_edge, "flux_edge"), (st, "state_t"), (ft, "flux_t"), (sn, "state_next")):
+        require_device(t, what)
+    B, _, nx = st.shape
+    dev = st.device
+    fe = flux_edge.detach().to(torch.float32).contiguous()
+    st, ft, sn = (t.to(torch.float32).contiguous() for t in (st, ft, sn))
+    if fe.numel() != B * 2 * nx or ft.shape != (B, nx) or sn.shape != st.shape or nx != grid.nx:
+        raise ValueError("ablation loss: shapes must be flux_edge [B,2nx], states [B,3,nx], flux_t [B,nx]")
+    loss = torch.empty((), device=dev)
+    fl = torch.empty((), device=dev)
+    dfe = torch.empty(B, 2 * nx, device=dev)
+    ws = torch.empty(int(lib().hf_ablation_loss_workspace_bytes(B, nx)), dtype=torch.uint8, device=dev)
+    lam_h = np.asarray(lam, dtype=np.float32)
+    _, pc = grid.on(dev)
+    with torch.cuda.device(dev):
+        check(lib().hf_ablation_loss(ptr(fe), ptr(st), ptr(ft), ptr(sn), B, nx, grid.c32, float(np.float32(grid.dx)),
+                                     ptr(lam_h), ptr(pc), ptr(loss), ptr(fl), ptr(dfe), ptr(ws),
+                                     ws.numel(), stream_of(dev)))
+    return loss, fl, dfe

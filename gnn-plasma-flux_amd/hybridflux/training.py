@@ -40,14 +40,39 @@ def _poisson_detached(grid, n):
     return engine.poisson(grid, n.detach())
 
 
-def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0):
+class _StepLoss(torch.autograd.Function):
+    """The single-step loss terms as one HIP pass (hf_ablation_loss): forward
+    returns (loss, flux_loss) and keeps d loss / d flux_edge, which backward
+    scales by the incoming gradient.  flux_loss is for reporting only."""
+
+    @staticmethod
+    def forward(ctx, flux_edge, st, ft, sn, grid, lam):
+        loss, fl, dfe = engine.ablation_loss_terms(grid, flux_edge, st, ft, sn, lam)
+        ctx.save_for_backward(dfe)
+        ctx.mark_non_differentiable(fl)
+        return loss, fl
+
+    @staticmethod
+    def backward(ctx, g_loss, g_fl):
+        (dfe,) = ctx.saved_tensors
+        return dfe * g_loss, None, None, None, None, None
+
+
+def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0, fused=True):
     """Loss of train_ablation.py:107-200 for a batch: st, st_next [B,3,nx], ft [B,nx]
-    on the device.  Returns (loss, flux_loss); B=1 is the reference formula."""
+    on the device.  Returns (loss, flux_loss); B=1 is the reference formula.
+    fused: the single-step terms (:124-170) in one HIP pass (hf_ablation_loss)
+    instead of the torch expressions below (kept as the readable statement of
+    the same arithmetic, and for the comparison test)."""
     B, _, nx = st.shape
     n_t, u_t = st[:, 0], st[:, 1]
     n_next_true, u_next_true, E_next_true = st_next[:, 0], st_next[:, 1], st_next[:, 2]
     nf, ei = build_chain_graph_batch(st, x)
     flux_edge = model(nf, ei).reshape(B, 2 * nx)
+    if fused and n0 == 1.0 and abs(dt / dx - grid.dt / grid.dx) <= 1e-12 * abs(dt / dx):
+        lam = (cfg["lambda_state"], cfg["lambda_poisson"], cfg["lambda_charge"], cfg["lambda_energy_one"])
+        loss, flux_loss = _StepLoss.apply(flux_edge, st, ft, st_next, grid, lam)
+        return _rollout_term(model, st, x, dt, dx, cfg, grid, B, nx, loss), flux_loss
     F_pred = 0.5 * (flux_edge[:, :nx] + flux_edge[:, nx:])                        # :124-126
     flux_loss = _mse(F_pred, ft)                                                   # :129
     loss = flux_loss
@@ -67,6 +92,11 @@ def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0):
         e_p = 0.5 * torch.mean(u_next_true ** 2 + E_next_pred ** 2, dim=-1)
         e_t = 0.5 * torch.mean(u_next_true ** 2 + E_next_true ** 2, dim=-1)
         loss = loss + cfg["lambda_energy_one"] * _mse(e_p, e_t)
+    return _rollout_term(model, st, x, dt, dx, cfg, grid, B, nx, loss), flux_loss
+
+
+def _rollout_term(model, st, x, dt, dx, cfg, grid, B, nx, loss):
+    """+ lambda_energy_multi * the multi-step rollout energy term (:173-205)."""
     if cfg["rollout_steps"] > 0 and cfg["lambda_energy_multi"] > 0:               # :173-200
         state = st.clone()
         energies = []
@@ -82,7 +112,7 @@ def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0):
             state = torch.stack([n_next_r, u_next_r, _poisson_detached(grid, n_next_r)], dim=1)
         energies = torch.stack(energies)                                           # [K, B]
         loss = loss + cfg["lambda_energy_multi"] * torch.mean((energies - energies[0]) ** 2)
-    return loss, flux_loss
+    return loss
 
 
 class FluxDataset:

@@ -143,9 +143,12 @@ int hf_graph_flux(hf_model_t model, const float *dev_node_features, int64_t N,
  * Weight gradients are split-K sums reduced in a fixed order: bitwise
  * deterministic for a given N, E.  chain_nx > 0 declares that edge_index is
  * N/chain_nx disjoint periodic chains of chain_nx cells in build_chain_graph
- * order (src/graph_constructor.py:34-38, E == 2N): the edge buckets are then
- * formed arithmetically instead of by the count/scan/fill CSR build.  0 for
- * any other graph.
+ * order (src/graph_constructor.py:34-38, E == 2N): with hidden a power of two
+ * in [4, 256] and in_dim <= 8 the chain training path runs (the aggregation as
+ * a stencil inside the GEMM operand loads, the edge readout split into
+ * per-node P/Q GEMMs, f32 MFMA GEMMs throughout); otherwise the edge buckets
+ * are formed arithmetically instead of by the count/scan/fill CSR build.  0
+ * for any other graph.
  */
 int64_t hf_graph_tape_bytes(int in_dim, int hidden, int layers, int64_t N, int64_t E);
 int64_t hf_graph_backward_workspace_bytes(int in_dim, int hidden, int layers, int64_t N, int64_t E);
@@ -156,6 +159,26 @@ int hf_graph_backward(const float *dev_params, int in_dim, int hidden, int layer
                       const float *dev_node_features, int64_t N, const int64_t *dev_edge_index, int64_t E,
                       int chain_nx, const void *dev_tape, const float *dev_grad_flux, float *dev_grad_params,
                       float *dev_grad_node_features, void *dev_workspace, void *stream);
+
+/*
+ * Replaces: the single-step terms of the reference trainer's ablation loss
+ * (scripts/training/train_ablation.py:120-170: flux MSE, state MSE of the
+ * finite-volume continuity update, Poisson MSE, charge and one-step energy
+ * terms), batched over B samples as hybridflux.training.ablation_loss does.
+ * dev_flux_edge [B][2nx] (FluxGNN output), dev_state_t / dev_state_next
+ * [B][3][nx], dev_flux_t [B][nx]; c = f32(dt/dx), dx = f32(dx); lam[4] =
+ * lambda_state, lambda_poisson, lambda_charge, lambda_energy_one; dev_c the
+ * Poisson plan.  Writes dev_loss[0] = loss, dev_flux_loss[0] = the flux MSE
+ * term and dev_dflux_edge
+ * [B][2nx] = d loss / d flux_edge (the Poisson and energy terms go through a
+ * detached solve, as in the reference, and the charge term's gradient is
+ * identically 0).  dev_workspace: hf_ablation_loss_workspace_bytes(B, nx).
+ */
+int64_t hf_ablation_loss_workspace_bytes(int B, int nx);
+int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const float *dev_flux_t,
+                     const float *dev_state_next, int B, int nx, float c, float dx, const float *lam,
+                     const double *dev_c, float *dev_loss, float *dev_flux_loss, float *dev_dflux_edge,
+                     void *dev_workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * The reference's other rollout models, inference.

@@ -289,3 +289,28 @@ def test_graphed_steps_equal_eager(hf):
     assert abs(res[0][0] - res[1][0]) <= 1e-6 * abs(res[0][0])
     for k in res[0][1]:
         assert np.abs(res[0][1][k] - res[1][1][k]).max() <= 1e-6, k
+
+
+@pytest.mark.parametrize("cfg_name", ["baseline", "physics", "full"])
+def test_fused_step_loss_equals_torch_terms(hf, cfg_name):
+    """hf_ablation_loss (the loss's single-step terms in one HIP pass, with its
+    own d loss / d flux_edge) against the same terms as torch expressions
+    (ablation_loss(fused=False)) on 48 samples: loss and parameter gradients."""
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import ablation_loss
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=3, steps_per_ic=16, out_path=None, device=DEV)
+    st, ft, sn = (torch.as_tensor(a, device=DEV) for a in (st, ft, sn))
+    solver = hf.BaselineSolver(64, device=DEV)
+    xd = torch.as_tensor(x, device=DEV)
+    cfg = hf.ABLATION_CONFIGS[cfg_name]
+    m = _w1_model(hf)
+    out = []
+    for fused in (True, False):
+        m.zero_grad()
+        loss, fl = ablation_loss(m, st, ft, sn, xd, solver.dt, solver.dx, cfg, solver.grid, fused=fused)
+        loss.backward()
+        out.append((loss.item(), fl.item(), {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}))
+    assert abs(out[0][0] - out[1][0]) <= 2e-6 * abs(out[1][0])
+    assert abs(out[0][1] - out[1][1]) <= 2e-6 * abs(out[1][1])
+    for k in out[0][2]:
+        grads_close(out[0][2][k], out[1][2][k], 1e-5)
