@@ -108,7 +108,7 @@ struct EpiAct {
   const float *bias;
   int nbias;
   bool relu;
-  __device__ void operator()(int64_t i, int64_t j, float v, int) const {
+  __device__ void operator()(int64_t i, int64_t j, float v) const {
     if (bias && j < nbias) v = __fadd_rn(v, bias[j]);
     if (relu) v = v > 0.f ? v : (v == v ? 0.f : v);  // NaN stays NaN, as torch.relu
     out[i * ld + j] = v;
@@ -119,14 +119,12 @@ struct EpiMask {
   int64_t ld;
   const float *mask;
   int64_t ldm;
-  __device__ void operator()(int64_t i, int64_t j, float v, int) const {
-    out[i * ld + j] = mask[i * ldm + j] > 0.f ? v : 0.f;
-  }
+  __device__ void operator()(int64_t i, int64_t j, float v) const { out[i * ld + j] = mask[i * ldm + j] > 0.f ? v : 0.f; }
 };
 struct EpiPart {
   float *part;
   int64_t I, J;
-  __device__ void operator()(int64_t i, int64_t j, float v, int z) const { part[((int64_t)z * I + i) * J + j] = v; }
+  __device__ void operator()(int64_t i, int64_t j, float v) const { part[(blockIdx.z * I + i) * J + j] = v; }
 };
 
 // C[i][j] = sum_{r in split} A(i, r) B(r, j) over I x J, R.  A(i, r) = GA(r, i)
@@ -135,82 +133,55 @@ struct EpiPart {
 // rows as they are; the MFMA reads adapt: an [i][r] tile gives each lane four
 // consecutive r in one ds_read_b128 (MFMA step s of lane half h uses
 // r = 8g + 4h + s), an [r][i] tile one ds_read_b32 per MFMA at the same r.
-// Tiles (x = row tile fastest, y = column tile, z = reduction split) are dealt
-// round-robin to a persistent grid of two workgroups per CU; the loads of a
-// workgroup's next tile are in flight while it finishes and stores the
-// current one, so no tile starts on an exposed HBM round trip.
-// COLSUM (ARM A only, one tile per workgroup): the split's column sums of GA
-// over its rows (the bias gradient), written to bias_part[split][i] by the
-// workgroups of column tile 0.
+// COLSUM (ARM A only): the split's column sums of GA over its rows (the bias
+// gradient), written to bias_part[split][i] by the blocks of column tile 0.
 template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM>
 __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, int64_t I, int64_t J, int64_t R,
-                                                       int64_t rsplit, int tx, int ty, int tz, float *bias_part) {
+                                                       int64_t rsplit, float *bias_part) {
   __shared__ float sA[2][kTileF];
   __shared__ float sB[2][kTileF];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wi = wave >> 1, wj = wave & 1, h = lane >> 5;
-  const int ntiles = tx * ty * tz;
-  struct Tile {
-    int64_t i0, j0, rb, re;
-    int z, y;
-  };
-  auto tile_of = [&](int id) {
-    Tile T;
-    const int x = id % tx, yz = id / tx;
-    T.y = yz % ty;
-    T.z = yz / ty;
-    T.i0 = (int64_t)x * kBM;
-    T.j0 = (int64_t)T.y * kBN;
-    T.rb = (int64_t)T.z * rsplit;
-    T.re = T.rb + rsplit < R ? T.rb + rsplit : R;
-    return T;
-  };
-  int id = blockIdx.x;
-  if (id >= ntiles) return;
-  Tile C = tile_of(id);
+  const int64_t i0 = (int64_t)blockIdx.x * kBM, j0 = (int64_t)blockIdx.y * kBN;
+  const int64_t rb = (int64_t)blockIdx.z * rsplit;
+  const int64_t re = rb + rsplit < R ? rb + rsplit : R;
   f16 acc[2][2];
-  auto zero_acc = [&]() {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
-  };
-  zero_acc();
+      for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
   f4 ra[4], rbv[4], csum = f4{0.f, 0.f, 0.f, 0.f};
   // thread -> (global row, col) of its 4 float4 per operand per stage.  The
-  // rows of an [i][r] operand are the same for every stage of a tile: their
-  // handles are made once per tile.
+  // rows of an [i][r] operand are the same every stage: their handles are made once.
   typename LA::Row rowa[4];
   typename LB::Row rowb[4];
-  auto make_rows = [&](const Tile &T) {
-    if (!ARM) {
+  if (!ARM) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rowa[q] = ga.row(T.i0 + ((t + 256 * q) >> 3));
-    }
-    if (!BRM) {
+    for (int q = 0; q < 4; ++q) rowa[q] = ga.row(i0 + ((t + 256 * q) >> 3));
+  }
+  if (!BRM) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rowb[q] = gb.row(T.j0 + ((t + 256 * q) >> 3));
-    }
-  };
-  auto gload = [&](const Tile &T, int64_t r0) {
+    for (int q = 0; q < 4; ++q) rowb[q] = gb.row(j0 + ((t + 256 * q) >> 3));
+  }
+  auto gload = [&](int64_t r0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int idx = t + 256 * q;
-      if (ARM) ra[q] = ga.load4(ga.row(r0 + (idx >> 5)), (int)(T.i0 + 4 * (idx & 31)));
-      else ra[q] = (r0 + 4 * (idx & 7) < T.re) ? ga.load4(rowa[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
-      if (BRM) rbv[q] = gb.load4(gb.row(r0 + (idx >> 5)), (int)(T.j0 + 4 * (idx & 31)));
-      else rbv[q] = (r0 + 4 * (idx & 7) < T.re) ? gb.load4(rowb[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
+      if (ARM) ra[q] = ga.load4(ga.row(r0 + (idx >> 5)), (int)(i0 + 4 * (idx & 31)));
+      else ra[q] = (r0 + 4 * (idx & 7) < re) ? ga.load4(rowa[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
+      if (BRM) rbv[q] = gb.load4(gb.row(r0 + (idx >> 5)), (int)(j0 + 4 * (idx & 31)));
+      else rbv[q] = (r0 + 4 * (idx & 7) < re) ? gb.load4(rowb[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
     }
     if (ARM) {  // rows past this split's end belong to the next split
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (r0 + ((t + 256 * q) >> 5) >= T.re) ra[q] = f4{0.f, 0.f, 0.f, 0.f};
+        if (r0 + ((t + 256 * q) >> 5) >= re) ra[q] = f4{0.f, 0.f, 0.f, 0.f};
     }
     if (BRM) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (r0 + ((t + 256 * q) >> 5) >= T.re) rbv[q] = f4{0.f, 0.f, 0.f, 0.f};
+        if (r0 + ((t + 256 * q) >> 5) >= re) rbv[q] = f4{0.f, 0.f, 0.f, 0.f};
     }
     if (COLSUM) {
 #pragma unroll
@@ -227,8 +198,16 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
       *reinterpret_cast<f4 *>(pb) = rbv[q];
     }
   };
-  auto compute = [&](int buf) {
-    const float *A = sA[buf], *B = sB[buf];
+  if (rb < re) {
+    gload(rb);
+    lstore(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int64_t r0 = rb; r0 < re; r0 += kKC) {
+    const bool more = r0 + kKC < re;
+    if (more) gload(r0 + kKC);
+    const float *A = sA[cur], *B = sB[cur];
 #pragma unroll
     for (int g = 0; g < kKC / 8; ++g) {
       float av[2][4], bv[2][4];
@@ -259,59 +238,22 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #pragma unroll
           for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][s], bv[b][s], acc[a][b], 0, 0, 0);
     }
-  };
-  auto epilogue = [&](const Tile &T) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int64_t j = T.j0 + 64 * wj + 32 * b + (lane & 31);
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int64_t i = T.i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3);
-          if (i < I && j < J) epi(i, j, acc[a][b][v], T.z);
-        }
-      }
-  };
-  make_rows(C);
-  if (C.rb < C.re) {
-    gload(C, C.rb);
-    lstore(0);
-  }
-  __syncthreads();
-  int cur = 0;
-  int64_t r0 = C.rb;
-  for (;;) {
-    // the next stage to load: this tile's, or the first of the workgroup's next tile
-    const bool more = r0 + kKC < C.re;
-    const int nid = id + (int)gridDim.x;
-    const bool next_tile = !more && !COLSUM && nid < ntiles;
-    Tile N = C;
-    if (more) {
-      gload(C, r0 + kKC);
-    } else if (next_tile) {
-      N = tile_of(nid);
-      make_rows(N);
-      if (N.rb < N.re) gload(N, N.rb);
-    }
-    if (C.rb < C.re) compute(cur);
-    if (!more) {
-      epilogue(C);
-      zero_acc();
-    }
-    if (more || (next_tile && N.rb < N.re)) lstore(cur ^ 1);
+    if (more) lstore(cur ^ 1);
     __syncthreads();
     cur ^= 1;
-    if (more) {
-      r0 += kKC;
-      continue;
-    }
-    if (!next_tile) break;
-    id = nid;
-    C = N;
-    r0 = C.rb;
   }
-  if (COLSUM && C.y == 0) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int64_t j = j0 + 64 * wj + 32 * b + (lane & 31);
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int64_t i = i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3);
+        if (i < I && j < J) epi(i, j, acc[a][b][v]);
+      }
+    }
+  if (COLSUM && blockIdx.y == 0) {
     // thread t summed the rows t>>5 (+8q) of columns 4(t&31)..+3: fold the 8 row groups in order
     __shared__ f4 s_cs[256];
     s_cs[t] = csum;
@@ -322,20 +264,11 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
       for (int g = 1; g < 8; ++g) v += s_cs[t + 32 * g];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t i = C.i0 + 4 * t + e;
-        if (i < I) bias_part[(int64_t)C.z * I + i] = v[e];
+        const int64_t i = i0 + 4 * t + e;
+        if (i < I) bias_part[(int64_t)blockIdx.z * I + i] = v[e];
       }
     }
   }
-}
-
-inline int persistent_slots() {
-  static const int slots = [] {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return 2 * (cus > 0 ? cus : 256);
-  }();
-  return slots;
 }
 
 template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM = false>
@@ -344,13 +277,10 @@ hipError_t tgemm(const LA &ga, const LB &gb, const Epi &epi, int64_t I, int64_t 
   if (I <= 0 || J <= 0) return hipSuccess;
   int64_t rsplit = (R + splits - 1) / splits;
   rsplit = (rsplit + kKC - 1) / kKC * kKC;
-  if (rsplit <= 0) rsplit = kKC;
   const int64_t S = R > 0 ? (R + rsplit - 1) / rsplit : 1;
-  const int tx = (int)((I + kBM - 1) / kBM), ty = (int)((J + kBN - 1) / kBN), tz = (int)S;
-  const int64_t ntiles = (int64_t)tx * ty * tz;
-  const int64_t blocks = COLSUM ? ntiles : std::min<int64_t>(ntiles, persistent_slots());
-  hipLaunchKernelGGL((tgemm_kernel<LA, ARM, LB, BRM, Epi, COLSUM>), dim3((unsigned)blocks), dim3(256), 0, s, ga, gb,
-                     epi, I, J, R, rsplit, tx, ty, tz, bias_part);
+  dim3 grid((unsigned)((I + kBM - 1) / kBM), (unsigned)((J + kBN - 1) / kBN), (unsigned)S);
+  hipLaunchKernelGGL((tgemm_kernel<LA, ARM, LB, BRM, Epi, COLSUM>), grid, dim3(256), 0, s, ga, gb, epi, I, J, R,
+                     rsplit > 0 ? rsplit : kKC, bias_part);
   return hipGetLastError();
 }
 // number of splits tgemm makes of R for a requested count
