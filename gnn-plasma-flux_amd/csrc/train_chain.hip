@@ -26,6 +26,7 @@
 // and the data gradient masked by the ReLU of the layer below.
 #include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "hf_internal.h"
 
@@ -61,43 +62,45 @@ struct VPlain {
   int64_t hoff;
   int cols;
   struct Row {
-    const float *ptr;  // nullptr: outside the matrix
+    int off;  // float offset of the row from p (< 2^31, host-checked); -1: outside the matrix
   };
   __device__ Row row(int64_t r) const {
-    if (r >= rows) return Row{nullptr};
+    if (r >= rows) return Row{-1};
     const int64_t lo = r & ((int64_t(1) << hshift) - 1), hi = r >> hshift;
-    return Row{p + lo * ld + hi * hoff};
+    return Row{(int)(lo * ld + hi * hoff)};
   }
   __device__ f4 load4(const Row &w, int c) const {
-    if (!w.ptr || c >= cols) return f4{0.f, 0.f, 0.f, 0.f};
-    return *reinterpret_cast<const f4 *>(w.ptr + c);
+    if (w.off < 0 || c >= cols) return f4{0.f, 0.f, 0.f, 0.f};
+    return *reinterpret_cast<const f4 *>(p + (unsigned)w.off + c);
   }
+  bool fits32() const { return (rows - 1 + 1) * ld + cols + (rows >> hshift) * hoff < (int64_t(1) << 31); }
 };
 constexpr int kNoSplit = 62;
 // [X ; agg X] of X [rows][C] on chains of nx rows: cols [0, C) are X, [C, 2C)
 // are (X[prev] + X[next]) * 0.5 (src/flux_gnn.py:53-59 on the chain).  The
-// row handle holds the three row pointers (one 32-bit remainder per row, rows
-// < 2^31), computed once per row rather than per load.
+// row handle holds the three row offsets (one 32-bit remainder per row, rows
+// < 2^31, offsets < 2^31), computed once per row rather than per load.
 struct VStencil {
   const float *X;
   int64_t rows;
   int C, nx;
   struct Row {
-    const float *self, *nxt, *prv;  // self == nullptr: outside the matrix
+    int self, nxt, prv;  // float offsets of the rows (nxt, prv less C); self < 0: outside the matrix
   };
   __device__ Row row(int64_t r) const {
-    if (r >= rows) return Row{nullptr, nullptr, nullptr};
+    if (r >= rows) return Row{-1, 0, 0};
     const int i = (int)((unsigned)r % (unsigned)nx);
     const int64_t nr = r + (i == nx - 1 ? 1 - nx : 1), pr = r + (i == 0 ? nx - 1 : -1);
-    return Row{X + r * C, X + nr * C - C, X + pr * C - C};
+    return Row{(int)(r * C), (int)(nr * C - C), (int)(pr * C - C)};
   }
   __device__ f4 load4(const Row &w, int c) const {
-    if (!w.self || c >= 2 * C) return f4{0.f, 0.f, 0.f, 0.f};
-    if (c < C) return *reinterpret_cast<const f4 *>(w.self + c);
-    const f4 a = *reinterpret_cast<const f4 *>(w.nxt + c);
-    const f4 b = *reinterpret_cast<const f4 *>(w.prv + c);
+    if (w.self < 0 || c >= 2 * C) return f4{0.f, 0.f, 0.f, 0.f};
+    if (c < C) return *reinterpret_cast<const f4 *>(X + (unsigned)w.self + c);
+    const f4 a = *reinterpret_cast<const f4 *>(X + (unsigned)(w.nxt + c));
+    const f4 b = *reinterpret_cast<const f4 *>(X + (unsigned)(w.prv + c));
     return (a + b) * 0.5f;
   }
+  bool fits32() const { return rows * C + C < (int64_t(1) << 31); }
 };
 
 // Epilogues: out[i][j] = act(v + bias[j]) (bias on j < nbias), or v masked by mask[i][j] > 0,
@@ -151,7 +154,10 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
-  f4 ra[4], rbv[4], csum = f4{0.f, 0.f, 0.f, 0.f};
+  // Two register sets of 4 float4 per operand: the loads of stage s+2 are
+  // issued while stage s computes and land in LDS at the end of stage s+1, so
+  // each load has two stages (~2 x 4096 MFMA cycles per wave) to arrive.
+  f4 ra[2][4], rbv[2][4], csum = f4{0.f, 0.f, 0.f, 0.f};
   // thread -> (global row, col) of its 4 float4 per operand per stage.  The
   // rows of an [i][r] operand are the same every stage: their handles are made once.
   typename LA::Row rowa[4];
@@ -164,49 +170,48 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #pragma unroll
     for (int q = 0; q < 4; ++q) rowb[q] = gb.row(j0 + ((t + 256 * q) >> 3));
   }
-  auto gload = [&](int64_t r0) {
+  auto gload = [&](int set, int64_t r0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int idx = t + 256 * q;
-      if (ARM) ra[q] = ga.load4(ga.row(r0 + (idx >> 5)), (int)(i0 + 4 * (idx & 31)));
-      else ra[q] = (r0 + 4 * (idx & 7) < re) ? ga.load4(rowa[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
-      if (BRM) rbv[q] = gb.load4(gb.row(r0 + (idx >> 5)), (int)(j0 + 4 * (idx & 31)));
-      else rbv[q] = (r0 + 4 * (idx & 7) < re) ? gb.load4(rowb[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
+      if (ARM) ra[set][q] = ga.load4(ga.row(r0 + (idx >> 5)), (int)(i0 + 4 * (idx & 31)));
+      else ra[set][q] = (r0 + 4 * (idx & 7) < re) ? ga.load4(rowa[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
+      if (BRM) rbv[set][q] = gb.load4(gb.row(r0 + (idx >> 5)), (int)(j0 + 4 * (idx & 31)));
+      else rbv[set][q] = (r0 + 4 * (idx & 7) < re) ? gb.load4(rowb[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
     }
     if (ARM) {  // rows past this split's end belong to the next split
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (r0 + ((t + 256 * q) >> 5) >= re) ra[q] = f4{0.f, 0.f, 0.f, 0.f};
+        if (r0 + ((t + 256 * q) >> 5) >= re) ra[set][q] = f4{0.f, 0.f, 0.f, 0.f};
     }
     if (BRM) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (r0 + ((t + 256 * q) >> 5) >= re) rbv[q] = f4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (COLSUM) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) csum += ra[q];
+        if (r0 + ((t + 256 * q) >> 5) >= re) rbv[set][q] = f4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, int set) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int idx = t + 256 * q;
       float *pa = ARM ? &sA[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sA[buf][(idx >> 3) * kStrIM + 4 * (idx & 7)];
       float *pb = BRM ? &sB[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sB[buf][(idx >> 3) * kStrIM + 4 * (idx & 7)];
-      *reinterpret_cast<f4 *>(pa) = ra[q];
-      *reinterpret_cast<f4 *>(pb) = rbv[q];
+      *reinterpret_cast<f4 *>(pa) = ra[set][q];
+      *reinterpret_cast<f4 *>(pb) = rbv[set][q];
+      if (COLSUM) csum += ra[set][q];
     }
   };
   if (rb < re) {
-    gload(rb);
-    lstore(0);
+    gload(0, rb);
+    if (rb + kKC < re) gload(1, rb + kKC);
+    lstore(0, 0);
   }
   __syncthreads();
-  int cur = 0;
-  for (int64_t r0 = rb; r0 < re; r0 += kKC) {
-    const bool more = r0 + kKC < re;
-    if (more) gload(r0 + kKC);
+  // one stage; register sets and LDS buffers indexed by the compile-time parity
+  auto stage = [&](auto parity, int64_t r0) {
+    constexpr int cur = decltype(parity)::value;
+    // LDS[cur] holds stage r0; register set cur^1 holds (in flight) stage r0 + kKC
+    if (r0 + 2 * kKC < re) gload(cur, r0 + 2 * kKC);
     const float *A = sA[cur], *B = sB[cur];
 #pragma unroll
     for (int g = 0; g < kKC / 8; ++g) {
@@ -238,9 +243,15 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #pragma unroll
           for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][s], bv[b][s], acc[a][b], 0, 0, 0);
     }
-    if (more) lstore(cur ^ 1);
+    if (r0 + kKC < re) lstore(cur ^ 1, cur ^ 1);
     __syncthreads();
-    cur ^= 1;
+  };
+  for (int64_t r0 = rb; r0 < re;) {
+    stage(std::integral_constant<int, 0>{}, r0);
+    r0 += kKC;
+    if (r0 >= re) break;
+    stage(std::integral_constant<int, 1>{}, r0);
+    r0 += kKC;
   }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -275,6 +286,7 @@ template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM = false
 hipError_t tgemm(const LA &ga, const LB &gb, const Epi &epi, int64_t I, int64_t J, int64_t R, int splits,
                  hipStream_t s, float *bias_part = nullptr) {
   if (I <= 0 || J <= 0) return hipSuccess;
+  if (!ga.fits32() || !gb.fits32()) return hipErrorInvalidValue;  // 32-bit row offsets
   int64_t rsplit = (R + splits - 1) / splits;
   rsplit = (rsplit + kKC - 1) / kKC * kKC;
   const int64_t S = R > 0 ? (R + rsplit - 1) / rsplit : 1;
