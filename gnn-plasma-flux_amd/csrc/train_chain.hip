@@ -62,18 +62,21 @@ struct VPlain {
   int64_t hoff;
   int cols;
   struct Row {
-    int off;  // float offset of the row from p (< 2^31, host-checked); -1: outside the matrix
+    int off;  // float offset of the row from p (< 2^31, host-checked)
   };
+  // Rows past the end are clamped to the last one, columns past the end to the
+  // last float4: the GEMM either discards what such loads feed (output rows /
+  // columns past I / J) or zeroes it (reduction rows past the split's end).
   __device__ Row row(int64_t r) const {
-    if (r >= rows) return Row{-1};
+    r = r < rows ? r : rows - 1;
     const int64_t lo = r & ((int64_t(1) << hshift) - 1), hi = r >> hshift;
     return Row{(int)(lo * ld + hi * hoff)};
   }
   __device__ f4 load4(const Row &w, int c) const {
-    if (w.off < 0 || c >= cols) return f4{0.f, 0.f, 0.f, 0.f};
-    return *reinterpret_cast<const f4 *>(p + (unsigned)w.off + c);
+    c = c < cols ? c : cols - 4;
+    return *reinterpret_cast<const f4 *>(p + (unsigned)(w.off + c));
   }
-  bool fits32() const { return (rows - 1 + 1) * ld + cols + (rows >> hshift) * hoff < (int64_t(1) << 31); }
+  bool fits32() const { return rows * ld + cols + (rows >> hshift) * hoff < (int64_t(1) << 31); }
 };
 constexpr int kNoSplit = 62;
 // [X ; agg X] of X [rows][C] on chains of nx rows: cols [0, C) are X, [C, 2C)
@@ -85,17 +88,17 @@ struct VStencil {
   int64_t rows;
   int C, nx;
   struct Row {
-    int self, nxt, prv;  // float offsets of the rows (nxt, prv less C); self < 0: outside the matrix
+    int self, nxt, prv;  // float offsets of the rows (nxt, prv less C)
   };
   __device__ Row row(int64_t r) const {
-    if (r >= rows) return Row{-1, 0, 0};
+    r = r < rows ? r : rows - 1;
     const int i = (int)((unsigned)r % (unsigned)nx);
     const int64_t nr = r + (i == nx - 1 ? 1 - nx : 1), pr = r + (i == 0 ? nx - 1 : -1);
     return Row{(int)(r * C), (int)(nr * C - C), (int)(pr * C - C)};
   }
   __device__ f4 load4(const Row &w, int c) const {
-    if (w.self < 0 || c >= 2 * C) return f4{0.f, 0.f, 0.f, 0.f};
-    if (c < C) return *reinterpret_cast<const f4 *>(X + (unsigned)w.self + c);
+    c = c < 2 * C ? c : 2 * C - 4;
+    if (c < C) return *reinterpret_cast<const f4 *>(X + (unsigned)(w.self + c));
     const f4 a = *reinterpret_cast<const f4 *>(X + (unsigned)(w.nxt + c));
     const f4 b = *reinterpret_cast<const f4 *>(X + (unsigned)(w.prv + c));
     return (a + b) * 0.5f;
@@ -105,15 +108,16 @@ struct VStencil {
 
 // Epilogues: out[i][j] = act(v + bias[j]) (bias on j < nbias), or v masked by mask[i][j] > 0,
 // or the split's partial tile.
+template <bool RELU>
 struct EpiAct {
   float *out;
   int64_t ld;
   const float *bias;
   int nbias;
-  bool relu;
-  __device__ void operator()(int64_t i, int64_t j, float v) const {
-    if (bias && j < nbias) v = __fadd_rn(v, bias[j]);
-    if (relu) v = v > 0.f ? v : (v == v ? 0.f : v);  // NaN stays NaN, as torch.relu
+  __device__ float bias_of(int64_t j) const { return (bias && j < nbias) ? bias[j] : 0.f; }
+  __device__ void operator()(int64_t i, int64_t j, float v, float bj) const {
+    v = __fadd_rn(v, bj);  // + 0 where there is no bias
+    if (RELU) v = v > 0.f ? v : (v == v ? 0.f : v);  // NaN stays NaN, as torch.relu
     out[i * ld + j] = v;
   }
 };
@@ -122,12 +126,16 @@ struct EpiMask {
   int64_t ld;
   const float *mask;
   int64_t ldm;
-  __device__ void operator()(int64_t i, int64_t j, float v) const { out[i * ld + j] = mask[i * ldm + j] > 0.f ? v : 0.f; }
+  __device__ float bias_of(int64_t) const { return 0.f; }
+  __device__ void operator()(int64_t i, int64_t j, float v, float) const {
+    out[i * ld + j] = mask[i * ldm + j] > 0.f ? v : 0.f;
+  }
 };
 struct EpiPart {
   float *part;
   int64_t I, J;
-  __device__ void operator()(int64_t i, int64_t j, float v) const { part[(blockIdx.z * I + i) * J + j] = v; }
+  __device__ float bias_of(int64_t) const { return 0.f; }
+  __device__ void operator()(int64_t i, int64_t j, float v, float) const { part[(blockIdx.z * I + i) * J + j] = v; }
 };
 
 // C[i][j] = sum_{r in split} A(i, r) B(r, j) over I x J, R.  A(i, r) = GA(r, i)
@@ -157,7 +165,11 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
   // Two register sets of 4 float4 per operand: the loads of stage s+2 are
   // issued while stage s computes and land in LDS at the end of stage s+1, so
   // each load has two stages (~2 x 4096 MFMA cycles per wave) to arrive.
-  f4 ra[2][4], rbv[2][4], csum = f4{0.f, 0.f, 0.f, 0.f};
+#ifndef HF_TG_DEPTH
+#define HF_TG_DEPTH 2
+#endif
+  constexpr int kDepth = HF_TG_DEPTH;  // stages of loads in flight (1: plain double buffer)
+  f4 ra[kDepth][4], rbv[kDepth][4], csum = f4{0.f, 0.f, 0.f, 0.f};
   // thread -> (global row, col) of its 4 float4 per operand per stage.  The
   // rows of an [i][r] operand are the same every stage: their handles are made once.
   typename LA::Row rowa[4];
@@ -170,24 +182,27 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #pragma unroll
     for (int q = 0; q < 4; ++q) rowb[q] = gb.row(j0 + ((t + 256 * q) >> 3));
   }
+  // Branch-free loads: addresses clamped by the views; only reduction rows
+  // past the split's end (RM operands) are zeroed, by select.  [i][r]
+  // operands need R % kKC == 0 (host-checked), so their r never runs past re.
   auto gload = [&](int set, int64_t r0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int idx = t + 256 * q;
-      if (ARM) ra[set][q] = ga.load4(ga.row(r0 + (idx >> 5)), (int)(i0 + 4 * (idx & 31)));
-      else ra[set][q] = (r0 + 4 * (idx & 7) < re) ? ga.load4(rowa[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
-      if (BRM) rbv[set][q] = gb.load4(gb.row(r0 + (idx >> 5)), (int)(j0 + 4 * (idx & 31)));
-      else rbv[set][q] = (r0 + 4 * (idx & 7) < re) ? gb.load4(rowb[q], (int)(r0 + 4 * (idx & 7))) : f4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (ARM) {  // rows past this split's end belong to the next split
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (r0 + ((t + 256 * q) >> 5) >= re) ra[set][q] = f4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (BRM) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (r0 + ((t + 256 * q) >> 5) >= re) rbv[set][q] = f4{0.f, 0.f, 0.f, 0.f};
+      if (ARM) {
+        const f4 v = ga.load4(ga.row(r0 + (idx >> 5)), (int)(i0 + 4 * (idx & 31)));
+        const bool in = r0 + (idx >> 5) < re;
+        ra[set][q] = f4{in ? v[0] : 0.f, in ? v[1] : 0.f, in ? v[2] : 0.f, in ? v[3] : 0.f};
+      } else {
+        ra[set][q] = ga.load4(rowa[q], (int)(r0 + 4 * (idx & 7)));
+      }
+      if (BRM) {
+        const f4 v = gb.load4(gb.row(r0 + (idx >> 5)), (int)(j0 + 4 * (idx & 31)));
+        const bool in = r0 + (idx >> 5) < re;
+        rbv[set][q] = f4{in ? v[0] : 0.f, in ? v[1] : 0.f, in ? v[2] : 0.f, in ? v[3] : 0.f};
+      } else {
+        rbv[set][q] = gb.load4(rowb[q], (int)(r0 + 4 * (idx & 7)));
+      }
     }
   };
   auto lstore = [&](int buf, int set) {
@@ -203,15 +218,19 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
   };
   if (rb < re) {
     gload(0, rb);
-    if (rb + kKC < re) gload(1, rb + kKC);
     lstore(0, 0);
+    if (kDepth == 2 && rb + kKC < re) gload(kDepth - 1, rb + kKC);
   }
   __syncthreads();
   // one stage; register sets and LDS buffers indexed by the compile-time parity
   auto stage = [&](auto parity, int64_t r0) {
     constexpr int cur = decltype(parity)::value;
-    // LDS[cur] holds stage r0; register set cur^1 holds (in flight) stage r0 + kKC
-    if (r0 + 2 * kKC < re) gload(cur, r0 + 2 * kKC);
+    // LDS[cur] holds stage r0; depth 2: register set cur^1 holds (in flight) stage r0 + kKC
+    if (kDepth == 2) {
+      if (r0 + 2 * kKC < re) gload(cur % kDepth, r0 + 2 * kKC);
+    } else if (r0 + kKC < re) {
+      gload(0, r0 + kKC);
+    }
     const float *A = sA[cur], *B = sB[cur];
 #pragma unroll
     for (int g = 0; g < kKC / 8; ++g) {
@@ -243,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #pragma unroll
           for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][s], bv[b][s], acc[a][b], 0, 0, 0);
     }
-    if (r0 + kKC < re) lstore(cur ^ 1, cur ^ 1);
+    if (r0 + kKC < re) lstore(cur ^ 1, (cur ^ 1) % kDepth);
     __syncthreads();
   };
   for (int64_t r0 = rb; r0 < re;) {
@@ -253,17 +272,30 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
     stage(std::integral_constant<int, 1>{}, r0);
     r0 += kKC;
   }
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
+  if (i0 + kBM <= I && j0 + kBN <= J) {  // workgroup-uniform: interior tiles store unchecked
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int64_t j = j0 + 64 * wj + 32 * b + (lane & 31);
+      const float bj = epi.bias_of(j);
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int64_t i = i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3);
-        if (i < I && j < J) epi(i, j, acc[a][b][v]);
-      }
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) epi(i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3), j, acc[a][b][v], bj);
     }
+  } else {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int64_t j = j0 + 64 * wj + 32 * b + (lane & 31);
+      const float bj = j < J ? epi.bias_of(j) : 0.f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int64_t i = i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3);
+          if (i < I && j < J) epi(i, j, acc[a][b][v], bj);
+        }
+    }
+  }
   if (COLSUM && blockIdx.y == 0) {
     // thread t summed the rows t>>5 (+8q) of columns 4(t&31)..+3: fold the 8 row groups in order
     __shared__ f4 s_cs[256];
@@ -287,6 +319,7 @@ hipError_t tgemm(const LA &ga, const LB &gb, const Epi &epi, int64_t I, int64_t 
                  hipStream_t s, float *bias_part = nullptr) {
   if (I <= 0 || J <= 0) return hipSuccess;
   if (!ga.fits32() || !gb.fits32()) return hipErrorInvalidValue;  // 32-bit row offsets
+  if ((!ARM || !BRM) && R % kKC != 0) return hipErrorInvalidValue;  // [i][r] operands: whole chunks
   int64_t rsplit = (R + splits - 1) / splits;
   rsplit = (rsplit + kKC - 1) / kKC * kKC;
   const int64_t S = R > 0 ? (R + rsplit - 1) / rsplit : 1;
@@ -695,7 +728,7 @@ hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t 
   for (int l = 0; l < L; ++l) {  // h[l+1] = ReLU(b_l + W_l [h[l] ; agg h[l]])               (:53-60)
     const VStencil A{t.h[l], N, H, nx};
     const VPlain B{w.w_l + l * w.lsw, 2LL * H, H, kNoSplit, 0, 2 * H};
-    if ((e = tgemm<VStencil, false, VPlain, false>(A, B, EpiAct{t.h[l + 1], H, w.b_l + l * w.lsb, H, true}, N, H,
+    if ((e = tgemm<VStencil, false, VPlain, false>(A, B, EpiAct<true>{t.h[l + 1], H, w.b_l + l * w.lsb, H}, N, H,
                                                    2 * H, 1, s)))
       return e;
   }
@@ -703,7 +736,7 @@ hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t 
   // edge_mlp.0.weight[c % H][(c / H) * H ...]
   const VPlain A{t.h[L], H, N, kNoSplit, 0, H};
   const VPlain B{w.w_e, 2LL * H, 2LL * H, hsh, H, H};
-  if ((e = tgemm<VPlain, false, VPlain, false>(A, B, EpiAct{t.pq, 2LL * H, w.b_e, H, false}, N, 2 * H, H, 1, s)))
+  if ((e = tgemm<VPlain, false, VPlain, false>(A, B, EpiAct<false>{t.pq, 2LL * H, w.b_e, H}, N, 2 * H, H, 1, s)))
     return e;
   hipLaunchKernelGGL(edge_forward_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, t.pq, H, N, nx, w.w_2,
                      w.b_2, flux);
