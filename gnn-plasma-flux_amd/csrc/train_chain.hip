@@ -166,9 +166,10 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
   // issued while stage s computes and land in LDS at the end of stage s+1, so
   // each load has two stages (~2 x 4096 MFMA cycles per wave) to arrive.
 #ifndef HF_TG_DEPTH
-#define HF_TG_DEPTH 2
+#define HF_TG_DEPTH 1
 #endif
-  constexpr int kDepth = HF_TG_DEPTH;  // stages of loads in flight (1: plain double buffer)
+  constexpr int kDepth = HF_TG_DEPTH;  // stages of loads in flight: 1 (double buffer) and 2 measured equal
+  // (profiles/r03_train_gemm_depth_ab.txt); 1 holds ~30 fewer registers
   f4 ra[kDepth][4], rbv[kDepth][4], csum = f4{0.f, 0.f, 0.f, 0.f};
   // thread -> (global row, col) of its 4 float4 per operand per stage.  The
   // rows of an [i][r] operand are the same every stage: their handles are made once.
