@@ -115,7 +115,9 @@ struct EpiAct {
   const float *bias;
   int nbias;
   __device__ float bias_of(int64_t j) const { return (bias && j < nbias) ? bias[j] : 0.f; }
-  __device__ void operator()(int64_t i, int64_t j, float v, float bj) const {
+  static constexpr bool kPre = false;
+  __device__ float pre(int64_t, int64_t) const { return 0.f; }
+  __device__ void operator()(int64_t i, int64_t j, float v, float bj, float) const {
     v = __fadd_rn(v, bj);  // + 0 where there is no bias
     if (RELU) v = v > 0.f ? v : (v == v ? 0.f : v);  // NaN stays NaN, as torch.relu
     out[i * ld + j] = v;
@@ -127,15 +129,20 @@ struct EpiMask {
   const float *mask;
   int64_t ldm;
   __device__ float bias_of(int64_t) const { return 0.f; }
-  __device__ void operator()(int64_t i, int64_t j, float v, float) const {
-    out[i * ld + j] = mask[i * ldm + j] > 0.f ? v : 0.f;
-  }
+  // the mask of the whole tile is loaded before any store: out may alias
+  // nothing, but the compiler cannot know, and would otherwise wait out one
+  // load latency per element
+  static constexpr bool kPre = true;
+  __device__ float pre(int64_t i, int64_t j) const { return mask[i * ldm + j]; }
+  __device__ void operator()(int64_t i, int64_t j, float v, float, float m) const { out[i * ld + j] = m > 0.f ? v : 0.f; }
 };
 struct EpiPart {
   float *part;
   int64_t I, J;
   __device__ float bias_of(int64_t) const { return 0.f; }
-  __device__ void operator()(int64_t i, int64_t j, float v, float) const { part[(blockIdx.z * I + i) * J + j] = v; }
+  static constexpr bool kPre = false;
+  __device__ float pre(int64_t, int64_t) const { return 0.f; }
+  __device__ void operator()(int64_t i, int64_t j, float v, float, float) const { part[(blockIdx.z * I + i) * J + j] = v; }
 };
 
 // C[i][j] = sum_{r in split} A(i, r) B(r, j) over I x J, R.  A(i, r) = GA(r, i)
@@ -274,6 +281,16 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
     r0 += kKC;
   }
   if (i0 + kBM <= I && j0 + kBN <= J) {  // workgroup-uniform: interior tiles store unchecked
+    f16 pm[2][2];
+    if (Epi::kPre) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int v = 0; v < 16; ++v)
+            pm[a][b][v] = epi.pre(i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3), j0 + 64 * wj + 32 * b + (lane & 31));
+    }
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int64_t j = j0 + 64 * wj + 32 * b + (lane & 31);
@@ -281,7 +298,8 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) epi(i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3), j, acc[a][b][v], bj);
+        for (int v = 0; v < 16; ++v)
+          epi(i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3), j, acc[a][b][v], bj, Epi::kPre ? pm[a][b][v] : 0.f);
     }
   } else {
 #pragma unroll
@@ -293,7 +311,7 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
           const int64_t i = i0 + 64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3);
-          if (i < I && j < J) epi(i, j, acc[a][b][v], bj);
+          if (i < I && j < J) epi(i, j, acc[a][b][v], bj, Epi::kPre ? epi.pre(i, j) : 0.f);
         }
     }
   }
