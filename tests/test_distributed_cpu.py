@@ -1,5 +1,5 @@
 """IC-sharded multi-process rollout (hybridflux/rollout.py) on CPU with gloo,
-world_size 2.  The device compute is replaced by the CPU oracle here (the
+world_size 2 and 4.  The device compute is replaced by the CPU oracle here (the
 collective and sharding logic are what is under test); on GPUs the same
 driver runs with backend "nccl" (RCCL) and the HIP kernels (bench.py)."""
 import os
@@ -76,14 +76,18 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_sharded_rollout(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_sharded_rollout(tmp_path, world):
+    """world 2: shards 3 + 2; world 4 (a rehearsal of more ranks than the GPU
+    test's 2): 2 + 1 + 1 + 1."""
     port = _free_port()
-    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     want, _ = _oracle_local(list(range(1000, 1000 + N_TOTAL)))
-    for r in range(2):
+    for r in range(world):
         d = torch.load(tmp_path / f"rank{r}.pt", weights_only=True)
-        assert d["max"] == 0.5
-        assert d["local_n"] == (3 if r == 0 else 2)
+        assert d["max"] == 0.25 * world
+        lo, hi = shard_bounds(N_TOTAL, world, r)
+        assert d["local_n"] == hi - lo
         assert d["gathered"].shape == (N_TOTAL, T + 1, 4)
         assert torch.equal(d["gathered"], want)   # same ICs, same order as one process
         assert torch.equal(d["summ"], torch.arange(N_TOTAL * 8, dtype=torch.float32).reshape(N_TOTAL, 8))
