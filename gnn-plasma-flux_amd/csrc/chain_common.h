@@ -171,8 +171,11 @@ __device__ __forceinline__ float nb_sum_halo(float v, float hl, float hr) {
 }
 
 constexpr int kSmallFloats = 512 + kH * (3 + kMaxChainLayers);  // win, bin, be, w2, bl[L]
-// per wave: n,u,E,x,F,rho | 64 doubles (Poisson column) | classical twin n,u,E,F,rho
-constexpr int kWaveScratchFloats = 6 * 64 + 2 * 64 + 5 * 64;
+// per wave (floats): n,u,E,x | F | classical twin n,u,E | its F | rho, twin rho
+// (64 doubles each) | the Poisson column twice (128 doubles, poisson_cell_nx)
+constexpr int kWaveScratchFloats = 4 * 64 + 64 + 3 * 64 + 64 + 2 * 128 + 256;
+constexpr int kScrF = 4 * 64, kScrCl = 5 * 64, kScrFc = 8 * 64, kScrRho = 9 * 64, kScrRhoC = 11 * 64, kScrC2 = 13 * 64;
+static_assert(kScrC2 + 256 == kWaveScratchFloats, "per-wave scratch layout");
 
 struct Small {  // LDS copies of the small weight arrays
   const float *win, *bin, *bl, *be, *w2;
@@ -579,12 +582,12 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
   const int lane = R.lane, j = lane & 15, g = lane >> 4;
   float *scratch = lds + kRingFloats + kSmallFloats + R.wave * kWaveScratchFloats;
   float *s_st = scratch;  // n | u | E | x   (4 x 64)
-  float *s_F = scratch + 4 * 64;
-  float *s_rho = scratch + 5 * 64;
-  double *s_c = reinterpret_cast<double *>(scratch + 6 * 64);
-  float *s_cl = scratch + 8 * 64;  // classical twin n | u | E
-  float *s_Fc = scratch + 11 * 64;
-  float *s_rhoc = scratch + 12 * 64;
+  float *s_F = scratch + kScrF;
+  double *s_rho = reinterpret_cast<double *>(scratch + kScrRho);
+  double *s_c2 = reinterpret_cast<double *>(scratch + kScrC2);
+  float *s_cl = scratch + kScrCl;  // classical twin n | u | E
+  float *s_Fc = scratch + kScrFc;
+  double *s_rhoc = reinterpret_cast<double *>(scratch + kScrRhoC);
   float *park = park_of<Core>(lds, R.wave);
   const bool twin = ex.mse != nullptr;
   static_assert(Core::kNW == kWaves, "rollout: 4 waves, one IC each");
@@ -599,7 +602,7 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
   }
   if (lane < NX) {
     s_st[3 * 64 + lane] = x[lane];
-    s_c[lane] = pc[lane];
+    s_c2[lane] = s_c2[NX + lane] = pc[lane];
   }
   __syncthreads();  // small weights + per-wave state visible (no DMA in flight yet)
   float *tj = (traj && live) ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
@@ -660,24 +663,24 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
       const float F = s_F[lane];
       n_new = continuity(s_st[lane], F, s_F[im], c);
       u_new = velocity_hybrid(s_st[64 + lane], s_st[64 + im], s_st[128 + lane], c, dt);
-      s_rho[lane] = __fsub_rn(n_new, 1.0f);
+      s_rho[lane] = (double)__fsub_rn(n_new, 1.0f);
       if (ftj) ftj[(int64_t)t * NX + lane] = F;
       if (twin) {  // BaselineSolver.step (src/baseline_solver.py:80-101)
         const int ip = lane == NX - 1 ? 0 : lane + 1;
         nc = continuity(s_cl[lane], s_Fc[lane], s_Fc[im], c);
         uc = velocity_classical(s_cl[64 + lane], s_cl[64 + im], s_cl[64 + ip], s_cl[128 + lane], c, dt, ex.nu,
                                 ex.dx2);
-        s_rhoc[lane] = __fsub_rn(nc, 1.0f);
+        s_rhoc[lane] = (double)__fsub_rn(nc, 1.0f);
       }
     }
     wave_lds_sync();
     if (lane < NX) {
-      const float E_new = poisson_cell(s_rho, s_c, lane, NX);
+      const float E_new = poisson_cell_nx<NX>(s_rho, s_c2, lane);
       s_st[lane] = n_new;
       s_st[64 + lane] = u_new;
       s_st[128 + lane] = E_new;
       if (twin) {
-        const float Ec = poisson_cell(s_rhoc, s_c, lane, NX);
+        const float Ec = poisson_cell_nx<NX>(s_rhoc, s_c2, lane);
         s_cl[lane] = nc;
         s_cl[64 + lane] = uc;
         s_cl[128 + lane] = Ec;
@@ -755,9 +758,9 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
   X.rw = shadow ? wave : slot * WPI + (pos + 1) % WPI;
   float *scratch = lds + kRingFloats + kSmallFloats + slot * kWaveScratchFloats;
   float *s_st = scratch;  // n | u | E | x   (4 x 64)
-  float *s_F = scratch + 4 * 64;
-  float *s_rho = scratch + 5 * 64;
-  double *s_c = reinterpret_cast<double *>(scratch + 6 * 64);
+  float *s_F = scratch + kScrF;
+  double *s_rho = reinterpret_cast<double *>(scratch + kScrRho);
+  double *s_c2 = reinterpret_cast<double *>(scratch + kScrC2);
   const int b_raw = blockIdx.x * IPW + slot;
   const bool live = b_raw < B;
   const int64_t b = live ? b_raw : B - 1;  // a missing IC mirrors the last one and writes nothing
@@ -766,7 +769,7 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
     for (int i = lane; i < 3 * NX; i += 64) s_st[(i / NX) * 64 + i % NX] = st0[i];
     if (lane < NX) {
       s_st[3 * 64 + lane] = x[lane];
-      s_c[lane] = pc[lane];
+      s_c2[lane] = s_c2[NX + lane] = pc[lane];
     }
   }
   __syncthreads();  // small weights + IC state visible (no DMA in flight yet)
@@ -840,12 +843,12 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
         const float Fv = s_F[lane];
         n_new = continuity(s_st[lane], Fv, s_F[im], c);
         u_new = velocity_hybrid(s_st[64 + lane], s_st[64 + im], s_st[128 + lane], c, dt);
-        s_rho[lane] = __fsub_rn(n_new, 1.0f);
+        s_rho[lane] = (double)__fsub_rn(n_new, 1.0f);
         if (ftj) ftj[(int64_t)t * NX + lane] = Fv;
       }
       wave_lds_sync();
       if (lane < NX) {
-        const float E_new = poisson_cell(s_rho, s_c, lane, NX);
+        const float E_new = poisson_cell_nx<NX>(s_rho, s_c2, lane);
         s_st[lane] = n_new;
         s_st[64 + lane] = u_new;
         s_st[128 + lane] = E_new;

@@ -68,6 +68,29 @@ __device__ __forceinline__ float poisson_cell(const float *s_rho, const double *
   return (float)(a0 + a1);
 }
 
+// poisson_cell for a compile-time even NX (the fused rollouts), term for term
+// and chain for chain the same sums: rho is held as double (the same value as
+// the (double) conversion above) and the column twice, s_c2[m] = c[m mod NX]
+// for m < 2 NX, so term j reads s_c2[i + NX - j] at a constant offset from one
+// per-lane base and every LDS read is an immediate-offset ds_read with no index
+// arithmetic; unrolled, the reads run ahead of the two fp64 FMA chains instead
+// of one wrap-around index update and two dependent reads per term.
+template <int NX>
+__device__ __forceinline__ float poisson_cell_nx(const double *s_rho, const double *s_c2, int i) {
+  static_assert(NX % 2 == 0, "even chain length");
+#ifdef HF_DIAG_NOPOISSON  // timing diagnostic only: results are wrong
+  return (float)(s_rho[i] * s_c2[i]);
+#endif
+  const double *cb = s_c2 + i + 1;  // term j at cb[NX - 1 - j]
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NX; j += 2) {
+    a0 = fma(cb[NX - 1 - j], s_rho[j], a0);
+    a1 = fma(cb[NX - 2 - j], s_rho[j + 1], a1);
+  }
+  return (float)(a0 + a1);
+}
+
 // ---------------------------------------------------------------- FFT Poisson
 // For power-of-two nx in [kFftMinNx, kFftMaxNx] the spectral operator is
 // applied as the reference writes it (src/baseline_solver.py:59-68),
