@@ -13,6 +13,7 @@
 // FLOPs of an edge-wise GEMM and no [E][H] message tensor in HBM.
 #include "hf_device.h"
 #include "hf_internal.h"
+#include "tgemm.h"
 
 namespace hf {
 namespace {
@@ -123,6 +124,15 @@ PureWs carve_pure(void *ws, int H, int64_t N) {
   return w;
 }
 
+// The chain form of PureGNN's layers (tgemm.h): on chains whose length
+// divides the 128-cell row tile and hidden widths in multiples of 64, a message
+// layer is ONE f32 MFMA GEMM h [N][H] x [W_a ; W_b]^T whose block epilogue
+// forms the messages and the residual (EpiMsg), and output_mlp.0 is a GEMM
+// with a tanh epilogue.  Otherwise: the generic linear + gather kernels.
+bool pure_chain_ok(int H, int chain_nx, int64_t N) {
+  return chain_nx > 0 && 128 % chain_nx == 0 && H % 64 == 0 && H <= 1024 && N * H < (int64_t(1) << 31);
+}
+
 // PureGNN.forward (train_pure_gnn.py:57-76) over buckets already built.
 hipError_t pure_forward(const PureW &w, const float *nf, int64_t N, const int64_t *src, const int *off,
                         const int *perm, int chain_nx, PureWs &b, float *delta, hipStream_t s) {
@@ -132,6 +142,25 @@ hipError_t pure_forward(const PureW &w, const float *nf, int64_t N, const int64_
                        N, H, kActTanh, nullptr, s)))
     return e;
   float *h = b.h0, *hn = b.h1;
+  if (pure_chain_ok(H, chain_nx, N)) {
+    using namespace tg;
+    for (int l = 0; l < w.L; ++l) {
+      const float *W = w.w_l + l * w.ls;
+      if ((e = tgemm<VPlain, false, VPQ, false, EpiMsg>(VPlain{h, H, N, kNoSplit, 0, H}, VPQ{W, H},
+                                                         EpiMsg{h, hn, w.b_l + l * w.ls, H, chain_nx}, N, 2LL * H, H, 1,
+                                                         s)))
+        return e;
+      float *t = h;
+      h = hn;
+      hn = t;
+    }
+    if ((e = tgemm<VPlain, false, VPlain, false, EpiTanh>(VPlain{h, H, N, kNoSplit, 0, H},
+                                                           VPlain{w.w_o1, H, H, kNoSplit, 0, H},
+                                                           EpiTanh{hn, H, w.b_o1}, N, H, H, 1, s)))
+      return e;
+    return gemm_linear(hn, H, nullptr, nullptr, 0, nullptr, wv_rows(w.w_o2, H, H), w.b_o2, delta, N, 3, kActNone,
+                       nullptr, s);
+  }
   const unsigned nb = (unsigned)((N * H + 255) / 256);
   for (int l = 0; l < w.L; ++l) {
     const float *W = w.w_l + l * w.ls;

@@ -4,7 +4,10 @@ For every method the reference times — classical solver, hybrid FluxGNN
 solver, PureGNN, PINN — report
   * `single_ic_s`: one 50-step rollout of the seed-42 IC, the reference's own
     methodology (N_RUNS=10 timed runs after a warmup, mean seconds per run);
-  * `batched`: IC-steps/s for a 4096-IC batch, 50 steps, trajectory recorded.
+  * `batched`: IC-steps/s for a 4096-IC batch, 50 steps, trajectory recorded,
+    with the model's algorithmic FLOPs per IC-step (`flop_per_ic_step`, the
+    matrix products of its forward) and the fraction of the fp32 MFMA peak
+    (157.3 TFLOP/s) the batched rate reaches.
 Weights are random-init of each architecture (no checkpoints ship with the
 reference).  CPU column: the oracle restatements, one IC, 50 steps (bounded).
 
@@ -34,6 +37,23 @@ def timed(fn, runs):
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     return float(np.mean(ts))
+
+
+PEAK_F32 = 157.3e12  # dense fp32 MFMA, MI355X_MICROARCH.md
+
+
+def flop_per_ic_step(name, nx=64, H=128, L=4, pinn_h=256, pinn_l=4):
+    """Matrix-product FLOPs of one model step of one IC (2 per MAC; activations,
+    FV, Poisson and the edge sums not counted)."""
+    if name == "hybrid":  # FluxGNN(4,128,4): input, L update layers [h; agg] -> H, P/Q readout,
+        # w2 . ReLU(z) of both edges (bench.py's 329,216 per cell)
+        return nx * (2 * (4 * H + L * 2 * H * H + 2 * H * H) + 4 * H)
+    if name == "pure_gnn":  # input, L layers of P = W_a h, Q = W_b h, output H -> H -> 3
+        return nx * 2 * (4 * H + L * 2 * H * H + H * H + 3 * H)
+    if name == "pinn":  # 3nx -> h, (L-2) x h -> h, h -> 3nx
+        D = 3 * nx
+        return 2 * (D * pinn_h + (pinn_l - 2) * pinn_h * pinn_h + pinn_h * D)
+    return 0
 
 
 def main():
@@ -67,6 +87,11 @@ def main():
         batched = timed(lambda: fn(ics), 3)
         res[name] = {"single_ic_s": round(single, 6), "single_ic_steps_per_s": round(T / single, 1),
                      "batched_ic_steps_per_s": round(B * T / batched, 1), "batched_ms_per_step": round(batched / T * 1e3, 4)}
+        fl = flop_per_ic_step(name)
+        if fl:
+            tf = fl * B * T / batched
+            res[name].update(flop_per_ic_step=fl, batched_tflops=round(tf / 1e12, 2),
+                             frac_of_f32_peak=round(tf / PEAK_F32, 4))
         print(name, res[name], file=sys.stderr, flush=True)
     cpu = None
     if not args.no_cpu:
