@@ -19,6 +19,7 @@ namespace hf {
 namespace {
 
 inline size_t a256(size_t v) { return (v + 255) & ~size_t(255); }
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float message(const float *P, int64_t s, int H, int f, float q, float b) {
   return tanhf(__fadd_rn(__fadd_rn(P[s * H + f], q), b));
@@ -202,6 +203,126 @@ PinnW pinn_view(const float *p, int D, int H, int L) {
   return w;
 }
 
+// ---------------------------------------------------------------------------
+// PINN rollout in one launch (train_pinn.py:48-61 iterated as
+// evaluate_multi_ic.py:75-81): a workgroup owns 16 ICs for all T steps, with
+// their state and the hidden activations in LDS, and runs every layer as
+// v_mfma_f32_16x16x4_f32 tiles (16 output features x 16 ICs) whose weight
+// operand comes straight from nn.Linear's [out][in] rows in global memory
+// (L2-resident: 0.9 MB), four k-blocks in flight.  The k order inside a
+// 16-block is permuted so that a lane's four MFMA steps read one float4 of its
+// weight row (k = 16 kb + 4 (lane >> 4) + step); the activations use the same
+// order, so LDS holds them as [k-block][lane][4]: an MFMA output tile is
+// written back with one ds_write_b128 per lane and read as the next layer's B
+// operand with one ds_read_b128.  No activation and no intermediate state
+// reaches HBM; the ICs never exchange anything, so no step needs a grid sync.
+constexpr int kPinnIcs = 16;
+
+template <int K, int NT, int ACT>  // ACT: 0 tanh, 1 residual (state + v, the last layer)
+__device__ __forceinline__ void pinn_layer(const float *__restrict__ W, const float *__restrict__ bias,
+                                           const float *in, float *out, int wave, int lane) {
+  constexpr int KB = K / 16, P = 4;
+  const int m = lane & 15, g = lane >> 4;
+  f4v acc[NT];
+  const float *wrow[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+    wrow[j] = W + (int64_t)(16 * (wave + 4 * j) + m) * K + 4 * g;
+  }
+  f4v wq[P][NT];  // k-blocks c .. c + P - 1 in flight while c is multiplied
+#pragma unroll
+  for (int kb = 0; kb < KB + P - 1; ++kb) {
+    if (kb < KB) {  // slot kb % P held k-block kb - P, consumed last iteration
+#pragma unroll
+      for (int j = 0; j < NT; ++j) wq[kb % P][j] = *reinterpret_cast<const f4v *>(wrow[j] + 16 * kb);
+    }
+    if (kb >= P - 1) {
+      const int c = kb - (P - 1);
+      const f4v bv = *reinterpret_cast<const f4v *>(in + c * 256 + lane * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int t = wave + 4 * j;
+    float *o = out + t * 256 + lane * 4;
+    f4v v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(acc[j][i], bias[16 * t + 4 * g + i]);
+    if (ACT == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+    } else {
+      const f4v st = *reinterpret_cast<const f4v *>(o);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(st[i], v[i]);
+    }
+    *reinterpret_cast<f4v *>(o) = v;
+  }
+}
+
+// LDS index of feature k of IC n in the [k-block][lane][4] order above
+__device__ __forceinline__ int pinn_at(int k, int n) { return (k >> 4) * 256 + (((k >> 2) & 3) * 16 + n) * 4 + (k & 3); }
+
+template <int D, int H>
+__global__ __launch_bounds__(256, 1) void pinn_run_kernel(PinnW w, const float *__restrict__ state0,
+                                                          float *__restrict__ final_state, float *__restrict__ traj,
+                                                          int64_t B, int T) {
+  static_assert(D % 64 == 0 && H % 64 == 0, "16-feature tiles, 4 waves");
+  __shared__ f4v s_state4[D * kPinnIcs / 4];
+  __shared__ f4v s_act4[2][H * kPinnIcs / 4];
+  float *s_state = reinterpret_cast<float *>(s_state4);
+  float *const act0 = reinterpret_cast<float *>(s_act4[0]), *const act1 = reinterpret_cast<float *>(s_act4[1]);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t b0 = (int64_t)blockIdx.x * kPinnIcs;
+  const int64_t ldt = (int64_t)(T + 1) * D;
+  for (int idx = tid; idx < kPinnIcs * D; idx += 256) {
+    const int n = idx / D, d = idx - n * D;
+    const int64_t b = b0 + n < B ? b0 + n : B - 1;  // missing ICs mirror the last one and write nothing
+    const float v = state0[b * D + d];
+    s_state[pinn_at(d, n)] = v;
+    if (traj && b0 + n < B) traj[b * ldt + d] = v;
+  }
+  __syncthreads();
+  const int L = w.L;
+  for (int t = 0; t < T; ++t) {
+    pinn_layer<D, H / 64, 0>(w.w[0], w.b[0], s_state, act0, wave, lane);
+    __syncthreads();
+    for (int l = 1; l < L - 1; ++l) {
+      pinn_layer<H, H / 64, 0>(w.w[l], w.b[l], (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane);
+      __syncthreads();
+    }
+    pinn_layer<H, D / 64, 1>(w.w[L - 1], w.b[L - 1], (L & 1) ? act1 : act0, s_state, wave, lane);
+    __syncthreads();
+    if (traj) {
+      for (int idx = tid; idx < kPinnIcs * D; idx += 256) {
+        const int n = idx / D, d = idx - n * D;
+        if (b0 + n < B) traj[(b0 + n) * ldt + (int64_t)(t + 1) * D + d] = s_state[pinn_at(d, n)];
+      }
+    }
+  }
+  for (int idx = tid; idx < kPinnIcs * D; idx += 256) {
+    const int n = idx / D, d = idx - n * D;
+    if (b0 + n < B) final_state[(b0 + n) * D + d] = s_state[pinn_at(d, n)];
+  }
+}
+
+// the one-launch rollout's shapes: the reference's PINN(3 * 64, 256, L)
+bool pinn_fused_ok(int D, int H, int L) { return D == 192 && H == 256 && L >= 2 && L <= kMaxChainLayers; }
+
+hipError_t pinn_fused(const PinnW &w, const float *state0, float *final_state, int64_t B, int T, float *traj,
+                      hipStream_t s) {
+  const int64_t blocks = (B + kPinnIcs - 1) / kPinnIcs;
+  if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((pinn_run_kernel<192, 256>), dim3((unsigned)blocks), dim3(256), 0, s, w, state0, final_state,
+                     traj, B, T);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 int64_t pure_gnn_ws_bytes(int H, int64_t N, int64_t E) {
@@ -254,6 +375,7 @@ int64_t pinn_ws_bytes(int D, int H, int64_t B) {
 hipError_t launch_pinn_forward(const float *params, int D, int H, int L, const float *state, float *out, int64_t B,
                                void *ws, hipStream_t s) {
   const PinnW w = pinn_view(params, D, H, L);
+  if (pinn_fused_ok(D, H, L)) return B > 0 ? pinn_fused(w, state, out, B, 1, nullptr, s) : hipSuccess;
   float *buf[2] = {static_cast<float *>(ws),
                    reinterpret_cast<float *>(static_cast<char *>(ws) + a256(sizeof(float) * B * H))};
   const float *in = state;
@@ -277,6 +399,8 @@ hipError_t launch_pinn_run(const float *params, int D, int H, int L, const float
   float *st[2] = {reinterpret_cast<float *>(p), reinterpret_cast<float *>(p + a256(sizeof(float) * B * D))};
   const size_t row = sizeof(float) * D, ldt = row * (T + 1);
   hipError_t e;
+  // one launch (the kernel writes trajectory row 0 itself)
+  if (T > 0 && pinn_fused_ok(D, H, L)) return pinn_fused(pinn_view(params, D, H, L), state0, final_state, B, T, traj, s);
   if (traj && (e = hipMemcpy2DAsync(traj, ldt, state0, row, row, B, hipMemcpyDeviceToDevice, s))) return e;
   if (T == 0) return hipMemcpyAsync(final_state, state0, row * B, hipMemcpyDeviceToDevice, s);
   const float *cur = state0;

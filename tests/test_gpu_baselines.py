@@ -96,6 +96,32 @@ def test_pinn_forward_and_rollout_vs_reference(models):
     assert torch.equal(r0["final"], torch.as_tensor(b["ics"], device=DEV))
 
 
+@pytest.mark.parametrize("nx,H,L,B", [(64, 256, 2, 5), (64, 256, 3, 33), (64, 256, 5, 16), (32, 128, 3, 7)])
+def test_pinn_shapes_vs_oracle(nx, H, L, B):
+    """PINN(3 nx, H, L) rollouts vs the oracle restatement (train_pinn.py:48-61):
+    the reference's shape (3*64, 256) runs the one-launch kernel (16 ICs per
+    workgroup; B = 5, 33 leave a partial workgroup), other shapes the per-layer
+    GEMMs.  T = 0 returns the initial state; forward() is one rollout step."""
+    import hybridflux as hf
+    torch.manual_seed(nx + H + L)
+    pn = hf.PINN(3 * nx, H, L).to(DEV)
+    grid = O.Grid(nx)
+    ics = np.stack([O.initial_condition(grid, s) for s in range(5000, 5000 + B)])
+    r = pn.rollout(torch.as_tensor(ics, device=DEV), 6)
+    pnp = O.params_from({k: v.detach().cpu() for k, v in pn.state_dict().items()})
+    want = [torch.from_numpy(ics)]
+    with torch.no_grad():
+        for _ in range(6):
+            want.append(O.pinn_forward(pnp, want[-1]))
+    want = torch.stack(want, 1).numpy()
+    close(r["traj"], want, 1e-5, 1e-5, what="traj")
+    assert torch.equal(r["final"], r["traj"][:, -1])
+    with torch.no_grad():
+        f = pn(torch.as_tensor(ics, device=DEV))
+    close(f, want[:, 1], 2e-6, 1e-5, what="forward")
+    assert torch.equal(pn.rollout(torch.as_tensor(ics, device=DEV), 0)["final"], torch.as_tensor(ics, device=DEV))
+
+
 def test_rollouts_vs_oracle_many_ics(models):
     """64 ICs (seeds 3000..), 20 steps, against the oracle restatements."""
     hf, pg, pn, b = models
