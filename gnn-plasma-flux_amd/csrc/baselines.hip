@@ -218,9 +218,19 @@ PinnW pinn_view(const float *p, int D, int H, int L) {
 // reaches HBM; the ICs never exchange anything, so no step needs a grid sync.
 constexpr int kPinnIcs = 16;
 
-template <int K, int NT, int ACT>  // ACT: 0 tanh, 1 residual (state + v, the last layer)
+#ifndef HF_PINN_WAVES
+#define HF_PINN_WAVES 16
+#endif
+// waves per workgroup: 16 (four per SIMD, one output tile each) measured 7 %
+// faster than 4 and 3 % faster than 8 (profiles/r03_pinn_ab.txt)
+constexpr int kPinnWaves = HF_PINN_WAVES;
+
+// One layer on this wave's output tiles t = wave + kPinnWaves * j (j < NT) of
+// NTILES: out = act(W in + b) (ACT 0: tanh; 1: the last layer, state += W in + b).
+template <int K, int NTILES, int ACT>
 __device__ __forceinline__ void pinn_layer(const float *__restrict__ W, const float *__restrict__ bias,
                                            const float *in, float *out, int wave, int lane) {
+  constexpr int NT = (NTILES + kPinnWaves - 1) / kPinnWaves;
   constexpr int KB = K / 16, P = 4;
   const int m = lane & 15, g = lane >> 4;
   f4v acc[NT];
@@ -228,7 +238,8 @@ __device__ __forceinline__ void pinn_layer(const float *__restrict__ W, const fl
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
-    wrow[j] = W + (int64_t)(16 * (wave + 4 * j) + m) * K + 4 * g;
+    const int t = wave + kPinnWaves * j < NTILES ? wave + kPinnWaves * j : NTILES - 1;  // a spare tile: not stored
+    wrow[j] = W + (int64_t)(16 * t + m) * K + 4 * g;
   }
   f4v wq[P][NT];  // k-blocks c .. c + P - 1 in flight while c is multiplied
 #pragma unroll
@@ -248,7 +259,8 @@ __device__ __forceinline__ void pinn_layer(const float *__restrict__ W, const fl
   }
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    const int t = wave + 4 * j;
+    const int t = wave + kPinnWaves * j;
+    if (NTILES % kPinnWaves != 0 && t >= NTILES) break;
     float *o = out + t * 256 + lane * 4;
     f4v v;
 #pragma unroll
@@ -269,18 +281,20 @@ __device__ __forceinline__ void pinn_layer(const float *__restrict__ W, const fl
 __device__ __forceinline__ int pinn_at(int k, int n) { return (k >> 4) * 256 + (((k >> 2) & 3) * 16 + n) * 4 + (k & 3); }
 
 template <int D, int H>
-__global__ __launch_bounds__(256, 1) void pinn_run_kernel(PinnW w, const float *__restrict__ state0,
+__global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, const float *__restrict__ state0,
                                                           float *__restrict__ final_state, float *__restrict__ traj,
                                                           int64_t B, int T) {
-  static_assert(D % 64 == 0 && H % 64 == 0, "16-feature tiles, 4 waves");
+  static_assert(D % 16 == 0 && H % 16 == 0, "16-feature tiles");
+  constexpr int NTH = 64 * kPinnWaves;
   __shared__ f4v s_state4[D * kPinnIcs / 4];
   __shared__ f4v s_act4[2][H * kPinnIcs / 4];
   float *s_state = reinterpret_cast<float *>(s_state4);
   float *const act0 = reinterpret_cast<float *>(s_act4[0]), *const act1 = reinterpret_cast<float *>(s_act4[1]);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t b0 = (int64_t)blockIdx.x * kPinnIcs;
+  static_assert(NTH == 256 || NTH == 512 || NTH == 1024, "4, 8 or 16 waves");
   const int64_t ldt = (int64_t)(T + 1) * D;
-  for (int idx = tid; idx < kPinnIcs * D; idx += 256) {
+  for (int idx = tid; idx < kPinnIcs * D; idx += NTH) {
     const int n = idx / D, d = idx - n * D;
     const int64_t b = b0 + n < B ? b0 + n : B - 1;  // missing ICs mirror the last one and write nothing
     const float v = state0[b * D + d];
@@ -290,22 +304,22 @@ __global__ __launch_bounds__(256, 1) void pinn_run_kernel(PinnW w, const float *
   __syncthreads();
   const int L = w.L;
   for (int t = 0; t < T; ++t) {
-    pinn_layer<D, H / 64, 0>(w.w[0], w.b[0], s_state, act0, wave, lane);
+    pinn_layer<D, H / 16, 0>(w.w[0], w.b[0], s_state, act0, wave, lane);
     __syncthreads();
     for (int l = 1; l < L - 1; ++l) {
-      pinn_layer<H, H / 64, 0>(w.w[l], w.b[l], (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane);
+      pinn_layer<H, H / 16, 0>(w.w[l], w.b[l], (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane);
       __syncthreads();
     }
-    pinn_layer<H, D / 64, 1>(w.w[L - 1], w.b[L - 1], (L & 1) ? act1 : act0, s_state, wave, lane);
+    pinn_layer<H, D / 16, 1>(w.w[L - 1], w.b[L - 1], (L & 1) ? act1 : act0, s_state, wave, lane);
     __syncthreads();
     if (traj) {
-      for (int idx = tid; idx < kPinnIcs * D; idx += 256) {
+      for (int idx = tid; idx < kPinnIcs * D; idx += NTH) {
         const int n = idx / D, d = idx - n * D;
         if (b0 + n < B) traj[(b0 + n) * ldt + (int64_t)(t + 1) * D + d] = s_state[pinn_at(d, n)];
       }
     }
   }
-  for (int idx = tid; idx < kPinnIcs * D; idx += 256) {
+  for (int idx = tid; idx < kPinnIcs * D; idx += NTH) {
     const int n = idx / D, d = idx - n * D;
     if (b0 + n < B) final_state[(b0 + n) * D + d] = s_state[pinn_at(d, n)];
   }
@@ -318,7 +332,7 @@ hipError_t pinn_fused(const PinnW &w, const float *state0, float *final_state, i
                       hipStream_t s) {
   const int64_t blocks = (B + kPinnIcs - 1) / kPinnIcs;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((pinn_run_kernel<192, 256>), dim3((unsigned)blocks), dim3(256), 0, s, w, state0, final_state,
+  hipLaunchKernelGGL((pinn_run_kernel<192, 256>), dim3((unsigned)blocks), dim3(64 * kPinnWaves), 0, s, w, state0, final_state,
                      traj, B, T);
   return hipGetLastError();
 }
