@@ -373,7 +373,10 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const float *__restrict
   }
 }
 
-constexpr int kWgradSplits = 256;
+#ifndef HF_WGRAD_SPLITS
+#define HF_WGRAD_SPLITS 256
+#endif
+constexpr int kWgradSplits = HF_WGRAD_SPLITS;
 constexpr int kInputSplits = 1024;
 
 inline size_t al256(size_t v) { return (v + 255) & ~size_t(255); }
