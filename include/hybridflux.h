@@ -192,12 +192,18 @@ int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const
  * hf_pure_gnn_run = the rollout of scripts/evaluation/evaluate_multi_ic.py:45-66
  * (state <- state + delta, node features [n,u,E,x]) for B ICs on chains of nx
  * cells: state0/final [B][3][nx], traj [B][T+1][3][nx] or NULL; x [nx].
- * Workspace: hf_pure_gnn_workspace_bytes(H, N = B*nx, E = 2N).
+ * Workspace: hf_pure_gnn_workspace_bytes(H, N = B*nx, E = 2N).  On chains
+ * whose nx divides 128 with H a multiple of 64, each message layer is one f32
+ * MFMA GEMM that forms the messages and the residual in its epilogue
+ * (csrc/tgemm.h EpiMsg); other shapes run the generic linear + gather kernels.
  *
  * PINN (scripts/training/train_pinn.py:36-61): net.0 [H][D], (layers-2) x
  * [H][H], net.last [D][H] (+biases), tanh between; out = state + net(state)
  * on states flattened to D = 3*nx.  hf_pinn_run = evaluate_multi_ic.py:70-83
- * for B ICs: state0/final [B][D], traj [B][T+1][D] or NULL.
+ * for B ICs: state0/final [B][D], traj [B][T+1][D] or NULL.  The reference's
+ * shape (D = 192, H = 256, 2 <= layers <= 8) runs as ONE launch for all T steps
+ * (16 ICs per workgroup, activations in LDS; hf_pinn_forward is its T = 1) and
+ * leaves the workspace unused; other shapes run per-layer GEMMs through it.
  */
 int64_t hf_pure_gnn_param_count(int in_dim, int hidden, int layers);
 int64_t hf_pure_gnn_workspace_bytes(int hidden, int64_t N, int64_t E);
