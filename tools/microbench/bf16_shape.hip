@@ -1,0 +1,345 @@
+// Microbenchmark for VERDICT r02 item 2: the cfg4 bf16 update-layer loop in
+// the two MFMA shapes, with the ring removed (weights static in LDS), so only
+// the shape-dependent parts are compared: MFMAs, their LDS fragment reads, the
+// epilogue VALU (neighbour sum with DPP shifts, add, ReLU, bf16 pack) and the
+// park writes / reloads of the new activations.  Random data (the clock
+// depends on it: MI355X_MICROARCH.md DVFS item 1).  Results are not checked;
+// the kernels compute nothing meaningful.
+//
+//   A: v_mfma_f32_16x16x32_bf16, 64 cells per wave as 4 m-tiles (the kept
+//      CoreBF16 layout: cell 4j + mt; 3 of 4 neighbour sums are plain adds,
+//      one per side a DPP row shift), output pairs of 2 x 16 features.
+//   B: v_mfma_f32_32x32x16_bf16, 64 cells per wave as 2 n-tiles of 32
+//      (cell 2j + mt): every neighbour sum is a DPP wave shift plus a fix-up
+//      at the window edge (lanes 0/32 or 31/63), output tiles of 32 features.
+// Both: 8 waves per workgroup (two per SIMD), 128 x 256 bf16 weights per
+// layer (W_a | W_b/2), K = 128, same FLOPs per layer per wave.
+//
+// Build + run (GPU):  hipcc -O3 --offload-arch=gfx950 -o build/mb_bf16_shape tools/microbench/bf16_shape.hip
+//                     ./build/mb_bf16_shape [iters]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+constexpr int kNW = 8;
+
+__device__ __forceinline__ unsigned pk_relu(float a, float b) {
+  a = a > 0.f ? a : 0.f;
+  b = b > 0.f ? b : 0.f;
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f2{a, b}, b2));
+}
+__device__ __forceinline__ f4 mma16(const u4 &a, const u4 &b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f16v mma32(const u4 &a, const u4 &b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
+}
+template <int NM, int NV, int ND>
+__device__ __forceinline__ void interleave() {
+  __builtin_amdgcn_sched_group_barrier(0x100, ND, 0);
+#pragma unroll
+  for (int i = 0; i < NM; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// ------------------------------------------------------------------ A: 16x16x32
+struct PairA {
+  f4 a[4][2], g[4][2];
+};
+// dword K of the next fragment from output pair P (tile K>>1, rows 2(K&1), +1)
+template <int K>
+__device__ __forceinline__ void pieceA(const PairA &P, u4 (&nh)[4]) {
+  constexpr int t = K >> 1, r0 = 2 * (K & 1);
+  float z[2][4];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int r = r0 + rr;
+    float s0 = P.g[1][t][r], s3 = P.g[2][t][r];
+    asm("v_add_f32_dpp %0, %1, %2 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(s0) : "v"(P.g[3][t][r]), "v"(P.g[1][t][r]));
+    asm("v_add_f32_dpp %0, %1, %2 row_shl:1 row_mask:0xf bank_mask:0xf" : "+v"(s3) : "v"(P.g[0][t][r]), "v"(P.g[2][t][r]));
+    z[rr][0] = __fadd_rn(P.a[0][t][r], s0);
+    z[rr][1] = __fadd_rn(P.a[1][t][r], __fadd_rn(P.g[0][t][r], P.g[2][t][r]));
+    z[rr][2] = __fadd_rn(P.a[2][t][r], __fadd_rn(P.g[1][t][r], P.g[3][t][r]));
+    z[rr][3] = __fadd_rn(P.a[3][t][r], s3);
+  }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) nh[mt][K] = pk_relu(z[0][mt], z[1][mt]);
+}
+template <int KB>
+__device__ __forceinline__ void unitA(const u4 *wl, int q, int lane, const u4 (&X)[4][4], PairA &P) {
+  u4 w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = wl[((q * 4 + KB) * 4 + i) * 64 + lane];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      P.a[mt][t] = mma16(w[2 * t], X[mt][KB], P.a[mt][t]);
+      P.g[mt][t] = mma16(w[2 * t + 1], X[mt][KB], P.g[mt][t]);
+    }
+}
+__device__ __forceinline__ void initA(PairA &P, float b) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      P.a[mt][t] = f4{b, b, b, b};
+      P.g[mt][t] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+__global__ __launch_bounds__(64 * kNW, 1) void layer_a(const u4 *__restrict__ wsrc, const u4 *__restrict__ xsrc,
+                                                        float *__restrict__ out, int iters) {
+  __shared__ u4 wl[4096];         // one layer: 4 pairs x 4 k-blocks x 4 fragments x 64 lanes
+  __shared__ u4 park[kNW][4][64];  // one pair's new fragments per wave (rewritten each pair)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) wl[i] = wsrc[i];
+  u4 X[4][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) X[mt][kb] = xsrc[((blockIdx.x * kNW + wave) * 16 + mt * 4 + kb) * 64 + lane];
+  __syncthreads();
+  const float bias = 0.01f * lane;
+  for (int it = 0; it < iters; ++it) {
+    PairA acc, prev;
+    u4 nh[4];
+    initA(acc, bias);
+    unitA<0>(wl, 0, lane, X, acc);
+    interleave<16, 0, 4>();
+    unitA<1>(wl, 0, lane, X, acc);
+    interleave<16, 0, 4>();
+    unitA<2>(wl, 0, lane, X, acc);
+    interleave<16, 0, 4>();
+    unitA<3>(wl, 0, lane, X, acc);
+    interleave<16, 0, 4>();
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      prev = acc;
+      initA(acc, bias);
+      unitA<0>(wl, q, lane, X, acc);
+      pieceA<0>(prev, nh);
+      interleave<16, 2, 4>();
+      unitA<1>(wl, q, lane, X, acc);
+      pieceA<1>(prev, nh);
+      interleave<16, 2, 4>();
+      unitA<2>(wl, q, lane, X, acc);
+      pieceA<2>(prev, nh);
+      interleave<16, 2, 4>();
+      unitA<3>(wl, q, lane, X, acc);
+      pieceA<3>(prev, nh);
+      interleave<16, 2, 4>();
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) park[wave][mt][lane] = nh[mt];
+    }
+    pieceA<0>(acc, nh);
+    pieceA<1>(acc, nh);
+    pieceA<2>(acc, nh);
+    pieceA<3>(acc, nh);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) park[wave][mt][lane] = nh[mt];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's park writes landed
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) X[mt][kb] = park[wave][(mt + kb) & 3][lane];
+  }
+  unsigned s = 0;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) s ^= X[mt][kb][0] ^ X[mt][kb][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+}
+
+// ------------------------------------------------------------------ B: 32x32x16
+struct TileB {
+  f16v a[2], g[2];
+};
+// values 2S, 2S+1 of both n-tiles: z = A + (G(i-1) + G(i+1)) on cells 2j + n;
+// the shifted neighbour is one DPP wave shift, the window edge a select
+template <int S>
+__device__ __forceinline__ void pieceB(const TileB &P, unsigned (&nd)[16], int lane, float seam) {
+  float z[2][2];
+#pragma unroll
+  for (int vv = 0; vv < 2; ++vv) {
+    const int v = 2 * S + vv;
+    // n = 0 (cell 2j): left = cell 2j - 1 = (n = 1, j - 1), right = (n = 1, j)
+    float s0 = P.g[1][v];
+    asm("v_add_f32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(s0) : "v"(P.g[1][v]), "v"(P.g[1][v]));
+    s0 = (lane & 31) == 0 ? __fadd_rn(seam, P.g[1][v]) : s0;
+    // n = 1 (cell 2j + 1): left = (n = 0, j), right = cell 2j + 2 = (n = 0, j + 1)
+    float s1 = P.g[0][v];
+    asm("v_add_f32_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf" : "+v"(s1) : "v"(P.g[0][v]), "v"(P.g[0][v]));
+    s1 = (lane & 31) == 31 ? __fadd_rn(seam, P.g[0][v]) : s1;
+    z[0][vv] = __fadd_rn(P.a[0][v], s0);
+    z[1][vv] = __fadd_rn(P.a[1][v], s1);
+  }
+  nd[S] = pk_relu(z[0][0], z[0][1]);
+  nd[8 + S] = pk_relu(z[1][0], z[1][1]);
+}
+template <int S>
+__device__ __forceinline__ void stepB(const u4 *wl, int q, int lane, const u4 (&X)[2][8], TileB &P) {
+  const u4 wa = wl[((q * 8 + S) * 2) * 64 + lane], wb = wl[((q * 8 + S) * 2 + 1) * 64 + lane];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    P.a[n] = mma32(wa, X[n][S], P.a[n]);
+    P.g[n] = mma32(wb, X[n][S], P.g[n]);
+  }
+}
+__device__ __forceinline__ void initB(TileB &P, float b) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      P.a[n][v] = b;
+      P.g[n][v] = 0.f;
+    }
+}
+template <int S>
+__device__ __forceinline__ void stepB_prev(const u4 *wl, int q, int lane, const u4 (&X)[2][8], TileB &acc,
+                                           const TileB &prev, unsigned (&nd)[16], float seam) {
+  stepB<S>(wl, q, lane, X, acc);
+  pieceB<S>(prev, nd, lane, seam);
+  interleave<4, 5, 2>();
+}
+
+__global__ __launch_bounds__(64 * kNW, 1) void layer_b(const u4 *__restrict__ wsrc, const u4 *__restrict__ xsrc,
+                                                        float *__restrict__ out, int iters) {
+  __shared__ u4 wl[4096];         // one layer: 4 tiles x 8 k-steps x 2 fragments x 64 lanes
+  __shared__ u4 park[kNW][4][64];  // one tile's new fragments per wave
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 4096; i += blockDim.x) wl[i] = wsrc[i];
+  u4 X[2][8];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int s = 0; s < 8; ++s) X[n][s] = xsrc[((blockIdx.x * kNW + wave) * 16 + n * 8 + s) * 64 + lane];
+  __syncthreads();
+  const float bias = 0.01f * lane, seam = 0.001f * lane;
+  for (int it = 0; it < iters; ++it) {
+    TileB acc, prev;
+    unsigned nd[16];
+    initB(acc, bias);
+    stepB<0>(wl, 0, lane, X, acc);
+    interleave<4, 0, 2>();
+    stepB<1>(wl, 0, lane, X, acc);
+    interleave<4, 0, 2>();
+    stepB<2>(wl, 0, lane, X, acc);
+    interleave<4, 0, 2>();
+    stepB<3>(wl, 0, lane, X, acc);
+    interleave<4, 0, 2>();
+    stepB<4>(wl, 0, lane, X, acc);
+    interleave<4, 0, 2>();
+    stepB<5>(wl, 0, lane, X, acc);
+    interleave<4, 0, 2>();
+    stepB<6>(wl, 0, lane, X, acc);
+    interleave<4, 0, 2>();
+    stepB<7>(wl, 0, lane, X, acc);
+    interleave<4, 0, 2>();
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      prev = acc;
+      initB(acc, bias);
+      stepB_prev<0>(wl, q, lane, X, acc, prev, nd, seam);
+      stepB_prev<1>(wl, q, lane, X, acc, prev, nd, seam);
+      stepB_prev<2>(wl, q, lane, X, acc, prev, nd, seam);
+      stepB_prev<3>(wl, q, lane, X, acc, prev, nd, seam);
+      stepB_prev<4>(wl, q, lane, X, acc, prev, nd, seam);
+      stepB_prev<5>(wl, q, lane, X, acc, prev, nd, seam);
+      stepB_prev<6>(wl, q, lane, X, acc, prev, nd, seam);
+      stepB_prev<7>(wl, q, lane, X, acc, prev, nd, seam);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) park[wave][i][lane] = u4{nd[4 * i], nd[4 * i + 1], nd[4 * i + 2], nd[4 * i + 3]};
+    }
+    pieceB<0>(acc, nd, lane, seam);
+    pieceB<1>(acc, nd, lane, seam);
+    pieceB<2>(acc, nd, lane, seam);
+    pieceB<3>(acc, nd, lane, seam);
+    pieceB<4>(acc, nd, lane, seam);
+    pieceB<5>(acc, nd, lane, seam);
+    pieceB<6>(acc, nd, lane, seam);
+    pieceB<7>(acc, nd, lane, seam);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) park[wave][i][lane] = u4{nd[4 * i], nd[4 * i + 1], nd[4 * i + 2], nd[4 * i + 3]};
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) X[n][s] = park[wave][(n * 8 + s) & 3][lane];
+  }
+  unsigned s = 0;
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s ^= X[n][k][0] ^ X[n][k][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+}
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                      \
+      return 1;                                                                    \
+    }                                                                              \
+  } while (0)
+
+int main(int argc, char **argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 400;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int grid = cus;  // one workgroup (8 waves) per CU
+  const size_t nw = 4096, nx = (size_t)grid * kNW * 16 * 64;
+  std::vector<unsigned> h((nw + nx) * 4);
+  unsigned r = 12345u;
+  for (auto &v : h) {  // random bf16 pairs in [-1, 1), exponents kept small
+    r = r * 1664525u + 1013904223u;
+    const unsigned lo = 0x3c00u | (r >> 25), hi = 0x3c00u | ((r >> 9) & 0x7fu);
+    v = (lo | ((r & 1u) << 15)) | ((hi | ((r & 2u) << 14)) << 16);
+  }
+  u4 *dw, *dx;
+  float *dout;
+  CK(hipMalloc(&dw, nw * 16));
+  CK(hipMalloc(&dx, nx * 16));
+  CK(hipMalloc(&dout, (size_t)grid * 64 * kNW * 4));
+  CK(hipMemcpy(dw, h.data(), nw * 16, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dx, h.data() + nw * 4, nx * 16, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const double flop = 2.0 * 64 * 128 * 256 * kNW * (double)grid * iters;  // per launch
+  // 8 warm-up launches (the clock ramps under load), then the two variants
+  // alternated 8 times each, so both see the same clock history
+  for (int step = 0; step < 24; ++step) {
+    const int variant = step < 8 ? 0 : (step & 1);
+    const int rep = step < 8 ? -1 : (step - 8) / 2;
+    CK(hipEventRecord(e0, 0));
+    if (variant == 0)
+      hipLaunchKernelGGL(layer_a, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters);
+    else
+      hipLaunchKernelGGL(layer_b, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters);
+    CK(hipGetLastError());
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("{\"variant\": \"%s\", \"rep\": %d, \"iters\": %d, \"ms\": %.4f, \"tflops\": %.1f, \"frac_dense_bf16\": %.4f}\n",
+           variant == 0 ? "16x16x32 (4 m-tiles)" : "32x32x16 (2 n-tiles)", rep, iters, ms, flop / ms / 1e9,
+           flop / ms / 1e9 / 2516.6);
+    fflush(stdout);
+  }
+  return 0;
+}
