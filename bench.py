@@ -61,14 +61,14 @@ def pinned(n):
     return set(avail[:n])
 
 
-def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=None, also=None, reps=1):
+def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=None, also=None, reps=1, warm_s=0.3):
     """Time one more BASELINE.json single-GPU config the same way as the
     headline (preallocated outputs and workspace, HIP events on the launch
     stream, wall clock around the launches).  Reported next to the headline,
-    never as it.  W untimed warmup steps run first as one rollout (cfg4: as
-    many as it times (cfg4 ~40 ms), so the timed rollout runs at the sustained
-    clock rather than in the clock ramp after the host-side setup; the headline
-    keeps the driver's --warmup).  also: the same workload in another precision,
+    never as it.  W untimed warmup steps run first as one rollout, then the
+    timed workload itself back to back for warm_s seconds, so the timed
+    rollouts run at the sustained clock rather than in the clock ramp after
+    the host-side setup (the headline keeps the driver's --warmup).  also: the same workload in another precision,
     timed the same way and reported under alt_<precision>.  fixture: {label: states [n, K+1, 3, nx]} of the batch's first
     n ICs (committed test vectors); the final states' max |error| against each
     is reported."""
@@ -78,9 +78,19 @@ def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=Non
     solver = HybridSolver(weights, radius=radius, nx=nx, dt=dt, device=dev, precision=precision)
     ics = solver.baseline.initial_conditions(range(1000, 1000 + B), as_tensor=True)
     ws, _ = engine.workspace(HF_OP_RUN, B, nx, K, dev, model=solver._dm())
-    solver.run_batch(ics, max(W, 1), traj=False, ws=ws)
     final = torch.empty_like(ics)
     met = torch.empty(B, K + 1, 4, device=dev)
+    # warm-up: the W-step rollout, then the timed workload back to back for at
+    # least warm_s of wall time, so the timed rollouts run at the clock the chip
+    # sustains on this workload (after the host-side setup above the GPU has
+    # idled and the clock ramps again, MI355X_MICROARCH.md DVFS)
+    solver.run_batch(ics, max(W, 1), traj=False, ws=ws)
+    torch.cuda.synchronize(dev)
+    t_end = time.perf_counter() + warm_s
+    while time.perf_counter() < t_end:
+        for _ in range(reps):
+            solver.run_batch(ics, K, traj=False, metrics=met, out=final, ws=ws)
+        torch.cuda.synchronize(dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -103,9 +113,14 @@ def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=Non
            "finite_fraction": float(met[:, -1, 2].float().mean().item())}
     if also:  # the same workload in another precision (reported beside, not instead)
         s2 = HybridSolver(weights, radius=radius, nx=nx, dt=dt, device=dev, precision=also)
-        s2.run_batch(ics, max(W, 1), traj=False, ws=ws)
         final2 = torch.empty_like(ics)
+        s2.run_batch(ics, max(W, 1), traj=False, ws=ws)
         torch.cuda.synchronize(dev)
+        t_end = time.perf_counter() + warm_s
+        while time.perf_counter() < t_end:
+            for _ in range(reps):
+                s2.run_batch(ics, K // reps, traj=False, metrics=met, out=final2, ws=ws)
+            torch.cuda.synchronize(dev)
         a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ta = time.perf_counter()
         a0.record(stream)
@@ -321,10 +336,10 @@ def main():
         w_r1 = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r1.npz"), allow_pickle=False))
         w_r2 = dict(np.load(os.path.join(ROOT, "tests", "golden", "weights_W1_r2.npz"), allow_pickle=False))
         # both at BASELINE's T = 30, warmed for as many steps as they time
-        # cfg2's 30-step rollout lasts ~1.6 ms, so five run back to back (the
+        # cfg2's 30-step rollout lasts ~1.4 ms, so twenty run back to back (the
         # first launch's host latency would otherwise be ~4 % of the timed region)
         others = [other_config(w_r1, dev, "cfg2: 64-cell chain, 256-IC batch, r=1, f32", 256, 64, "f32", 30, 30, 1,
-                               also="f16x3", reps=5),
+                               also="f16x3", reps=20),
                   other_config(w_r2, dev, "cfg4: 1024-cell chain, 4096-IC batch, r=2, bf16 MLP weights, dt=3.125e-4",
                                4096, 1024, "bf16", 30, 30, 2, fixture=fx)]
 

@@ -1,7 +1,8 @@
 """Where the f32 rollout kernel's time goes (diagnostic, not a bench line).
 
 Times, on cfg3 shapes (4096 ICs x 64 cells, 50 steps):
-  * the headline rollout (trajectory + metrics) and a bare rollout (no outputs);
+  * the headline rollout (trajectory + metrics), a bare rollout (no outputs)
+    and each output alone;
   * hf_chain_flux (GNN only, no FV/Poisson) called once per step;
   * bare rollouts of FluxGNN(4,128,L) for L = 0,1,2,4: the per-layer slope is
     the message-passing loop's cost, the intercept input layer + readout + FV.
@@ -10,6 +11,7 @@ Every figure is kernel time from HIP events on the launch stream.
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gnn-plasma-flux_amd"))
@@ -69,8 +71,16 @@ def main():
     tr = torch.empty(B, T + 1, 3, nx, device=dev)
     me = torch.empty(B, T + 1, 4, device=dev)
     fin = torch.empty_like(s0)
+    # the clock ramps under load (MI355X_MICROARCH.md DVFS): ~0.5 s of rollouts
+    # before the first timed one, or the first figure reads several % high
+    t_end = time.perf_counter() + 0.5
+    while time.perf_counter() < t_end:
+        engine.run(m4, grid, s0, T, traj=False, metrics=False, out=fin)
+        torch.cuda.synchronize()
     out["headline_ms"] = timed(lambda: engine.run(m4, grid, s0, T, traj=tr, metrics=me, out=fin))
     out["bare_ms"] = timed(lambda: engine.run(m4, grid, s0, T, traj=False, metrics=False, out=fin))
+    out["traj_only_ms"] = timed(lambda: engine.run(m4, grid, s0, T, traj=tr, metrics=False, out=fin))
+    out["metrics_only_ms"] = timed(lambda: engine.run(m4, grid, s0, T, traj=False, metrics=me, out=fin))
     nf = torch.randn(B * nx, 4, device=dev)
     out["flux_only_x50_ms"] = timed(lambda: [engine.chain_flux(m4, nf, B, nx) for _ in range(T)])
     per_l = {}

@@ -10,7 +10,7 @@ shift
 mkdir -p gpurun_out
 for rep in 1 2; do
   for v in in "$@"; do
-    lib=build/diag/lib_$v.so
+    lib=${DIAG_DIR:-build/diag}/lib_$v.so
     [ "$v" = in ] && lib=gnn-plasma-flux_amd/hybridflux/_lib/libhybridflux.so
     DIAG_B=256 HYBRIDFLUX_LIB=$lib timeout -k 10 120 python tools/diag_rollout.py > gpurun_out/dc2_${TAG}_${v}_$rep.json || exit $?
     python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], round(d['headline_ms'],4), round(d['bare_ms'],4), round(d['layer_ms'],4), round(d['fixed_ms'],4))" gpurun_out/dc2_${TAG}_${v}_$rep.json $v $rep
