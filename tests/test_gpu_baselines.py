@@ -84,6 +84,26 @@ def test_pure_gnn_rollout_vs_reference(models):
     assert torch.equal(one["final"][0], out["final"][2])
 
 
+@pytest.mark.parametrize("H,nx,L,B", [(128, 64, 4, 3), (64, 64, 3, 2), (128, 32, 2, 5), (64, 16, 1, 3),
+                                       (128, 48, 0, 2), (64, 100, 2, 2)])
+def test_pure_gnn_rollout_shapes_vs_oracle(H, nx, L, B):
+    """PureGNN(4, H, L) rollouts vs the oracle restatement (evaluate_multi_ic.py:45-66):
+    nx in {16, 32, 48, 64} with H in {64, 128} run the one-launch kernel (one IC per
+    workgroup), nx = 100 the per-step GEMMs; T = 0 returns the initial state."""
+    import hybridflux as hf
+    torch.manual_seed(H + nx + L)
+    pg = hf.PureGNN(4, H, L).to(DEV)
+    grid = O.Grid(nx)
+    ics = np.stack([O.initial_condition(grid, s) for s in range(6000, 6000 + B)])
+    x = hf.BaselineSolver(nx, device=DEV).x
+    out = pg.rollout(torch.as_tensor(ics, device=DEV), 8, x)
+    pgp = O.params_from({k: v.detach().cpu() for k, v in pg.state_dict().items()})
+    for j in range(B):
+        close(out["traj"][j], O.pure_gnn_rollout(pgp, grid, ics[j], 8), 5e-5, 5e-5, what=f"ic{j}")
+    assert torch.equal(out["final"], out["traj"][:, -1])
+    assert torch.equal(pg.rollout(torch.as_tensor(ics, device=DEV), 0, x)["final"], torch.as_tensor(ics, device=DEV))
+
+
 def test_pinn_forward_and_rollout_vs_reference(models):
     hf, _, pn, b = models
     with torch.no_grad():
