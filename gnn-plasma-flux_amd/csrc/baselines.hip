@@ -327,61 +327,83 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
 
 // ---------------------------------------------------------------------------
 // PureGNN rollout in one launch (train_pure_gnn.py:57-76 iterated as
-// evaluate_multi_ic.py:45-66): a workgroup owns ONE IC for all T steps.  Its
-// state and hidden activations stay in LDS; node features [n, u, E, x] are
-// formed there each step.  Every GEMM runs as v_mfma_f32_16x16x4_f32 tiles of 16
-// output features x 16 cells with the weight operand read straight from
-// nn.Linear's rows (float4 per lane, the PINN kernel's permuted k order) and
-// the activations held in LDS as [k-block][cell group][lane][4].
-//  * message layer l: wave w computes output tile w of [P ; Q] = [W_a ; W_b] h
-//    (2H rows); the tiles go to LDS, then every thread finishes (feature, cell)
-//    pairs: h += tanh(P[i-1] + Q[i] + b) + tanh(P[i+1] + Q[i] + b), messages in
-//    edge order (from i-1, then i+1, as index_add_);
-//  * output_mlp: tanh(W_o1 h + b) as tiles, then the 3 x nx outputs as dot
-//    products; state += delta.
-// Shapes: nx = 16 NC (NC <= 4), H = 8 x waves (64 or 128).
-template <int H, int NC>
-__device__ __forceinline__ float *pure_act_at(float *act, int f, int c) {
-  // feature f (k index of the next GEMM) of cell c in the [k-block][group][lane][4] order
-  return act + (((f >> 4) * NC + (c >> 4)) * 64 + ((f >> 2) & 3) * 16 + (c & 15)) * 4 + (f & 3);
+// evaluate_multi_ic.py:45-66): a workgroup owns ONE IC for all T steps, its
+// state and hidden activations in LDS; node features [n, u, E, x] are formed
+// there each step.  Every GEMM runs as v_mfma_f32_16x16x4_f32 tiles (16 output
+// features x 16 cells) with the weight operand read straight from nn.Linear's
+// rows (float4 per lane: the PINN kernel's permuted k order) and the
+// activations held in LDS as [k-block][cell group g][lane][4], cell group g
+// holding cells NC c + g (c = lane & 15): the chain kernels' interleaved layout,
+// so a cell's neighbours are in the same lane of the next group, or one DPP row
+// rotation away at the group ends (periodic: row_ror wraps lane 15 to lane 0).
+//  * message layer: wave u computes P and Q (W_a h and W_b h, rows of
+//    update_mlps.l.0) for features 16u .. 16u + 15 over all cells; after a
+//    barrier (every read of h done) it finishes those features in registers:
+//    h += tanh(P[i-1] + Q[i] + b) + tanh(P[i+1] + Q[i] + b), messages in edge
+//    order (from i-1, then i+1, as index_add_), and writes them back in place;
+//  * output_mlp: o = tanh(W_o1 h + b) as tiles into LDS, then the 3 x nx
+//    outputs as dot products; state += delta (benchmark_timing.py:128-130).
+// A workgroup is H/16 waves; two share a CU, so one's epilogue runs beside
+// the other's MFMAs.  Shapes: nx = 16 NC (NC <= 4), H in {64, 128}.
+template <int NC>
+__device__ __forceinline__ int pure_act_idx(int f, int cell) {
+  const int g = cell % NC, c = cell / NC;
+  return (((f >> 4) * NC + g) * 64 + ((f >> 2) & 3) * 16 + c) * 4 + (f & 3);
+}
+__device__ __forceinline__ float dpp_ror(float v, int ctrl_is_15) {
+  const int iv = __builtin_bit_cast(int, v);
+  return __builtin_bit_cast(float, ctrl_is_15 ? __builtin_amdgcn_mov_dpp(iv, 0x12F, 0xf, 0xf, false)
+                                              : __builtin_amdgcn_mov_dpp(iv, 0x121, 0xf, 0xf, false));
 }
 
-// acc[g] = rows 16 t .. 16 t + 15 of W X over cell group g, W row r at rowptr(r) (K floats)
-template <int K, int NC, class RowPtr>
-__device__ __forceinline__ void pure_tile(const RowPtr &rowptr, int t, const float *act, int lane, f4v (&acc)[NC]) {
+// acc[j][g] (j < NR row tiles) = rows of W X over cell group g; row tile j's
+// weight row for lane row m (0..15) is rowptr(j, m), K floats each.
+template <int K, int NC, int NR, class RowPtr>
+__device__ __forceinline__ void pure_tiles(const RowPtr &rowptr, const float *act, int lane, f4v (&acc)[NR][NC]) {
   constexpr int KB = K / 16, P = 3;
-  const float *wr = rowptr(16 * t + (lane & 15)) + 4 * (lane >> 4);
+  const float *wr[NR];
 #pragma unroll
-  for (int g = 0; g < NC; ++g) acc[g] = f4v{0.f, 0.f, 0.f, 0.f};
-  f4v wq[P];
+  for (int j = 0; j < NR; ++j) {
+    wr[j] = rowptr(j, lane & 15) + 4 * (lane >> 4);
+#pragma unroll
+    for (int g = 0; g < NC; ++g) acc[j][g] = f4v{0.f, 0.f, 0.f, 0.f};
+  }
+  f4v wq[P][NR];
 #pragma unroll
   for (int kb = 0; kb < KB + P - 1; ++kb) {
-    if (kb < KB) wq[kb % P] = *reinterpret_cast<const f4v *>(wr + 16 * kb);
+    if (kb < KB) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j) wq[kb % P][j] = *reinterpret_cast<const f4v *>(wr[j] + 16 * kb);
+    }
     if (kb >= P - 1) {
       const int c = kb - (P - 1);
 #pragma unroll
       for (int g = 0; g < NC; ++g) {
         const f4v bv = *reinterpret_cast<const f4v *>(act + ((c * NC + g) * 64 + lane) * 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][e], bv[e], acc[g], 0, 0, 0);
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[j][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j][g], 0, 0, 0);
       }
     }
   }
 }
 
+#ifndef HF_PURE_WG
+#define HF_PURE_WG 2
+#endif
 template <int H, int NC>
-__global__ __launch_bounds__(64 * (H / 8), 1) void pure_run_kernel(PureW w, const float *__restrict__ state0,
-                                                                   float *__restrict__ final_state,
-                                                                   const float *__restrict__ x, float *__restrict__ traj,
-                                                                   int B, int T) {
-  constexpr int NX = 16 * NC, NTH = 64 * (H / 8);
+__global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(PureW w, const float *__restrict__ state0,
+                                                                    float *__restrict__ final_state,
+                                                                    const float *__restrict__ x,
+                                                                    float *__restrict__ traj, int B, int T) {
+  constexpr int NX = 16 * NC, NTH = 64 * (H / 16);
   __shared__ float s_st[3 * NX];
   __shared__ float s_x[NX];
   __shared__ f4v s_act4[H * NX / 4];
-  __shared__ f4v s_stg4[2 * H * NX / 4];  // [2H][NX]: P | Q of a message layer, then o = tanh(W_o1 h + b)
   float *act = reinterpret_cast<float *>(s_act4);
-  float *stg = reinterpret_cast<float *>(s_stg4);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, u = tid >> 6, lane = tid & 63, q4 = 4 * (lane >> 4);
   const int64_t b = blockIdx.x;
   const int64_t ldt = (int64_t)(T + 1) * 3 * NX;
   for (int i = tid; i < 3 * NX; i += NTH) {
@@ -400,51 +422,58 @@ __global__ __launch_bounds__(64 * (H / 8), 1) void pure_run_kernel(PureW w, cons
       v = __fmaf_rn(wi[1], s_st[NX + c], v);
       v = __fmaf_rn(wi[2], s_st[2 * NX + c], v);
       v = __fmaf_rn(wi[3], s_x[c], v);
-      *pure_act_at<H, NC>(act, f, c) = tanhf(__fadd_rn(v, w.b_in[f]));
+      act[pure_act_idx<NC>(f, c)] = tanhf(__fadd_rn(v, w.b_in[f]));
     }
     __syncthreads();
     for (int l = 0; l < w.L; ++l) {
-      const float *W = w.w_l + l * w.ls;
-      f4v acc[NC];
-      // output row r < H: P (W_a, columns [0, H) of row r); r >= H: Q (columns [H, 2H) of row r - H)
-      pure_tile<H, NC>([&](int r) { return W + (int64_t)(r < H ? r : r - H) * 2 * H + (r < H ? 0 : H); }, wave, act,
-                       lane, acc);
+      const float *W = w.w_l + l * w.ls, *bl = w.b_l + l * w.ls;
+      f4v acc[2][NC];  // [P | Q][cell group]
+      pure_tiles<H, NC, 2>([&](int j, int m) { return W + (int64_t)(16 * u + m) * 2 * H + j * H; }, act, lane, acc);
+      __syncthreads();  // every wave's reads of h are done: h is rewritten in place below
+      f4v bq;
 #pragma unroll
-      for (int g = 0; g < NC; ++g)
+      for (int i = 0; i < 4; ++i) bq[i] = bl[16 * u + q4 + i];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) stg[(16 * wave + 4 * (lane >> 4) + i) * NX + 16 * g + (lane & 15)] = acc[g][i];
-      __syncthreads();
-      const float *bl = w.b_l + l * w.ls;
-      for (int idx = tid; idx < H * NX; idx += NTH) {
-        const int f = idx / NX, c = idx - f * NX;
-        const int cp = c == 0 ? NX - 1 : c - 1, cn = c == NX - 1 ? 0 : c + 1;
-        const float q = stg[(H + f) * NX + c], bf = bl[f];
-        float m = tanhf(__fadd_rn(__fadd_rn(stg[f * NX + cp], q), bf));
-        m = __fadd_rn(m, tanhf(__fadd_rn(__fadd_rn(stg[f * NX + cn], q), bf)));
-        float *h = pure_act_at<H, NC>(act, f, c);
-        *h = __fadd_rn(*h, m);
+      for (int g = 0; g < NC; ++g) {
+        float *hp = act + ((u * NC + g) * 64 + lane) * 4;
+        f4v h = *reinterpret_cast<const f4v *>(hp);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          // cell NC c + g: left (g - 1, c) or, at g = 0, (NC - 1, c - 1); right (g + 1, c) or (0, c + 1)
+          const float pl = g > 0 ? acc[0][g - 1][i] : dpp_ror(acc[0][NC - 1][i], 0);
+          const float pr = g < NC - 1 ? acc[0][g + 1][i] : dpp_ror(acc[0][0][i], 1);
+          const float qv = acc[1][g][i];
+          float m = tanhf(__fadd_rn(__fadd_rn(pl, qv), bq[i]));
+          m = __fadd_rn(m, tanhf(__fadd_rn(__fadd_rn(pr, qv), bq[i])));
+          h[i] = __fadd_rn(h[i], m);
+        }
+        *reinterpret_cast<f4v *>(hp) = h;
       }
       __syncthreads();
     }
-    // output_mlp.0: o = tanh(W_o1 h + b_o1), rows [0, H) -> stg[f][c]
-    if (wave < H / 16) {
-      f4v acc[NC];
-      pure_tile<H, NC>([&](int r) { return w.w_o1 + (int64_t)r * H; }, wave, act, lane, acc);
+    // output_mlp.0: o = tanh(W_o1 h + b_o1), written over h once every wave has read it
+    {
+      f4v acc[1][NC];
+      pure_tiles<H, NC, 1>([&](int, int m) { return w.w_o1 + (int64_t)(16 * u + m) * H; }, act, lane, acc);
+      f4v bo;
 #pragma unroll
-      for (int g = 0; g < NC; ++g)
+      for (int i = 0; i < 4; ++i) bo[i] = w.b_o1[16 * u + q4 + i];
+      __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int f = 16 * wave + 4 * (lane >> 4) + i;
-          stg[f * NX + 16 * g + (lane & 15)] = tanhf(__fadd_rn(acc[g][i], w.b_o1[f]));
-        }
+      for (int g = 0; g < NC; ++g) {
+        f4v o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = tanhf(__fadd_rn(acc[0][g][i], bo[i]));
+        *reinterpret_cast<f4v *>(act + ((u * NC + g) * 64 + lane) * 4) = o;
+      }
     }
     __syncthreads();
-    // output_mlp.2 and the update (benchmark_timing.py:128-130): state += W_o2 o + b_o2
+    // output_mlp.2 and the update: state += W_o2 o + b_o2
     if (tid < 3 * NX) {
       const int ch = tid / NX, c = tid - ch * NX;
       const float *wo = w.w_o2 + ch * H;
       float v = 0.f;
-      for (int f = 0; f < H; ++f) v = __fmaf_rn(wo[f], stg[f * NX + c], v);
+      for (int f = 0; f < H; ++f) v = __fmaf_rn(wo[f], act[pure_act_idx<NC>(f, c)], v);
       s_st[tid] = __fadd_rn(s_st[tid], __fadd_rn(v, w.b_o2[ch]));
     }
     __syncthreads();
@@ -460,10 +489,10 @@ template <int H>
 hipError_t pure_fused_h(const PureW &w, const float *state0, float *final_state, const float *x, int B, int nx, int T,
                         float *traj, hipStream_t s) {
   switch (nx / 16) {
-    case 1: hipLaunchKernelGGL((pure_run_kernel<H, 1>), dim3(B), dim3(64 * (H / 8)), 0, s, w, state0, final_state, x, traj, B, T); break;
-    case 2: hipLaunchKernelGGL((pure_run_kernel<H, 2>), dim3(B), dim3(64 * (H / 8)), 0, s, w, state0, final_state, x, traj, B, T); break;
-    case 3: hipLaunchKernelGGL((pure_run_kernel<H, 3>), dim3(B), dim3(64 * (H / 8)), 0, s, w, state0, final_state, x, traj, B, T); break;
-    default: hipLaunchKernelGGL((pure_run_kernel<H, 4>), dim3(B), dim3(64 * (H / 8)), 0, s, w, state0, final_state, x, traj, B, T); break;
+    case 1: hipLaunchKernelGGL((pure_run_kernel<H, 1>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
+    case 2: hipLaunchKernelGGL((pure_run_kernel<H, 2>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
+    case 3: hipLaunchKernelGGL((pure_run_kernel<H, 3>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
+    default: hipLaunchKernelGGL((pure_run_kernel<H, 4>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
   }
   return hipGetLastError();
 }

@@ -192,10 +192,13 @@ int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const
  * hf_pure_gnn_run = the rollout of scripts/evaluation/evaluate_multi_ic.py:45-66
  * (state <- state + delta, node features [n,u,E,x]) for B ICs on chains of nx
  * cells: state0/final [B][3][nx], traj [B][T+1][3][nx] or NULL; x [nx].
- * Workspace: hf_pure_gnn_workspace_bytes(H, N = B*nx, E = 2N).  On chains
- * whose nx divides 128 with H a multiple of 64, each message layer is one f32
- * MFMA GEMM that forms the messages and the residual in its epilogue
- * (csrc/tgemm.h EpiMsg); other shapes run the generic linear + gather kernels.
+ * Workspace: hf_pure_gnn_workspace_bytes(H, N = B*nx, E = 2N).
+ * hf_pure_gnn_run at nx in {16, 32, 48, 64} with H in {64, 128} is ONE launch
+ * for all T steps (one IC per workgroup, activations in LDS; the workspace is
+ * unused).  Otherwise, on chains whose nx divides 128 with H a multiple of 64,
+ * each message layer is one f32 MFMA GEMM that forms the messages and the
+ * residual in its epilogue (csrc/tgemm.h EpiMsg); other shapes run the generic
+ * linear + gather kernels.
  *
  * PINN (scripts/training/train_pinn.py:36-61): net.0 [H][D], (layers-2) x
  * [H][H], net.last [D][H] (+biases), tanh between; out = state + net(state)
