@@ -42,7 +42,7 @@ def flop_per_sample(cfg_name, nx=64, H=128, L=4, F=4):
     return evals * (fwd + bwd) * nx
 
 
-def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False, fused_adam=False):
+def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False, fused_adam=False, warm_s=0.3):
     """samples/s of `steps` optimizer steps at `batch` samples each (eager, or
     replaying the captured step: hybridflux.training.GraphedStep; fused_adam:
     torch's single-kernel Adam instead of the default multi-tensor one)."""
@@ -61,6 +61,13 @@ def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False,
 
     run(warmup + (4 if graphed else 0))  # graphed: 3 eager warmup steps, the capture, then replays
     torch.cuda.synchronize()
+    # then the timed workload back to back for warm_s seconds: the GPU idled
+    # during the model setup, and the clock ramps under load again
+    # (MI355X_MICROARCH.md DVFS), so the timed steps run at the sustained clock
+    t_end = time.perf_counter() + warm_s
+    while time.perf_counter() < t_end:
+        run(steps)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(steps)
     torch.cuda.synchronize()
@@ -93,6 +100,7 @@ def main():
     ap.add_argument("--batches", default="1,64,256,2000")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warm-s", type=float, default=0.3, help="seconds of the timed workload run before timing it")
     ap.add_argument("--cpu-samples", type=int, default=100)
     args = ap.parse_args()
     import hybridflux as hf
@@ -106,10 +114,10 @@ def main():
     rates = {}
     for b in [int(v) for v in args.batches.split(",") if v]:
         steps = max(2, args.steps if b > 1 else args.steps * 5)
-        r, ms = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver)
-        rg, msg = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, graphed=True)
+        r, ms = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, warm_s=args.warm_s)
+        rg, msg = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, graphed=True, warm_s=args.warm_s)
         try:
-            rf, _ = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, fused_adam=True)
+            rf, _ = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, fused_adam=True, warm_s=args.warm_s)
         except (RuntimeError, TypeError) as e:  # fused Adam unavailable in this torch build
             print(f"fused Adam: {e}", file=sys.stderr)
             rf = 0.0
