@@ -288,6 +288,150 @@ __global__ __launch_bounds__(64 * kNW, 1) void layer_b(const u4 *__restrict__ ws
   out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
 }
 
+// ------------------------------------------------------------- A + weight ring
+// layer_a with the weights streamed through a 3-slot LDS ring of 16 KiB chunks
+// (one output pair each) by LDS-DMA, as CoreBF16 does: before each pair a ring
+// barrier (own DMA of the chunk landed, then s_barrier), then the DMA of the
+// chunk two ahead into the slot just freed.  DMAV selects who issues it and when:
+//   0: all 8 waves, 2 pieces each, right after the barrier
+//   1: all 8 waves, 2 pieces each, after unit 0's fragment reads (the kept form)
+//   2: waves 0-3 (one per SIMD), 4 pieces each, after unit 0's fragment reads
+//   3: no DMA at all (barriers only; the slots are never refilled)
+struct RingM {
+  __amdgpu_buffer_rsrc_t rsrc;
+  unsigned lds0;  // LDS byte address of slot 0
+  int lane_off, wave, pos, chunks;
+  __device__ void issue(int chunk, int slot, int j0, int j1) const {
+#pragma unroll
+    for (int j = j0; j < j1; ++j) {
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + slot * 16384 + j * 1024);
+      const unsigned soff = __builtin_amdgcn_readfirstlane((unsigned)(chunk * 16384 + j * 1024));
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %1, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(lane_off), "s"(dst), "s"(rsrc), "s"(soff)
+          : "memory");
+    }
+  }
+};
+template <int DMAV>
+__device__ __forceinline__ void ring_dma(const RingM &R, int chunk, int slot) {
+  if constexpr (DMAV == 0 || DMAV == 1) R.issue(chunk, slot, 2 * R.wave, 2 * R.wave + 2);
+  if constexpr (DMAV == 2) {
+    if (R.wave < 4) R.issue(chunk, slot, 4 * R.wave, 4 * R.wave + 4);
+  }
+}
+template <int DMAV>
+__device__ __forceinline__ void ring_wait() {
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (DMAV == 3) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (DMAV == 2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int KB>
+__device__ __forceinline__ void unitR(const u4 *slot, int lane, const u4 (&X)[4][4], PairA &P) {
+  u4 w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = slot[(KB * 4 + i) * 64 + lane];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      P.a[mt][t] = mma16(w[2 * t], X[mt][KB], P.a[mt][t]);
+      P.g[mt][t] = mma16(w[2 * t + 1], X[mt][KB], P.g[mt][t]);
+    }
+}
+// one output pair from ring chunk R.pos (prev: the pair whose epilogue runs under it, or none)
+template <int DMAV, bool PREV>
+__device__ __forceinline__ void pairR(RingM &R, const u4 *ring, int lane, const u4 (&X)[4][4], PairA &acc,
+                                      const PairA &prev, u4 (&nh)[4], float bias) {
+  ring_wait<DMAV>();
+  const int slot = R.pos % 3, ahead = (R.pos + 2) % R.chunks, aslot = (R.pos + 2) % 3;
+  if constexpr (DMAV == 0) ring_dma<DMAV>(R, ahead, aslot);
+  const u4 *sl = ring + slot * 1024;
+  initA(acc, bias);
+  unitR<0>(sl, lane, X, acc);
+  if constexpr (DMAV == 1 || DMAV == 2) ring_dma<DMAV>(R, ahead, aslot);
+  if constexpr (PREV) pieceA<0>(prev, nh);
+  interleave<16, PREV ? 2 : 0, 4>();
+  unitR<1>(sl, lane, X, acc);
+  if constexpr (PREV) pieceA<1>(prev, nh);
+  interleave<16, PREV ? 2 : 0, 4>();
+  unitR<2>(sl, lane, X, acc);
+  if constexpr (PREV) pieceA<2>(prev, nh);
+  interleave<16, PREV ? 2 : 0, 4>();
+  unitR<3>(sl, lane, X, acc);
+  if constexpr (PREV) pieceA<3>(prev, nh);
+  interleave<16, PREV ? 2 : 0, 4>();
+  R.pos = R.pos + 1;
+}
+
+template <int DMAV>
+__global__ __launch_bounds__(64 * kNW, 1) void layer_ring(const u4 *__restrict__ wsrc, const u4 *__restrict__ xsrc,
+                                                          float *__restrict__ out, int iters, int chunks) {
+  __shared__ u4 ring[3 * 1024];     // 3 slots of 16 KiB
+  __shared__ u4 park[kNW][4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  RingM R;
+  R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<u4 *>(wsrc), 0, chunks * 16384, 0x00020000);
+  R.lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void *)ring;
+  R.lane_off = lane * 16;
+  R.wave = wave;
+  R.pos = 0;
+  R.chunks = chunks;
+  u4 X[4][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) X[mt][kb] = xsrc[((blockIdx.x * kNW + wave) * 16 + mt * 4 + kb) * 64 + lane];
+  if constexpr (DMAV == 3) {  // fill the three slots once
+    for (int i = threadIdx.x; i < 3 * 1024; i += blockDim.x) ring[i] = wsrc[i];
+  } else {
+    if (wave < 8) {
+      const int per = DMAV == 2 ? 4 : 2;
+      if (DMAV != 2 || wave < 4) {
+        R.issue(0, 0, per * wave, per * wave + per);
+        R.issue(1, 1, per * wave, per * wave + per);
+      }
+    }
+  }
+  __syncthreads();
+  const float bias = 0.01f * lane;
+  for (int it = 0; it < iters; ++it) {
+    PairA acc, prev;
+    u4 nh[4];
+    pairR<DMAV, false>(R, ring, lane, X, acc, prev, nh, bias);
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      prev = acc;
+      pairR<DMAV, true>(R, ring, lane, X, acc, prev, nh, bias);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) park[wave][mt][lane] = nh[mt];
+    }
+    pieceA<0>(acc, nh);
+    pieceA<1>(acc, nh);
+    pieceA<2>(acc, nh);
+    pieceA<3>(acc, nh);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) park[wave][mt][lane] = nh[mt];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) X[mt][kb] = park[wave][(mt + kb) & 3][lane];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned s = 0;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) s ^= X[mt][kb][0] ^ X[mt][kb][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+}
+
 #define CK(x)                                                                      \
   do {                                                                             \
     hipError_t e_ = (x);                                                           \
@@ -302,7 +446,8 @@ int main(int argc, char **argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int grid = cus;  // one workgroup (8 waves) per CU
-  const size_t nw = 4096, nx = (size_t)grid * kNW * 16 * 64;
+  const int chunks = 20;  // the ring's stream: 5 layers x 4 pairs x 16 KiB (cfg4's forward pass)
+  const size_t nw = (size_t)chunks * 1024, nx = (size_t)grid * kNW * 16 * 64;
   std::vector<unsigned> h((nw + nx) * 4);
   unsigned r = 12345u;
   for (auto &v : h) {  // random bf16 pairs in [-1, 1), exponents kept small
@@ -321,24 +466,30 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double flop = 2.0 * 64 * 128 * 256 * kNW * (double)grid * iters;  // per launch
-  // 8 warm-up launches (the clock ramps under load), then the two variants
-  // alternated 8 times each, so both see the same clock history
-  for (int step = 0; step < 24; ++step) {
-    const int variant = step < 8 ? 0 : (step & 1);
-    const int rep = step < 8 ? -1 : (step - 8) / 2;
+  // 8 warm-up launches (the clock ramps under load), then the variants in
+  // turn, 6 rounds, so all see the same clock history
+  const char *names[6] = {"16x16x32 static LDS weights", "32x32x16 static LDS weights", "16x16x32 ring, DMA at barrier",
+                          "16x16x32 ring, DMA after unit 0 (kept form)", "16x16x32 ring, DMA by 4 waves",
+                          "16x16x32 ring barriers, no DMA"};
+  for (int step = 0; step < 8 + 6 * 6; ++step) {
+    const int variant = step < 8 ? 0 : (step - 8) % 6;
+    const int rep = step < 8 ? -1 : (step - 8) / 6;
     CK(hipEventRecord(e0, 0));
-    if (variant == 0)
-      hipLaunchKernelGGL(layer_a, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters);
-    else
-      hipLaunchKernelGGL(layer_b, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters);
+    switch (variant) {
+      case 0: hipLaunchKernelGGL(layer_a, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters); break;
+      case 1: hipLaunchKernelGGL(layer_b, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters); break;
+      case 2: hipLaunchKernelGGL(layer_ring<0>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
+      case 3: hipLaunchKernelGGL(layer_ring<1>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
+      case 4: hipLaunchKernelGGL(layer_ring<2>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
+      default: hipLaunchKernelGGL(layer_ring<3>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
+    }
     CK(hipGetLastError());
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0.f;
     CK(hipEventElapsedTime(&ms, e0, e1));
     printf("{\"variant\": \"%s\", \"rep\": %d, \"iters\": %d, \"ms\": %.4f, \"tflops\": %.1f, \"frac_dense_bf16\": %.4f}\n",
-           variant == 0 ? "16x16x32 (4 m-tiles)" : "32x32x16 (2 n-tiles)", rep, iters, ms, flop / ms / 1e9,
-           flop / ms / 1e9 / 2516.6);
+           names[variant], rep, iters, ms, flop / ms / 1e9, flop / ms / 1e9 / 2516.6);
     fflush(stdout);
   }
   return 0;
