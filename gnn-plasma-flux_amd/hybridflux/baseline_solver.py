@@ -60,6 +60,9 @@ class BaselineSolver:
     def initial_conditions(self, seeds, as_tensor=False):
         """Batched ICs for a list of seeds -> [B,3,nx] (numpy, or a device tensor)."""
         nu = [self._modes(s) for s in seeds]
+        if not nu:  # an empty shard (an IC-sharded job with more ranks than ICs)
+            st = torch.zeros(0, 3, self.nx, dtype=torch.float32, device=self.device)
+            return st if as_tensor else st.cpu().numpy()
         n = torch.as_tensor(np.stack([a for a, _ in nu]), device=self.device)
         u = torch.as_tensor(np.stack([b for _, b in nu]), device=self.device)
         st = torch.stack([n, u, engine.poisson(self.grid, n)], dim=1).contiguous()

@@ -25,9 +25,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 # (label, n_total, nx, T, precision, weights): the fused nx = 64 rollout
-# (cfg5's per-rank kernel) and the generic two-launch sequencing (nx = 256)
+# (cfg5's per-rank kernel), the generic two-launch sequencing (nx = 256), and
+# one IC over the ranks (empty shards still take part in every exchange)
 CASES = [("fused64_f32", 37, 64, 12, "f32", "W1_r2"),
-         ("generic256_bf16", 9, 256, 6, "bf16", "W1_r2")]
+         ("generic256_bf16", 9, 256, 6, "bf16", "W1_r2"),
+         ("one_ic", 1, 64, 5, "f32", "W1_r2")]  # at 2 ranks rank 1's shard is EMPTY
 
 
 def main(out):

@@ -41,6 +41,8 @@ def _oracle_local(seeds):
     sys.path.insert(0, root)
     from oracle import hybrid_oracle as O
     G = O.Grid(64)
+    if not len(seeds):  # an empty shard (more ranks than ICs)
+        return torch.zeros(0, T + 1, 4), np.zeros((0, T + 1, 3, 64), np.float32)
     w = dict(np.load(os.path.join(root, "tests", "golden", "weights_W1_r1.npz")))
     ics = np.stack([O.initial_condition(G, s) for s in seeds])
     S, _ = O.hybrid_run(O.params_from(w), G, ics, T)
@@ -76,10 +78,11 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_gloo_sharded_rollout(tmp_path, world):
     """world 2: shards 3 + 2; world 4 (a rehearsal of more ranks than the GPU
-    test's 2): 2 + 1 + 1 + 1."""
+    test's 2): 2 + 1 + 1 + 1; world 8: 1 x 5 then three EMPTY shards (more
+    ranks than ICs), which still take part in the gather."""
     port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     want, _ = _oracle_local(list(range(1000, 1000 + N_TOTAL)))

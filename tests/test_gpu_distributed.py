@@ -51,7 +51,7 @@ def test_two_ranks_equal_one_rank_bitwise(tmp_path):
     a, b = np.load(one), np.load(two)
     assert int(a["world"]) == 1 and int(b["world"]) == 2
     assert float(b["max_over_ranks"]) == 2.0
-    for label in ("fused64_f32", "generic256_bf16"):
+    for label in ("fused64_f32", "generic256_bf16", "one_ic"):
         for key in ("metrics", "summary", "final", "cmp_mse", "cmp_summary"):
             x, y = a[f"{label}/{key}"], b[f"{label}/{key}"]
             assert x.shape == y.shape, (label, key, x.shape, y.shape)
@@ -60,6 +60,7 @@ def test_two_ranks_equal_one_rank_bitwise(tmp_path):
             assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (label, key)
     # the ragged shards: rank 0 holds ceil(n/2) ICs
     assert int(b["fused64_f32/local_n"]) == 19 and int(b["generic256_bf16/local_n"]) == 5
+    assert int(b["one_ic/local_n"]) == 1 and a["one_ic/metrics"].shape[0] == 1  # rank 1 held 0 ICs
 
 
 @pytest.mark.timeout(400)
