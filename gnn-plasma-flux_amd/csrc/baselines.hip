@@ -483,6 +483,9 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
   for (int i = tid; i < 3 * NX; i += NTH) final_state[b * 3 * NX + i] = s_st[i];
 }
 
+#ifndef HF_PURE_FUSED
+#define HF_PURE_FUSED 1
+#endif
 bool pure_fused_ok(int H, int nx) { return (H == 64 || H == 128) && nx % 16 == 0 && nx >= 16 && nx <= 64; }
 
 template <int H>
@@ -532,21 +535,18 @@ hipError_t launch_pure_gnn_run(const float *params, int H, int L, const float *s
                                const float *x, int B, int nx, int T, float *traj, void *ws, hipStream_t s) {
   const PureW w = pure_view(params, 4, H, L);
   const int64_t N = (int64_t)B * nx, S = 3LL * nx;
-  PureWs b = carve_pure(ws, H, N);
-  float *st[2] = {reinterpret_cast<float *>(b.buckets),
-                  reinterpret_cast<float *>(static_cast<char *>(b.buckets) + a256(sizeof(float) * N * 3))};
   const int64_t ldt = (T + 1) * S;
   hipError_t e;
-#ifndef HF_PURE_FUSED
-#define HF_PURE_FUSED 1
-#endif
-  if (HF_PURE_FUSED && T > 0 && pure_fused_ok(H, nx))  // one launch (it writes trajectory row 0 itself)
+  if (HF_PURE_FUSED && T > 0 && pure_fused_ok(H, nx))  // one launch (it writes trajectory row 0 itself; no workspace)
     return H == 64 ? pure_fused_h<64>(w, state0, final_state, x, B, nx, T, traj, s)
                    : pure_fused_h<128>(w, state0, final_state, x, B, nx, T, traj, s);
   if (traj && (e = hipMemcpy2DAsync(traj, sizeof(float) * ldt, state0, sizeof(float) * S, sizeof(float) * S, B,
                                     hipMemcpyDeviceToDevice, s)))
     return e;
   if (T == 0) return hipMemcpyAsync(final_state, state0, sizeof(float) * N * 3, hipMemcpyDeviceToDevice, s);
+  PureWs b = carve_pure(ws, H, N);  // (the workspace is non-NULL on this path: hf_pure_gnn_run checks)
+  float *st[2] = {reinterpret_cast<float *>(b.buckets),
+                  reinterpret_cast<float *>(static_cast<char *>(b.buckets) + a256(sizeof(float) * N * 3))};
   const unsigned nb = (unsigned)((N + 255) / 256), sb = (unsigned)((N * 3 + 255) / 256);
   const float *cur = state0;
   for (int t = 0; t < T; ++t) {
@@ -562,6 +562,16 @@ hipError_t launch_pure_gnn_run(const float *params, int H, int L, const float *s
 
 int64_t pinn_ws_bytes(int D, int H, int64_t B) {
   return (int64_t)(2 * a256(sizeof(float) * B * H) + 2 * a256(sizeof(float) * B * D));
+}
+
+int64_t pure_gnn_run_ws_bytes(int H, int B, int nx, int T) {
+  if (B == 0 || T == 0 || (HF_PURE_FUSED && pure_fused_ok(H, nx))) return 0;
+  return pure_gnn_ws_bytes(H, (int64_t)B * nx, 2LL * B * nx);
+}
+
+int64_t pinn_run_ws_bytes(int D, int H, int64_t B) {
+  // the one-launch shape needs no scratch for any layer count the ABI admits
+  return (B == 0 || pinn_fused_ok(D, H, 2)) ? 0 : pinn_ws_bytes(D, H, B);
 }
 
 hipError_t launch_pinn_forward(const float *params, int D, int H, int L, const float *state, float *out, int64_t B,
@@ -587,14 +597,14 @@ hipError_t launch_pinn_forward(const float *params, int D, int H, int L, const f
 // evaluate_multi_ic.py:70-83 for B ICs at once: traj [B][T+1][D] (optional).
 hipError_t launch_pinn_run(const float *params, int D, int H, int L, const float *state0, float *final_state,
                            int64_t B, int T, float *traj, void *ws, hipStream_t s) {
-  char *p = static_cast<char *>(ws) + 2 * a256(sizeof(float) * B * H);
-  float *st[2] = {reinterpret_cast<float *>(p), reinterpret_cast<float *>(p + a256(sizeof(float) * B * D))};
   const size_t row = sizeof(float) * D, ldt = row * (T + 1);
   hipError_t e;
-  // one launch (the kernel writes trajectory row 0 itself)
+  // one launch (the kernel writes trajectory row 0 itself; no workspace)
   if (T > 0 && pinn_fused_ok(D, H, L)) return pinn_fused(pinn_view(params, D, H, L), state0, final_state, B, T, traj, s);
   if (traj && (e = hipMemcpy2DAsync(traj, ldt, state0, row, row, B, hipMemcpyDeviceToDevice, s))) return e;
   if (T == 0) return hipMemcpyAsync(final_state, state0, row * B, hipMemcpyDeviceToDevice, s);
+  char *p = static_cast<char *>(ws) + 2 * a256(sizeof(float) * B * H);  // non-NULL here: hf_pinn_run checks
+  float *st[2] = {reinterpret_cast<float *>(p), reinterpret_cast<float *>(p + a256(sizeof(float) * B * D))};
   const float *cur = state0;
   for (int t = 0; t < T; ++t) {
     float *nxt = t == T - 1 ? final_state : st[t & 1];

@@ -472,6 +472,11 @@ int64_t hf_pure_gnn_workspace_bytes(int hidden, int64_t N, int64_t E) {
   return hf::pure_gnn_ws_bytes(hidden, N, E);
 }
 
+int64_t hf_pure_gnn_run_workspace_bytes(int hidden, int B, int nx, int T) {
+  if (hidden < 1 || B < 0 || nx < 1 || T < 0) return -1;
+  return hf::pure_gnn_run_ws_bytes(hidden, B, nx, T);
+}
+
 int hf_pure_gnn_forward(const float *params, int in_dim, int hidden, int layers, const float *nf, int64_t N,
                         const int64_t *ei, int64_t E, int chain_nx, float *delta, void *ws, void *stream) {
   if (in_dim < 1 || hidden < 1 || layers < 0) return fail(HF_EINVAL, "hf_pure_gnn_forward: bad model dimensions");
@@ -490,7 +495,9 @@ int hf_pure_gnn_run(const float *params, int hidden, int layers, const float *st
                     const float *x, int B, int nx, int T, float *traj, void *ws, void *stream) {
   if (hidden < 1 || layers < 0 || B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_pure_gnn_run: bad argument");
   if (B == 0) return HF_OK;
-  if (!params || !state0 || !final_state || !x || !ws) return fail(HF_EINVAL, "hf_pure_gnn_run: NULL pointer");
+  if (!params || !state0 || !final_state || !x) return fail(HF_EINVAL, "hf_pure_gnn_run: NULL pointer");
+  if (!ws && hf::pure_gnn_run_ws_bytes(hidden, B, nx, T) > 0)
+    return fail(HF_EINVAL, "hf_pure_gnn_run: NULL workspace (hf_pure_gnn_run_workspace_bytes > 0 for this shape)");
   HF_CHECK_HIP(hf::launch_pure_gnn_run(params, hidden, layers, state0, final_state, x, B, nx, T, traj, ws,
                                        as_stream(stream)),
                "hf_pure_gnn_run");
@@ -505,7 +512,7 @@ int64_t hf_pinn_param_count(int dim, int hidden, int layers) {
 
 int64_t hf_pinn_workspace_bytes(int dim, int hidden, int64_t B) {
   if (dim < 1 || hidden < 1 || B < 0) return -1;
-  return hf::pinn_ws_bytes(dim, hidden, B);
+  return hf::pinn_run_ws_bytes(dim, hidden, B);
 }
 
 static int pinn_args(const char *fn, int dim, int hidden, int layers, int64_t B) {
@@ -518,7 +525,9 @@ int hf_pinn_forward(const float *params, int dim, int hidden, int layers, const 
                     void *ws, void *stream) {
   if (int rc = pinn_args("hf_pinn_forward", dim, hidden, layers, B)) return rc;
   if (B == 0) return HF_OK;
-  if (!params || !state || !out || !ws) return fail(HF_EINVAL, "hf_pinn_forward: NULL pointer");
+  if (!params || !state || !out) return fail(HF_EINVAL, "hf_pinn_forward: NULL pointer");
+  if (!ws && hf::pinn_run_ws_bytes(dim, hidden, B) > 0)
+    return fail(HF_EINVAL, "hf_pinn_forward: NULL workspace (hf_pinn_workspace_bytes > 0 for this shape)");
   if (state == out) return fail(HF_EINVAL, "hf_pinn_forward: state and out must not alias");
   HF_CHECK_HIP(hf::launch_pinn_forward(params, dim, hidden, layers, state, out, B, ws, as_stream(stream)),
                "hf_pinn_forward");
@@ -530,7 +539,9 @@ int hf_pinn_run(const float *params, int dim, int hidden, int layers, const floa
   if (int rc = pinn_args("hf_pinn_run", dim, hidden, layers, B)) return rc;
   if (T < 0) return fail(HF_EINVAL, "hf_pinn_run: T < 0");
   if (B == 0) return HF_OK;
-  if (!params || !state0 || !final_state || !ws) return fail(HF_EINVAL, "hf_pinn_run: NULL pointer");
+  if (!params || !state0 || !final_state) return fail(HF_EINVAL, "hf_pinn_run: NULL pointer");
+  if (!ws && T > 0 && hf::pinn_run_ws_bytes(dim, hidden, B) > 0)
+    return fail(HF_EINVAL, "hf_pinn_run: NULL workspace (hf_pinn_workspace_bytes > 0 for this shape)");
   HF_CHECK_HIP(hf::launch_pinn_run(params, dim, hidden, layers, state0, final_state, B, T, traj, ws,
                                    as_stream(stream)),
                "hf_pinn_run");

@@ -48,6 +48,7 @@ SIGNATURES = {
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hf_pure_gnn_param_count": (c_int64, [c_int, c_int, c_int]),
     "hf_pure_gnn_workspace_bytes": (c_int64, [c_int, c_int64, c_int64]),
+    "hf_pure_gnn_run_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int]),
     "hf_pure_gnn_forward": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int,
                                     c_void_p, c_void_p, c_void_p]),
     "hf_pure_gnn_run": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,

@@ -78,12 +78,13 @@ class PureGNN(nn.Module):
         final = torch.empty_like(s0)
         tr = torch.empty(B, n_steps + 1, 3, nx, device=s0.device) if traj else None
         N = B * nx
-        ws = torch.empty(int(lib().hf_pure_gnn_workspace_bytes(self.hidden_dim, N, 2 * N)), dtype=torch.uint8,
-                         device=s0.device)
+        nb = int(lib().hf_pure_gnn_run_workspace_bytes(self.hidden_dim, B, nx, int(n_steps)))
+        ws = torch.empty(nb, dtype=torch.uint8, device=s0.device) if nb > 0 else None
         with torch.no_grad(), torch.cuda.device(s0.device):
             check(lib().hf_pure_gnn_run(ptr(self._flat.get(self, s0.device)), self.hidden_dim, self.num_layers,
                                         ptr(s0), ptr(final), ptr(xd), B, nx, int(n_steps),
-                                        ptr(tr) if tr is not None else None, ptr(ws), engine.stream_of(s0.device)))
+                                        ptr(tr) if tr is not None else None, ptr(ws) if ws is not None else None,
+                                        engine.stream_of(s0.device)))
         return {"final": final, "traj": tr}
 
 
@@ -108,11 +109,11 @@ class PINN(nn.Module):
         flat = s.reshape(-1, self.input_dim)
         out = torch.empty_like(flat)
         B = flat.shape[0]
-        ws = torch.empty(int(lib().hf_pinn_workspace_bytes(self.input_dim, self.hidden_dim, B)), dtype=torch.uint8,
-                         device=s.device)
+        nb = int(lib().hf_pinn_workspace_bytes(self.input_dim, self.hidden_dim, B))
+        ws = torch.empty(nb, dtype=torch.uint8, device=s.device) if nb > 0 else None
         with torch.cuda.device(s.device):
             check(lib().hf_pinn_forward(ptr(self._flat.get(self, s.device)), self.input_dim, self.hidden_dim,
-                                        self.num_layers, ptr(flat), ptr(out), B, ptr(ws),
+                                        self.num_layers, ptr(flat), ptr(out), B, ptr(ws) if ws is not None else None,
                                         engine.stream_of(s.device)))
         return out.reshape(state.shape)
 
@@ -125,10 +126,11 @@ class PINN(nn.Module):
             raise ValueError(f"states0 must hold {self.input_dim} values per IC")
         final = torch.empty_like(s0)
         tr = torch.empty((B, n_steps + 1) + tuple(s0.shape[1:]), device=s0.device) if traj else None
-        ws = torch.empty(int(lib().hf_pinn_workspace_bytes(self.input_dim, self.hidden_dim, B)), dtype=torch.uint8,
-                         device=s0.device)
+        nb = int(lib().hf_pinn_workspace_bytes(self.input_dim, self.hidden_dim, B))
+        ws = torch.empty(nb, dtype=torch.uint8, device=s0.device) if nb > 0 else None
         with torch.no_grad(), torch.cuda.device(s0.device):
             check(lib().hf_pinn_run(ptr(self._flat.get(self, s0.device)), self.input_dim, self.hidden_dim,
                                     self.num_layers, ptr(s0), ptr(final), B, int(n_steps),
-                                    ptr(tr) if tr is not None else None, ptr(ws), engine.stream_of(s0.device)))
+                                    ptr(tr) if tr is not None else None, ptr(ws) if ws is not None else None,
+                                    engine.stream_of(s0.device)))
         return {"final": final, "traj": tr}

@@ -185,3 +185,20 @@ def test_workspace_need_classical():
     assert L.hf_workspace_need(None, HF_OP_RUN, 7, 100, 0, 0) == 0          # T = 0 copies only
     for op in (HF_OP_STEP, HF_OP_RUN, HF_OP_COMPARE):                         # the bound covers the exact need
         assert L.hf_run_workspace_bytes(op, 7, 100, 3) >= max(L.hf_workspace_need(None, op, 7, 100, 3, 0), 0)
+
+
+def test_baseline_rollout_workspace_queries():
+    """hf_pure_gnn_run_workspace_bytes / hf_pinn_workspace_bytes: 0 on the
+    one-launch rollouts (the workspace may then be NULL), the per-step GEMMs'
+    scratch otherwise, -1 on bad arguments (no GPU needed)."""
+    from hybridflux._lib import lib
+    L = lib()
+    for H, nx in ((64, 16), (128, 64), (64, 48)):
+        assert L.hf_pure_gnn_run_workspace_bytes(H, 4096, nx, 50) == 0
+    assert L.hf_pure_gnn_run_workspace_bytes(128, 7, 100, 5) == L.hf_pure_gnn_workspace_bytes(128, 700, 1400) > 0
+    assert L.hf_pure_gnn_run_workspace_bytes(96, 7, 64, 5) > 0      # H not in {64, 128}: per-step path
+    assert L.hf_pure_gnn_run_workspace_bytes(128, 7, 100, 0) == 0   # T = 0 only copies
+    assert L.hf_pure_gnn_run_workspace_bytes(0, 7, 64, 5) == -1
+    assert L.hf_pinn_workspace_bytes(192, 256, 4096) == 0
+    assert L.hf_pinn_workspace_bytes(96, 128, 7) > 0
+    assert L.hf_pinn_workspace_bytes(0, 128, 7) == -1
