@@ -19,7 +19,16 @@ namespace tg {
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16 __attribute__((ext_vector_type(16)));
 
-constexpr int kBM = 128, kBN = 128, kKC = 32;
+#ifndef HF_TG_KC
+#define HF_TG_KC 32
+#endif
+#ifndef HF_TG_WG
+#define HF_TG_WG 2
+#endif
+constexpr int kBM = 128, kBN = 128, kKC = HF_TG_KC;  // reduction chunk per stage (32; 16: a build knob)
+constexpr int kNQ = kBM * kKC / 4 / 256;             // float4 per thread per operand per stage
+constexpr int kIMSh = kKC == 32 ? 3 : 2;             // log2(float4 per [i][r] row)
+static_assert(kKC == 32 || kKC == 16, "stage depth");
 constexpr int kStrIM = kKC + 4;   // [i][r] tile rows: 36 floats (conflict-free b128 reads of 16 lanes)
 constexpr int kStrRM = kBM + 8;   // [r][i] tile rows: 136 floats (the two lane halves 4 rows apart land on disjoint banks)
 constexpr int kTileF = (kBM * kStrIM > kKC * kStrRM) ? kBM * kStrIM : kKC * kStrRM;
@@ -217,10 +226,12 @@ struct EpiMsg {
 // COLSUM (ARM A only): the split's column sums of GA over its rows (the bias
 // gradient), written to bias_part[split][i] by the blocks of column tile 0.
 template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM>
-__global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, int64_t I, int64_t J, int64_t R,
+__global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi epi, int64_t I, int64_t J, int64_t R,
                                                        int64_t rsplit, float *bias_part) {
-  __shared__ float sA[2][kTileF];
-  __shared__ float sB[2][kTileF];
+  // (a block epilogue parks a 128 x 65 tile in each operand's two buffers)
+  constexpr int kBufF = (Epi::kBlock && 2 * kTileF < kBM * 65) ? (kBM * 65 + 1) / 2 : kTileF;
+  __shared__ float sA[2][kBufF];
+  __shared__ float sB[2][kBufF];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wi = wave >> 1, wj = wave & 1, h = lane >> 5;
   const int64_t i0 = (int64_t)blockIdx.x * kBM, j0 = (int64_t)blockIdx.y * kBN;
   const int64_t rb = (int64_t)blockIdx.z * rsplit;
@@ -240,48 +251,48 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
 #endif
   constexpr int kDepth = HF_TG_DEPTH;  // stages of loads in flight: 1 (double buffer) and 2 measured equal
   // (profiles/r03_train_gemm_depth_ab.txt); 1 holds ~30 fewer registers
-  f4 ra[kDepth][4], rbv[kDepth][4], csum = f4{0.f, 0.f, 0.f, 0.f};
+  f4 ra[kDepth][kNQ], rbv[kDepth][kNQ], csum = f4{0.f, 0.f, 0.f, 0.f};
   // thread -> (global row, col) of its 4 float4 per operand per stage.  The
   // rows of an [i][r] operand are the same every stage: their handles are made once.
-  typename LA::Row rowa[4];
-  typename LB::Row rowb[4];
+  typename LA::Row rowa[kNQ];
+  typename LB::Row rowb[kNQ];
   if (!ARM) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) rowa[q] = ga.row(i0 + ((t + 256 * q) >> 3));
+    for (int q = 0; q < kNQ; ++q) rowa[q] = ga.row(i0 + ((t + 256 * q) >> kIMSh));
   }
   if (!BRM) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) rowb[q] = gb.row(j0 + ((t + 256 * q) >> 3));
+    for (int q = 0; q < kNQ; ++q) rowb[q] = gb.row(j0 + ((t + 256 * q) >> kIMSh));
   }
   // Branch-free loads: addresses clamped by the views; only reduction rows
   // past the split's end (RM operands) are zeroed, by select.  [i][r]
   // operands need R % kKC == 0 (host-checked), so their r never runs past re.
   auto gload = [&](int set, int64_t r0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kNQ; ++q) {
       const int idx = t + 256 * q;
       if (ARM) {
         const f4 v = ga.load4(ga.row(r0 + (idx >> 5)), (int)(i0 + 4 * (idx & 31)));
         const bool in = r0 + (idx >> 5) < re;
         ra[set][q] = f4{in ? v[0] : 0.f, in ? v[1] : 0.f, in ? v[2] : 0.f, in ? v[3] : 0.f};
       } else {
-        ra[set][q] = ga.load4(rowa[q], (int)(r0 + 4 * (idx & 7)));
+        ra[set][q] = ga.load4(rowa[q], (int)(r0 + 4 * (idx & ((1 << kIMSh) - 1))));
       }
       if (BRM) {
         const f4 v = gb.load4(gb.row(r0 + (idx >> 5)), (int)(j0 + 4 * (idx & 31)));
         const bool in = r0 + (idx >> 5) < re;
         rbv[set][q] = f4{in ? v[0] : 0.f, in ? v[1] : 0.f, in ? v[2] : 0.f, in ? v[3] : 0.f};
       } else {
-        rbv[set][q] = gb.load4(rowb[q], (int)(r0 + 4 * (idx & 7)));
+        rbv[set][q] = gb.load4(rowb[q], (int)(r0 + 4 * (idx & ((1 << kIMSh) - 1))));
       }
     }
   };
   auto lstore = [&](int buf, int set) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int idx = t + 256 * q;
-      float *pa = ARM ? &sA[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sA[buf][(idx >> 3) * kStrIM + 4 * (idx & 7)];
-      float *pb = BRM ? &sB[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sB[buf][(idx >> 3) * kStrIM + 4 * (idx & 7)];
+    for (int q = 0; q < kNQ; ++q) {
+      const int idx = t + 256 * q, im = (1 << kIMSh) - 1;
+      float *pa = ARM ? &sA[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sA[buf][(idx >> kIMSh) * kStrIM + 4 * (idx & im)];
+      float *pb = BRM ? &sB[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sB[buf][(idx >> kIMSh) * kStrIM + 4 * (idx & im)];
       *reinterpret_cast<f4 *>(pa) = ra[set][q];
       *reinterpret_cast<f4 *>(pb) = rbv[set][q];
       if (COLSUM) csum += ra[set][q];
@@ -344,7 +355,7 @@ __global__ __launch_bounds__(256, 2) void tgemm_kernel(LA ga, LB gb, Epi epi, in
     r0 += kKC;
   }
   if constexpr (Epi::kBlock) {
-    static_assert(kBM * EpiMsg::kS <= 2 * kTileF, "a parked P or Q tile fits one operand's two buffers");
+    static_assert(kBM * EpiMsg::kS <= 2 * kBufF, "a parked P or Q tile fits one operand's two buffers");
     epi.block(acc, sA[0], sB[0], i0, j0, I, wi, wj, lane, t);
     return;
   }
