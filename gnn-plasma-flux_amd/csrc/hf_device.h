@@ -252,18 +252,23 @@ __device__ __forceinline__ void poisson_wave(double2 (&v)[N / 64], double2 *lds,
 }
 
 // Per-state rollout metrics, partial sums for one cell.
+// The finite flag is not tested per value: every value a lane adds is finite
+// exactly when its double sums are (a finite float term is bounded, |n| <
+// 2^128 and u^2 + E^2 < 2^257, so no nx overflows them; a NaN or +-Inf value
+// makes its sum NaN or +-Inf, and +Inf + -Inf is NaN), so settle() derives it
+// from the sums before they are combined.  Same flag, bit for bit, as a
+// per-value isfinite test, without its compare and select per value.
 struct MetricAcc {
   double energy;  // sum u^2 + E^2
   double charge;  // sum n
   float maxdev;   // max |n - 1|
-  int finite;     // 1 while every value is finite
+  int finite;     // 1 while every value is finite (settled from the sums)
   __device__ void init() { energy = 0; charge = 0; maxdev = 0.f; finite = 1; }
   __device__ void add(float n, float u, float E) {
     energy += (double)u * u + (double)E * E;
     charge += n;
     float dv = fabsf(n - 1.0f);
     maxdev = dv > maxdev ? dv : maxdev;
-    finite &= (isfinite(n) && isfinite(u) && isfinite(E)) ? 1 : 0;
   }
   // the same sums split in two: n, u when the update produces them, E after the solve
   __device__ void add_nu(float n, float u) {
@@ -271,13 +276,11 @@ struct MetricAcc {
     charge += n;
     float dv = fabsf(n - 1.0f);
     maxdev = dv > maxdev ? dv : maxdev;
-    finite &= (isfinite(n) && isfinite(u)) ? 1 : 0;
   }
-  __device__ void add_E(float E) {
-    energy += (double)E * E;
-    finite &= isfinite(E) ? 1 : 0;
-  }
+  __device__ void add_E(float E) { energy += (double)E * E; }
+  __device__ void settle() { finite &= (isfinite(energy) && isfinite(charge)) ? 1 : 0; }
   __device__ void wave_reduce() {
+    settle();
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       energy += __shfl_xor(energy, o, 64);
@@ -288,10 +291,11 @@ struct MetricAcc {
     }
   }
   __device__ void store(float *dst, int nx) const {
+    const bool fin = finite && isfinite(energy) && isfinite(charge);
     dst[0] = (float)(0.5 * energy / nx);
     dst[1] = (float)(charge / nx);
-    dst[2] = finite ? 1.f : 0.f;
-    dst[3] = finite ? maxdev : __int_as_float(0x7fc00000);
+    dst[2] = fin ? 1.f : 0.f;
+    dst[3] = fin ? maxdev : __int_as_float(0x7fc00000);
   }
 };
 
