@@ -275,7 +275,7 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 2048 ? 1 : 2) void fv_step_fft
     float *__restrict__ flux_out, int64_t ld_flux, float *__restrict__ metrics, int64_t ld_metrics, int B) {
   constexpr int V = N / 64;
   __shared__ double2 s_fft[kFftWaves][fft_lds_elems<N>()];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform: scalar IC indices and bases
   const int64_t a = 2 * ((int64_t)blockIdx.x * kFftWaves + wave), b = a + 1;
   if (a >= B) return;  // a whole wave; nothing below synchronises the workgroup
   const bool two = b < B;
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_
   __shared__ double2 s_plan[N];
   for (int i = threadIdx.x; i < 2 * N; i += 64 * kFftWaves) reinterpret_cast<double *>(s_plan)[i] = pc[N + i];
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform: scalar IC indices and bases
   const int64_t a = 2 * ((int64_t)blockIdx.x * kFftWaves + wave), b = a + 1;
   if (a >= B) return;  // a whole wave; nothing below synchronises the workgroup
   const bool two = b < B;
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 2048 ? 1 : 2) void poisson_fft
                                                                      const double *__restrict__ pc, int B) {
   constexpr int V = N / 64;
   __shared__ double2 s_fft[kFftWaves][fft_lds_elems<N>()];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform: scalar IC indices and bases
   const int64_t b0 = 2 * ((int64_t)blockIdx.x * kFftWaves + wave);
   if (b0 >= B) return;
   const bool two = b0 + 1 < B;
