@@ -513,7 +513,7 @@ __global__ __launch_bounds__(kFvThreads) void fv_run_small_kernel(const float *s
   __shared__ float s_rho[kFvThreads / 64][kFvSmallMaxNx];
   for (int i = threadIdx.x; i < nx; i += kFvThreads) s_c[i] = pc[i];
   __syncthreads();
-  const int wave = threadIdx.x >> 6, i = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), i = threadIdx.x & 63;  // wave-uniform
   const int64_t b = (int64_t)blockIdx.x * (kFvThreads / 64) + wave;
   if (b >= B) return;  // a whole wave; nothing below synchronises the workgroup
   const int64_t S = 3LL * nx, ldT = (T + 1) * S, ldM = (int64_t)(T + 1) * HF_NUM_METRICS;
