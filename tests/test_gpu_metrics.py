@@ -148,3 +148,35 @@ def test_traj_metrics_vs_oracle(hf):
     np.testing.assert_allclose(got[..., 0], e, rtol=1e-7)
     np.testing.assert_allclose(got[..., 1], q, rtol=1e-7)
     assert (got[..., 2] == 1).all()
+
+
+def test_metric_finite_flag_edge_values(hf):
+    """The metric series' finite flag and max|n - 1| (hf_traj_metrics; the
+    flag is settled from the float64 energy / charge sums, hf_device.h
+    MetricAcc) on states holding NaN, +Inf, -Inf, +Inf beside -Inf in one
+    channel (charge NaN), and the largest finite floats (sums that must stay
+    finite), against np.isfinite(state).all() and the float32 max|n - 1|
+    (NaN where the state is not finite), as evaluate_long_rollout.py:53-66
+    tests finiteness."""
+    from hybridflux import engine
+    B, nx = 8, 64
+    rng = np.random.default_rng(7)
+    st = (1 + 0.1 * rng.standard_normal((B, 2, 3, nx))).astype(np.float32)
+    big = np.float32(3.4e38)
+    st[0, 1, 0, 5] = np.nan
+    st[1, 1, 1, 7] = np.inf
+    st[2, 1, 2, 9] = -np.inf
+    st[3, 1, 0, 3], st[3, 1, 0, 40] = np.inf, -np.inf
+    st[4, 1, 1, :], st[4, 1, 2, :] = big, -big
+    st[5, 1, 0, :] = big
+    st[6, 1, 1, 11], st[6, 1, 0, 12] = np.nan, np.inf
+    got = engine.traj_metrics(torch.as_tensor(st, device=DEV)).cpu().numpy()
+    fin = np.isfinite(st).all(axis=(2, 3))
+    assert (got[:, :, 2] == fin.astype(np.float32)).all(), (got[:, :, 2], fin)
+    dev = np.abs(st[:, :, 0, :] - np.float32(1)).max(axis=2)
+    for b in range(B):
+        for t in range(2):
+            if fin[b, t]:
+                assert got[b, t, 3] == dev[b, t], (b, t, got[b, t, 3], dev[b, t])
+            else:
+                assert np.isnan(got[b, t, 3]), (b, t, got[b, t, 3])
