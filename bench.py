@@ -8,7 +8,11 @@ the reference IC generator (seeds 1000 + global IC index).  A step is one full
 hybrid timestep of the whole batch: GNN -> flux symmetrisation -> FV
 continuity + Burgers -> spectral Poisson; the rollout records every state
 (as HybridSolver.run does).  N GPUs: weak scaling, 4096 ICs per rank, no
-communication while stepping, one RCCL all_gather of per-IC metrics.
+communication while stepping, one RCCL all_gather of per-IC metrics inside the
+timed region — at N = 1 too (a one-rank RCCL group); the line reports the
+calls and bytes that exchange actually moved.  The timed rollout's first 16
+ICs are checked against the reference's committed trajectories ("parity"),
+and a library built with diagnostic flags is refused.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--ics-per-gpu B] [--no-cpu-baseline]
 """
@@ -139,21 +143,73 @@ def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=Non
     return out
 
 
-def pmc_traffic(K, B, nx, traj):
+def pmc_traffic(K, B, nx, traj, build):
     """HBM bytes per launch of the headline kernel from the committed PMC passes
     (tools/gpu_pmc_traffic.sh + tools/pmc_traffic.py): FETCH_SIZE / WRITE_SIZE at two
     step counts give a fixed part and a per-step part, so the figure applies to
-    any --steps of the same workload."""
+    any --steps of the same workload.  The record names the src: hash of the
+    library it was measured on; for any other build the figure is not this
+    binary's, and the traffic is reported as null with the reason."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no profiles/pmc_traffic.json"
     if (t.get("ics_per_gpu"), t.get("nx"), t.get("traj")) != (B, nx, traj) or "per_step_bytes" not in t:
-        return None
+        return None, "profiles/pmc_traffic.json is for another workload"
+    if t.get("build") != build:
+        return None, f"stale: profiles/pmc_traffic.json was measured on src:{t.get('build')}, this is src:{build}"
     return {"traffic_bytes": t["fixed_bytes"] + t["per_step_bytes"] * K, "source": t["source"],
-            "fixed_bytes": t["fixed_bytes"], "per_step_bytes": t["per_step_bytes"]}
+            "fixed_bytes": t["fixed_bytes"], "per_step_bytes": t["per_step_bytes"], "build": t["build"]}, None
+
+
+def headline_parity(traj_buf, nx, K, weights_path, precision):
+    """Self-check of the timed rollout: the first 16 ICs of rank 0 are seeds
+    1000..1015, whose reference trajectories (src/hybrid_solver.py:66-73, run on
+    the CPU by tests/golden/make_golden.py) are committed for the default
+    weights; the recorded states 0..min(K, 30) must match them within the
+    parity tests' rollout gate |gpu - ref| <= 2e-6 + 2e-6 |ref|
+    (tests/test_gpu_parity.py ROLL_ATOL / ROLL_RTOL).  None when the timed run
+    is not that workload (other weights / nx / precision, or no trajectory)."""
+    default_w = os.path.join(ROOT, "tests", "golden", "weights_W1_r3.npz")
+    if traj_buf is None or nx != 64 or precision != "f32" or traj_buf.shape[0] < 16 \
+            or os.path.abspath(weights_path) != default_w:
+        return None
+    ref = np.load(os.path.join(ROOT, "tests", "golden", "hybrid_W1_r3_nx64.npz"))
+    assert list(ref["seeds"]) == list(range(1000, 1016))
+    k = min(K, ref["states"].shape[1] - 1)
+    want = ref["states"][:, :k + 1].astype(np.float64)
+    got = traj_buf[:16, :k + 1].cpu().numpy().astype(np.float64)
+    err = np.abs(got - want)
+    excess = float((err - (2e-6 + 2e-6 * np.abs(want))).max())
+    return {"max_err_vs_reference_f32": float(err.max()), "ics": 16, "steps_checked": k,
+            "gate": "|gpu - ref| <= 2e-6 + 2e-6*|ref| (tests/test_gpu_parity.py ROLL_ATOL/ROLL_RTOL)",
+            "within_gate": bool(excess <= 0.0 and np.isfinite(got).all()),
+            "reference": "tests/golden/hybrid_W1_r3_nx64.npz (seeds 1000..1015, reference CPU HybridSolver)"}
+
+
+def init_group(backend, world, dev):
+    """The process group of this job.  RCCL (backend nccl) gets a group at every
+    world size, one rank included, so the end-of-rollout metric exchange is a
+    real RCCL all_gather on the device even at N = 1 (a plain `python bench.py`
+    has no launcher env: it becomes rank 0 of 1 on a free local port).  gloo is
+    only for rehearsing N ranks and is not started at N = 1."""
+    if world == 1 and backend != "nccl":
+        return False
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", str(world))
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    return True
 
 
 def launch_ranks(n):
@@ -214,16 +270,15 @@ def main():
         raise SystemExit(f"LOCAL_RANK {local} but only {ndev} visible GPU(s); RCCL needs one GPU per rank")
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+    grouped = init_group(args.dist_backend, world, dev)
 
     from hybridflux import HybridSolver, engine
-    from hybridflux._lib import HF_OP_RUN, version
-    from hybridflux.rollout import gather_rollout, max_over_ranks, shard_seeds
+    from hybridflux._lib import HF_OP_RUN, build_hash, diagnostic_build, version
+    from hybridflux.rollout import COLLECTIVES, gather_rollout, max_over_ranks, reset_collective_stats, shard_seeds
+    if diagnostic_build():
+        # HF_DIAG_* / HF_EXP_* builds time deliberately broken or experimental
+        # kernels: never a headline (tools/diag_*.py measure those)
+        raise SystemExit(f"bench.py: refusing to benchmark a diagnostic build ({version()}); rebuild with make")
 
     weights = dict(np.load(args.weights, allow_pickle=False))
     B, nx, K, W = args.ics_per_gpu, args.nx, args.steps, args.warmup
@@ -255,9 +310,11 @@ def main():
     warm = solver.run_batch(ics, Wr, traj=warm_traj if warm_traj is not None else False, metrics=warm_met,
                             out=warm_final, ws=ws)
     gather_rollout(warm, n_total)
-    if world > 1:
+    ev_g = torch.cuda.Event(enable_timing=True)
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    reset_collective_stats()
     t0 = time.perf_counter()
     ev0.record(stream)
     res = solver.run_batch(ics, K, traj=traj_buf if traj_buf is not None else False, metrics=met_buf, out=final,
@@ -265,13 +322,19 @@ def main():
     ev1.record(stream)
     # per-IC summaries (first non-finite step, drifts) on the device,
     # then ONE exchange of the full metric series [B_rank, T+1, K] + summaries
+    # (a real all_gather whenever a group exists: RCCL at every N by default)
     gathered = gather_rollout(res, n_total)
+    ev_g.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if grouped:
         dist.barrier()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1)
-    gather_bytes = (gathered["metrics"].numel() + gathered["summary"].numel()) * 4
+    exchange_ms = ev1.elapsed_time(ev_g)
+    coll = dict(COLLECTIVES)
+    # the timed rollout's own states against the reference's (before anything
+    # below reuses traj_buf)
+    parity = headline_parity(traj_buf, nx, K, args.weights, args.precision) if rank == 0 else None
 
     # diagnostic only (not the value): the same K-step rollout once more, right
     # behind the timed one, i.e. at the clock the chip holds once it is warm;
@@ -343,12 +406,12 @@ def main():
                   other_config(w_r2, dev, "cfg4: 1024-cell chain, 4096-IC batch, r=2, bf16 MLP weights, dt=3.125e-4",
                                4096, 1024, "bf16", 30, 30, 2, fixture=fx)]
 
-    wall_max = max_over_ranks(wall, device=dev if args.dist_backend == "nccl" else "cpu")
+    wall_max = max_over_ranks(wall)
     finite = float(gathered["metrics"][:, -1, 2].float().mean().item())
     exploded = int((gathered["summary"][:, 0] >= 0).sum().item())
 
     if rank == 0:
-        traffic = pmc_traffic(K, B, nx, not args.no_traj)
+        traffic, traffic_why = pmc_traffic(K, B, nx, not args.no_traj, build_hash())
         value = n_total * K / wall_max
         flop = GNN_FLOP_PER_CELL_STEP * B * nx * K
         achieved = flop / (kernel_ms * 1e-3) / 1e12
@@ -388,12 +451,19 @@ def main():
             "config": {"workload": f"{'cfg3' if (nx == 64 and B == 4096) else 'cfg2' if (nx == 64 and B == 256) else 'cfg4' if nx == 1024 else 'custom'}: {nx}-cell periodic chain, {B}-IC batch per GPU, FluxGNN(4,128,4) {args.precision}, "
                                    f"{K}-step persistent rollout{'' if args.no_traj else ' recording every state'}",
                        "nx": nx, "dt": dt, "ics_per_gpu": B, "global_ics": n_total, "parallelism": f"ic-shard x{world}",
-                       "collective": f"{'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_gather of the per-IC "
-                                     f"metric series [B,T+1,4] + summaries [B,8] ({gather_bytes} B gathered)"},
+                       "collective": ({"op": "all_gather of the per-IC metric series [B,T+1,4] + summaries [B,8] "
+                                             "(inside the timed region)",
+                                       "backend": {"nccl": "nccl (RCCL)", "gloo": "gloo"}[coll["backend"]],
+                                       "world_size": world, "calls": coll["calls"],
+                                       "bytes_sent_per_rank": coll["bytes_sent"],
+                                       "bytes_received_per_rank": coll["bytes_received"],
+                                       "exchange_ms": round(exchange_ms, 4)}
+                                      if coll["calls"] else None)},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "traffic": traffic["traffic_bytes"] if traffic else None,
-                         "traffic_source": traffic["source"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else traffic_why,
+                         "traffic_build": traffic["build"] if traffic else None,
                          "traffic_model": ({"fixed_bytes": traffic["fixed_bytes"],
                                             "per_step_bytes": traffic["per_step_bytes"]} if traffic else None),
                          "algorithmic_bytes": (12 * B * nx * (K + 1) if not args.no_traj else 0)
@@ -404,6 +474,7 @@ def main():
                          "hbm_state_frac": round(STATE_BYTES_PER_CELL_STEP * B * nx * K / (kernel_ms * 1e-3)
                                                  / (PEAK_HBM_GBS * 1e9), 6)},
             "cpu_baseline": cpu,
+            "parity": parity,
             "finite_fraction": finite,
             "exploded_ics": exploded,
             "build": version(),
@@ -414,7 +485,7 @@ def main():
             "other_configs": others,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

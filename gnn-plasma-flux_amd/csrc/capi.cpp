@@ -235,9 +235,17 @@ extern "C" {
 #ifndef HF_SOURCE_HASH
 #define HF_SOURCE_HASH "unknown"
 #endif
+#ifndef HF_BUILD_FLAGS
+#define HF_BUILD_FLAGS ""
+#endif
 // "hybridflux <version> gfx950 src:<hash>": the hash covers every source,
-// header and the Makefile the library was built from (Makefile SRC_HASH).
-const char *hf_version(void) { return "hybridflux 0.2 gfx950 src:" HF_SOURCE_HASH; }
+// header and the Makefile the library was built from, and the extra compiler
+// flags (Makefile SRC_HASH).  A build with extra flags (HF_DIAG_* timing
+// diagnostics, HF_EXP_* experiments) says so: "... src:<hash> flags:<flags>".
+const char *hf_version(void) {
+  return sizeof(HF_BUILD_FLAGS) > 1 ? "hybridflux 0.2 gfx950 src:" HF_SOURCE_HASH " flags:" HF_BUILD_FLAGS
+                                    : "hybridflux 0.2 gfx950 src:" HF_SOURCE_HASH;
+}
 
 const char *hf_last_error(void) { return g_err.c_str(); }
 

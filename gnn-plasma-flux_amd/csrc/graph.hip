@@ -581,7 +581,7 @@ int64_t graph_backward_ws_bytes(const GraphW &w, int64_t N, int64_t E) {
 hipError_t launch_graph_forward_train(const GraphW &w, const float *nf, int64_t N, const int64_t *ei, int64_t E,
                                       int chain_nx, float *flux, void *tape, hipStream_t s) {
   if (E <= 0) return hipSuccess;  // no flux to compute; the backward returns zeros
-  if (chain_train_ok(w, chain_nx)) return launch_chain_forward_train(w, nf, N, chain_nx, flux, tape, s);
+  if (chain_train_ok(w, chain_nx, N)) return launch_chain_forward_train(w, nf, N, chain_nx, flux, tape, s);
   Tape t = carve_tape(w, N, E, tape);
   hipError_t err;
   if ((err = build_csr(ei, E, N, t.deg, t.off, t.cur, t.perm, s, chain_nx, false))) return err;
@@ -607,7 +607,7 @@ hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, co
     if (grad_nf && (err = hipMemsetAsync(grad_nf, 0, sizeof(float) * N * w.in_dim, s))) return err;
     return hipSuccess;
   }
-  if (chain_train_ok(w, chain_nx))
+  if (chain_train_ok(w, chain_nx, N))
     return launch_chain_backward(w, nf, N, chain_nx, tape, grad_flux, grad_params, grad_nf, ws, s);
   Carve c{static_cast<char *>(ws)};
   float *dz = c.take<float>(E * H);

@@ -202,8 +202,10 @@ hipError_t launch_graph_backward(const GraphW &w, const float *nf, int64_t N, co
                                  int chain_nx, const void *tape, const float *grad_flux, float *grad_params, float *grad_nf,
                                  void *ws, hipStream_t s);
 // Chain-specialised training path (train_chain.hip): tagged chain graphs
-// (chain_nx > 0) with hidden % 4 == 0, hidden <= 512, in_dim <= 8.
-bool chain_train_ok(const GraphW &w, int chain_nx);
+// (chain_nx > 0) with hidden a power of two in [32, 256], in_dim <= 8 and
+// N * 2 * hidden + 2 * hidden < 2^31; other graphs and widths take the
+// generic CSR path.
+bool chain_train_ok(const GraphW &w, int chain_nx, int64_t N);
 int64_t chain_tape_bytes(const GraphW &w, int64_t N);
 int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N);
 hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t N, int nx, float *flux, void *tape,

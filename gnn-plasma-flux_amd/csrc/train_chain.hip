@@ -302,7 +302,8 @@ __device__ __forceinline__ float block_sum256(float v, float *sh) {
 // sum (E' - E'_t)^2, sum (n - 1), sum (n' - 1), sum (u'_t^2 + E'^2),
 // sum (u'_t^2 + E'_t^2); and d loss / d flux_edge: with r = n' - n'_t and
 // N = B nx, dL/dF_i = 2 (F_i - F_t,i) / N + lam_s 2 c (r_{i+1} - r_i) / N
-// (the continuity update's adjoint), half of it to each edge of face i.
+// (the continuity update's adjoint; the second term only when lam_s > 0),
+// half of it to each edge of face i.
 __global__ __launch_bounds__(256) void loss_terms_kernel(const float *__restrict__ fe, const float *__restrict__ st,
                                                          const float *__restrict__ ft, const float *__restrict__ sn,
                                                          const float *__restrict__ nn, const float *__restrict__ En,
@@ -328,7 +329,11 @@ __global__ __launch_bounds__(256) void loss_terms_kernel(const float *__restrict
     s[4] = __fadd_rn(s[4], __fsub_rn(np[i], 1.0f));
     s[5] = __fadd_rn(s[5], __fadd_rn(__fmul_rn(ut[i], ut[i]), __fmul_rn(Ep[i], Ep[i])));
     s[6] = __fadd_rn(s[6], __fadd_rn(__fmul_rn(ut[i], ut[i]), __fmul_rn(Et[i], Et[i])));
-    const float g = __fadd_rn(__fmul_rn(inv, dF), __fmul_rn(lam_s, __fmul_rn(__fmul_rn(inv, c), __fsub_rn(rn, r))));
+    // the state term only where the loss has it (lam_s > 0, as loss_final_kernel
+    // and train_ablation.py:132 gate it): no 0 * NaN from a non-finite n'
+    const float g = lam_s > 0.f
+                        ? __fadd_rn(__fmul_rn(inv, dF), __fmul_rn(lam_s, __fmul_rn(__fmul_rn(inv, c), __fsub_rn(rn, r))))
+                        : __fmul_rn(inv, dF);
     const float h = __fmul_rn(0.5f, g);
     dfe[(int64_t)b * 2 * nx + i] = h;
     dfe[(int64_t)b * 2 * nx + nx + i] = h;
@@ -398,9 +403,16 @@ ChainTape carve_chain_tape(const GraphW &w, int64_t N, void *base) {
 
 }  // namespace
 
-bool chain_train_ok(const GraphW &w, int chain_nx) {
-  const int H = w.hidden;  // power of two in [4, 256] (split weight views, input-gradient lanes), in_dim <= 8
-  return chain_nx > 0 && H >= 4 && H <= 256 && (H & (H - 1)) == 0 && w.in_dim >= 1 && w.in_dim <= 8;
+bool chain_train_ok(const GraphW &w, int chain_nx, int64_t N) {
+  // hidden: a power of two in [32, 256] — power of two for the split weight
+  // views and the input-gradient lanes, >= kKC so that every [i][r] GEMM
+  // operand (reduction H in the P/Q readout, 2H in the layers) is whole kKC
+  // chunks (tgemm refuses a partial chunk); in_dim <= 8; and the largest
+  // activation view [N][2H] within tgemm's 32-bit row offsets.  Anything else
+  // takes the generic CSR path.
+  const int64_t H = w.hidden;
+  return chain_nx > 0 && H >= kKC && H <= 256 && (H & (H - 1)) == 0 && H % kKC == 0 && w.in_dim >= 1 &&
+         w.in_dim <= 8 && N > 0 && N * 2 * H + 2 * H < (int64_t(1) << 31);
 }
 
 int64_t chain_tape_bytes(const GraphW &w, int64_t N) {

@@ -111,13 +111,34 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 
 
 def version():
-    """hf_version() of the loaded library: "hybridflux <ver> gfx950 src:<hash>"."""
+    """hf_version() of the loaded library: "hybridflux <ver> gfx950 src:<hash>",
+    followed by " flags:<CXXFLAGS_EXTRA>" for a build with extra compiler flags."""
     return lib().hf_version().decode()
 
 
-def source_hash():
+def build_hash(v=None):
+    """The src:<hash> of hf_version() (of the loaded library when v is None)."""
+    v = version() if v is None else v
+    return v.split("src:")[-1].split(" flags:")[0]
+
+
+def build_flags(v=None):
+    """The extra compiler flags the loaded library was built with ('' = none)."""
+    v = version() if v is None else v
+    return v.split(" flags:", 1)[1] if " flags:" in v else ""
+
+
+def diagnostic_build(v=None):
+    """True when the library was built with an HF_DIAG_* timing diagnostic or an
+    HF_EXP_* experiment switch (or any other extra flag): its results are not
+    the shipped kernels' and no headline may be printed from it."""
+    return build_flags(v) != ""
+
+
+def source_hash(extra_flags=""):
     """The hash the Makefile embeds (SRC_HASH): sha256 prefix of SRCS, HDRS and the
-    Makefile, in that order, recomputed from the tree (None when the sources are absent)."""
+    Makefile, in that order, then the CXXFLAGS_EXTRA text, recomputed from the
+    tree (None when the sources are absent)."""
     import hashlib
     import re
     mk = os.path.join(CSRC, "Makefile")
@@ -131,6 +152,7 @@ def source_hash():
     for f in files + ["Makefile"]:
         with open(os.path.join(CSRC, f), "rb") as fh:
             h.update(fh.read())
+    h.update(extra_flags.encode())
     return h.hexdigest()[:16]
 
 

@@ -6,9 +6,12 @@ their checkpoints load with load_state_dict unchanged, and forward()
 signatures; inference runs in the HIP kernels of baselines.hip
 (hf_pure_gnn_* / hf_pinn_*).  `rollout` batches the per-IC loops of
 scripts/evaluation/evaluate_multi_ic.py:45-83 and benchmark_timing.py:100-203
-over B initial conditions in one call.  Inference only: these modules have no
-backward kernels (the reference trains them with its own torch loops), so a
-forward under autograd raises.
+over B initial conditions in one call.  forward() takes the reference's host
+(CPU) tensors too (evaluate_multi_ic.py:53-83 calls them with
+torch.FloatTensor states): they are staged to the current HIP device and the
+result is copied back.  Inference only: these modules have no backward
+kernels (the reference trains them with its own torch loops), so a forward
+under autograd raises.
 """
 import torch
 import torch.nn as nn
@@ -56,7 +59,9 @@ class PureGNN(nn.Module):
     def forward(self, node_features, edge_index):
         """node_features [N, input_dim], edge_index [2, E] -> delta_state [N, 3]."""
         _no_grad_guard(self, node_features)
-        nf, ei, N, E, chain_nx = engine._graph_inputs(node_features, edge_index, self.input_dim)
+        home = node_features.device
+        dev = engine.compute_device(node_features, "node_features")
+        nf, ei, N, E, chain_nx = engine._graph_inputs(node_features.to(dev), edge_index, self.input_dim)
         delta = torch.empty(N, 3, device=nf.device)
         H = self.hidden_dim
         ws = torch.empty(int(lib().hf_pure_gnn_workspace_bytes(H, N, E)), dtype=torch.uint8, device=nf.device)
@@ -64,7 +69,7 @@ class PureGNN(nn.Module):
             check(lib().hf_pure_gnn_forward(ptr(self._flat.get(self, nf.device)), self.input_dim, H,
                                             self.num_layers, ptr(nf), N, ptr(ei), E, chain_nx, ptr(delta), ptr(ws),
                                             engine.stream_of(nf.device)))
-        return delta
+        return delta.to(home)
 
     def rollout(self, states0, n_steps, x, traj=True):
         """B ICs [B,3,nx] (device) -> dict(final [B,3,nx], traj [B,T+1,3,nx] or None);
@@ -104,8 +109,8 @@ class PINN(nn.Module):
     def forward(self, state):
         """state [..., 3, nx] -> state + delta, same shape."""
         _no_grad_guard(self, state)
-        engine.require_device(state, "state")
-        s = state.to(torch.float32).contiguous()
+        dev = engine.compute_device(state, "state")
+        s = state.to(device=dev, dtype=torch.float32).contiguous()
         flat = s.reshape(-1, self.input_dim)
         out = torch.empty_like(flat)
         B = flat.shape[0]
@@ -115,7 +120,7 @@ class PINN(nn.Module):
             check(lib().hf_pinn_forward(ptr(self._flat.get(self, s.device)), self.input_dim, self.hidden_dim,
                                         self.num_layers, ptr(flat), ptr(out), B, ptr(ws) if ws is not None else None,
                                         engine.stream_of(s.device)))
-        return out.reshape(state.shape)
+        return out.reshape(state.shape).to(state.device)
 
     def rollout(self, states0, n_steps, traj=True):
         """B ICs [B,3,nx] -> dict(final, traj [B,T+1,3,nx] or None) (evaluate_multi_ic.py:75-81)."""

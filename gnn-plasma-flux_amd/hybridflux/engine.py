@@ -28,6 +28,22 @@ def require_device(t, what="tensor"):
     return t
 
 
+def compute_device(t, what="tensor"):
+    """The HIP device a drop-in call computes on: t's own device when t is a
+    device tensor; for a host tensor (the reference's CPU call pattern,
+    examples/smoke_test.py:50-56) the current HIP device, to which the
+    caller's inputs are staged and from which results are copied back.  No HIP
+    device visible: raises (the kernels are the only implementation)."""
+    if isinstance(t, torch.Tensor) and t.is_cuda:
+        return t.device
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"hybridflux: {what} must be a torch tensor, got {type(t).__name__}")
+    if not torch.cuda.is_available():
+        raise RuntimeError(f"hybridflux: {what} is a host tensor and no HIP device is visible; this engine has "
+                           "no CPU path (host tensors are staged to the current HIP device, and there is none)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
 def stream_of(device):
     return c_void_p(torch.cuda.current_stream(device).cuda_stream)
 

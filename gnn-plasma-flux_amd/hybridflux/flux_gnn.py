@@ -5,18 +5,27 @@ The nn.Module layout (input_mlp / update_mlps / edge_mlp Sequentials) is kept
 so reference checkpoints load with `load_state_dict` unchanged.  forward()
 never runs these Linear layers itself: the parameters are packed (once per
 change) into a device weight handle and the edge fluxes come from
-  * the fused chain kernel (chain_gnn.hip) when edge_index is a periodic chain
-    — tagged by graph_constructor, or recognised by content — and the model
-    has MODEL_CONFIG's width (in 4, hidden 128);
+  * the fused chain kernel (hf_chain_flux: chain_f32.hip / chain_k32.hip /
+    chain_bf16.hip) when edge_index is a periodic chain — tagged by
+    graph_constructor, or recognised by content — and the model has
+    MODEL_CONFIG's width (in 4, hidden 128);
   * the generic-graph kernels (graph.hip) for any other edge_index
     (examples/smoke_test.py:53 passes a random one) or width.
-There is no CPU path: CPU inputs raise.
+
+Host (CPU) tensors and a CPU-resident module — the reference's own call
+pattern (examples/smoke_test.py:50-56, src/flux_gnn.py:40-67: the flux comes
+back on the caller's device) — are staged to the current HIP device, computed
+by the same kernels and copied back; gradients land on the parameters' and the
+node features' own devices.  There is no CPU compute path: with no HIP device
+visible a call raises.
 
 Under autograd (grad enabled and a parameter or the node features requiring
-grad) forward() runs the generic-graph training kernels instead: the forward
-keeps an activation tape on the device and backward() runs the HIP backward
-kernels (hf_graph_backward), so `loss.backward()` in the reference trainer
-(scripts/training/train_ablation.py:203-205) works unchanged.
+grad) forward() runs the training kernels instead: the forward keeps an
+activation tape on the device and backward() runs the HIP backward kernels
+(hf_graph_backward: the chain-layout MFMA GEMMs of train_chain.hip on tagged
+chains, the generic-graph kernels of graph.hip otherwise), so `loss.backward()`
+in the reference trainer (scripts/training/train_ablation.py:203-205) works
+unchanged.
 """
 import torch
 import torch.nn as nn
@@ -30,14 +39,17 @@ class _TrainForward(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, node_features, edge_index, dims, *params):
-        flat = torch.cat([q.detach().reshape(-1).to(torch.float32) for q in params])
-        flux, tape, nf, ei, chain_nx = engine.graph_forward_train(flat, dims, node_features, edge_index)
+        dev = engine.compute_device(node_features, "node_features")
+        flat = torch.cat([q.detach().reshape(-1).to(device=dev, dtype=torch.float32) for q in params])
+        flux, tape, nf, ei, chain_nx = engine.graph_forward_train(flat, dims, node_features.detach().to(dev),
+                                                                  edge_index)
         ctx.save_for_backward(flat, tape, nf, ei)
         ctx.dims = dims
         ctx.chain_nx = chain_nx
         ctx.shapes = [q.shape for q in params]
-        ctx.nf_dtype = node_features.dtype
-        return flux
+        ctx.param_devices = [q.device for q in params]
+        ctx.nf_dtype, ctx.nf_device = node_features.dtype, node_features.device
+        return flux.to(node_features.device)
 
     @staticmethod
     @torch.autograd.function.once_differentiable
@@ -50,9 +62,10 @@ class _TrainForward(torch.autograd.Function):
             n = 1
             for d in shp:
                 n *= d
-            grads.append(gp[o:o + n].view(shp))
+            grads.append(gp[o:o + n].view(shp).to(ctx.param_devices[len(grads)]))
             o += n
-        return (gnf.to(ctx.nf_dtype) if gnf is not None else None, None, None, *grads)
+        gnf = gnf.to(device=ctx.nf_device, dtype=ctx.nf_dtype) if gnf is not None else None
+        return (gnf, None, None, *grads)
 
 
 class FluxGNN(nn.Module):
@@ -111,16 +124,19 @@ class FluxGNN(nn.Module):
         return None
 
     def forward(self, node_features, edge_index):
-        """node_features [N, input_dim] float32, edge_index [2, E] int64 -> flux [E]."""
-        engine.require_device(node_features, "node_features")
+        """node_features [N, input_dim] float32, edge_index [2, E] int64 -> flux [E]
+        on node_features' device (host inputs are computed on the current HIP
+        device and the flux copied back)."""
+        dev = engine.compute_device(node_features, "node_features")
         params = list(self.parameters())
         if torch.is_grad_enabled() and (node_features.requires_grad or any(q.requires_grad for q in params)):
             dims = (self.input_dim, self.hidden_dim, self.num_layers)
             return _TrainForward.apply(node_features, edge_index, dims, *params)
-        dm = self.device_model(node_features.device)
+        dm = self.device_model(dev)
         geom = self._chain_geometry(node_features, edge_index)
+        nf = node_features.to(device=dev, dtype=torch.float32)
         if geom is not None and dm.chain_ok:
-            flux = engine.chain_flux(dm, node_features.to(torch.float32), geom[0], geom[1])
+            flux = engine.chain_flux(dm, nf, geom[0], geom[1])
         else:
-            flux = engine.graph_flux(dm, node_features, edge_index)
-        return flux
+            flux = engine.graph_flux(dm, nf, edge_index)
+        return flux.to(node_features.device)

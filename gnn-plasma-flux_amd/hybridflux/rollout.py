@@ -8,9 +8,30 @@ This is the reference's multi-IC evaluation loop
 time) turned into a data-parallel job: IC j of rank r is seed
 `seed0 + start(r) + j`, so the union over ranks is the same seed range at any
 world size.  A 64-cell chain never shards spatially (BASELINE.json north star).
+
+Whenever a process group is initialised the exchange is a real collective,
+world size 1 included (a one-rank RCCL group still runs the all_gather kernel
+on the device); without a group the local tensors are returned as they are.
+Every collective issued here is counted in `COLLECTIVES` (backend, calls, bytes
+each rank received), so a benchmark line reports the transfer that happened,
+not one computed from tensor shapes.
 """
 import torch
 import torch.distributed as dist
+
+# running tally of the collectives this module issued (reset_collective_stats)
+COLLECTIVES = {"backend": None, "calls": 0, "bytes_received": 0, "bytes_sent": 0}
+
+
+def reset_collective_stats():
+    COLLECTIVES.update(backend=None, calls=0, bytes_received=0, bytes_sent=0)
+
+
+def _count(backend, sent, received):
+    COLLECTIVES["backend"] = backend
+    COLLECTIVES["calls"] += 1
+    COLLECTIVES["bytes_sent"] += int(sent)
+    COLLECTIVES["bytes_received"] += int(received)
 
 
 def shard_bounds(n_total, world, rank):
@@ -28,33 +49,58 @@ def shard_seeds(seed0, n_total, world, rank):
 
 def gather_ic_rows(local, n_total, group=None):
     """all_gather a per-IC tensor [b_local, ...] into [n_total, ...] on every
-    rank (ragged shards are padded to the largest shard for the collective)."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if world == 1:
+    rank, in global IC order (ragged shards are padded to the largest shard for
+    the collective).  RCCL gathers device tensors in place into one contiguous
+    [world*cap, ...] buffer (all_gather_into_tensor); gloo moves host memory, so
+    device tensors are staged through the host for it.  No process group: the
+    local tensor itself."""
+    if not dist.is_initialized():
         return local
+    world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     counts = [shard_bounds(n_total, world, r)[1] - shard_bounds(n_total, world, r)[0] for r in range(world)]
     assert local.shape[0] == counts[rank], (local.shape, counts)
     cap = max(counts)
-    # gloo moves host memory: stage device tensors through the host for it
-    stage = local.is_cuda and dist.get_backend(group) == "gloo"
+    if cap == 0:
+        return local
+    backend = dist.get_backend(group)
+    stage = local.is_cuda and backend == "gloo"
     src = local.cpu() if stage else local
-    pad = src.new_zeros((cap,) + tuple(src.shape[1:]))
-    pad[: src.shape[0]] = src
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(bufs, pad.contiguous(), group=group)
-    out = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+    if src.shape[0] == cap:
+        pad = src.contiguous()
+    else:
+        pad = src.new_zeros((cap,) + tuple(src.shape[1:]))
+        pad[: src.shape[0]] = src
+    row_bytes = pad.numel() * pad.element_size()
+    if backend == "gloo":
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(bufs, pad, group=group)
+        out = torch.cat([b[:c] for b, c in zip(bufs, counts)], dim=0)
+    else:
+        flat = pad.new_empty((world * cap,) + tuple(pad.shape[1:]))
+        dist.all_gather_into_tensor(flat, pad, group=group)
+        if all(c == cap for c in counts):
+            out = flat
+        else:
+            out = torch.cat([flat[r * cap: r * cap + c] for r, c in enumerate(counts)], dim=0)
+    _count(backend, row_bytes, row_bytes * world)
     return out.to(local.device) if stage else out
 
 
-def max_over_ranks(value, group=None, device="cpu"):
+def max_over_ranks(value, group=None, device=None):
     """The job's wall time: the MAX of each rank's value (bench.py's timing rule:
-    the slowest shard ends the job).  float64 all_reduce on `device` (the
-    rank's GPU for RCCL, the CPU for gloo); the value itself when not distributed."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    the slowest shard ends the job).  A float64 all_reduce whenever a group is
+    initialised (world 1 included), on the rank's current HIP device for RCCL
+    and on the CPU for gloo unless `device` says otherwise; the value itself
+    when not distributed."""
+    if not dist.is_initialized():
         return float(value)
+    backend = dist.get_backend(group)
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if backend != "gloo" else "cpu"
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    _count(backend, 8, 8)
     return float(t.item())
 
 

@@ -144,7 +144,8 @@ int hf_graph_flux(hf_model_t model, const float *dev_node_features, int64_t N,
  * deterministic for a given N, E.  chain_nx > 0 declares that edge_index is
  * N/chain_nx disjoint periodic chains of chain_nx cells in build_chain_graph
  * order (src/graph_constructor.py:34-38, E == 2N): with hidden a power of two
- * in [4, 256] and in_dim <= 8 the chain training path runs (the aggregation as
+ * in [32, 256], in_dim <= 8 and N * 2 * hidden + 2 * hidden < 2^31 the chain
+ * training path runs (the aggregation as
  * a stencil inside the GEMM operand loads, the edge readout split into
  * per-node P/Q GEMMs, f32 MFMA GEMMs throughout); otherwise the edge buckets
  * are formed arithmetically instead of by the count/scan/fill CSR build.  0

@@ -1,7 +1,10 @@
 """One rank of the IC-sharded rollout on the HIP path (tests/test_gpu_distributed.py).
 
-Run as a plain process (one rank) or under torch.distributed.run (N ranks,
-backend gloo, every rank on cuda:0 of a one-GPU box).  Each rank takes its
+Run as a plain process (one rank, no process group) or under
+torch.distributed.run (N ranks, every rank on cuda:0 of a one-GPU box).  The
+backend is HF_DIST_BACKEND: gloo (default; any N on one GPU) or nccl = RCCL
+(one GPU per rank, so N = 1 here: a one-rank RCCL group whose all_gathers and
+all_reduce run on the device).  Each rank takes its
 contiguous shard of the seeds (hybridflux.rollout.shard_seeds), runs it through
 the real HybridSolver (run_batch and compare_batch), and the shard results are
 exchanged exactly as bench.py does at N > 1 (gather_rollout: device summary
@@ -37,12 +40,17 @@ def main(out):
     rank = int(os.environ.get("RANK", "0"))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("gloo")
+    backend = os.environ.get("HF_DIST_BACKEND", "gloo")
+    grouped = "WORLD_SIZE" in os.environ  # launched by torch.distributed.run
+    if grouped:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     from hybridflux import HybridSolver
-    from hybridflux.rollout import gather_ic_rows, gather_rollout, max_over_ranks, shard_seeds
+    from hybridflux.rollout import COLLECTIVES, gather_ic_rows, gather_rollout, max_over_ranks, shard_seeds
 
-    res = {"world": np.int64(world)}
+    res = {"world": np.int64(world), "grouped": np.int64(grouped)}
     for label, n_total, nx, T, prec, w in CASES:
         weights = dict(np.load(os.path.join(ROOT, "tests", "golden", f"weights_{w}.npz"), allow_pickle=False))
         solver = HybridSolver(weights, radius=2, nx=nx, dt=5e-3 * 64.0 / nx, device=dev, precision=prec)
@@ -60,9 +68,12 @@ def main(out):
         res[f"{label}/cmp_summary"] = gc["summary"].cpu().numpy()
         res[f"{label}/local_n"] = np.int64(ics.shape[0])
     res["max_over_ranks"] = np.float64(max_over_ranks(float(rank + 1)))
+    res["backend"] = np.array(dist.get_backend() if grouped else "none")
+    res["collective_calls"] = np.int64(COLLECTIVES["calls"])
+    res["collective_bytes_received"] = np.int64(COLLECTIVES["bytes_received"])
     if rank == 0:
         np.savez(out, **res)
-    if world > 1:
+    if grouped:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -44,6 +44,17 @@ baselines.npz         the reference's other rollout models
                       graph, and 10-step rollouts of ICs 1000..1003 with the
                       loops of scripts/evaluation/evaluate_multi_ic.py:45-83.
 
+smoke_test.npz        examples/smoke_test.py's own call sequence, verbatim, on the
+                      CPU: test_graph_constructor (:30-42, np.random.seed(s)
+                      first) and test_flux_gnn (:45-58: torch.manual_seed(s),
+                      FluxGNN(4,64,3) built on the CPU, grad enabled,
+                      torch.randn node features and a torch.randint
+                      edge_index) for s in 0, 1, 2 — the fluxes, and the
+                      gradients of sum(flux) w.r.t. the parameters; plus
+                      FluxGNN(4,128,4)=W1_r1 on build_chain_graph(IC 1000, x,
+                      'cpu') under grad (the trainer's call, train_ablation.py:
+                      119-124) with d sum(flux)/d params.
+
 metrics.npz           the reference's rollout scoring:
                       evaluate_all.compute_metrics (scripts/evaluation/
                       evaluate_all.py:118-159) of the hybrid W1_r1 rollouts of
@@ -62,6 +73,7 @@ metrics.npz           the reference's rollout scoring:
     python tests/golden/make_golden.py grads       # regenerate grads.npz only
     python tests/golden/make_golden.py baselines   # regenerate baselines.npz only
     python tests/golden/make_golden.py metrics     # regenerate metrics.npz only
+    python tests/golden/make_golden.py smoke       # regenerate smoke_test.npz only
 """
 import json
 import os
@@ -379,6 +391,41 @@ def make_baselines():
     save("baselines.npz", **arrs)
 
 
+SMOKE_SEEDS = (0, 1, 2)
+
+
+def make_smoke():
+    arrs = {}
+    for s in SMOKE_SEEDS:
+        np.random.seed(s)                                   # smoke_test.py:35-38
+        state = np.random.randn(3, 64)
+        x = np.linspace(0, 1, 64)
+        nf, ei = build_chain_graph(state, x, "cpu")
+        arrs[f"graph{s}_state"], arrs[f"graph{s}_nf"], arrs[f"graph{s}_ei"] = state, nf.numpy(), ei.numpy()
+        torch.manual_seed(s)                                # smoke_test.py:50-55, grad enabled
+        model = FluxGNN(input_dim=4, hidden_dim=64, num_layers=3)
+        node_features = torch.randn(64, 4)
+        edge_index = torch.randint(0, 64, (2, 128))
+        fluxes = model(node_features, edge_index)
+        fluxes.sum().backward()
+        arrs[f"flux{s}"] = fluxes.detach().numpy()
+        arrs[f"flux{s}_nf"], arrs[f"flux{s}_ei"] = node_features.numpy(), edge_index.numpy()
+        arrs.update({f"flux{s}_w.{k}": v for k, v in sd_to_np(model.state_dict()).items()})
+        arrs.update({f"flux{s}_grad.{k}": p.grad.numpy() for k, p in model.named_parameters()})
+    w1 = np.load(OUT / "weights_W1_r1.npz")
+    model = FluxGNN(input_dim=4, hidden_dim=128, num_layers=4)
+    model.load_state_dict({k: torch.from_numpy(w1[k]) for k in w1.files})
+    solver = BaselineSolver(nx=64)
+    st = solver.initial_condition(seed=1000)
+    nf, ei = build_chain_graph(st, solver.x, device="cpu")
+    fe = model(nf, ei)
+    fe.sum().backward()
+    arrs["chain_flux"] = fe.detach().numpy()
+    arrs.update({f"chain_grad.{k}": p.grad.numpy() for k, p in model.named_parameters()})
+    arrs["seeds"] = np.array(SMOKE_SEEDS)
+    save("smoke_test.npz", **arrs)
+
+
 LONG_ROLLOUTS = ((1.0, 300), (30.0, 100), (100.0, 60))  # (edge_mlp.2.weight scale, steps), seed 2000
 
 
@@ -429,6 +476,9 @@ def main():
     if sys.argv[1:] == ["metrics"]:
         make_metrics()
         return
+    if sys.argv[1:] == ["smoke"]:
+        make_smoke()
+        return
     if sys.argv[1:] == ["grads"]:
         make_grads()
         return
@@ -450,6 +500,7 @@ def main():
         make_grads()
         make_baselines()
         make_metrics()
+        make_smoke()
     meta = {"torch": torch.__version__, "numpy": np.__version__,
             "reference": "shanedirksen/gnn-plasma-flux @ /root/reference (2026-01-02 snapshot)",
             "generator": "tests/golden/make_golden.py"}

@@ -42,7 +42,43 @@ def test_library_built_from_these_sources():
     """hf_version() carries the hash of the sources the .so was built from; it must
     be this tree's, so no record is ever produced by a stale binary."""
     v = _lib.version()
-    assert v.split("src:")[-1] == _lib.source_hash(), f"stale libhybridflux.so ({v}); rebuild with make"
+    assert _lib.build_hash(v) == _lib.source_hash(), f"stale libhybridflux.so ({v}); rebuild with make"
+    assert not _lib.diagnostic_build(v), f"libhybridflux.so was built with extra flags ({v}); rebuild with make"
+
+
+def test_build_hash_covers_extra_flags(tmp_path):
+    """SRC_HASH folds in CXXFLAGS_EXTRA, and the version string spells the flags
+    out: a timing-diagnostic build (HF_DIAG_*, results wrong by design) can never
+    carry the shipped library's hash (make -n prints the capi.cpp compile line
+    the Makefile would run, with the hash and the flags it would embed)."""
+    import subprocess
+    csrc = _lib.CSRC
+    for extra in ("", "-DHF_DIAG_NOFV", "-DHF_EXP_PREFETCH -DHF_DIAG_NOSYNC"):
+        p = subprocess.run(["make", "-n", "-B", "-C", csrc, f"BUILD={tmp_path}", f"OUT={tmp_path}/x.so",
+                            f"CXXFLAGS_EXTRA={extra}", f"{tmp_path}/capi.cpp.o"],
+                           capture_output=True, text=True, check=True)
+        line = [ln for ln in p.stdout.splitlines() if "capi.cpp" in ln and "HF_SOURCE_HASH" in ln][0]
+        h = re.search(r'HF_SOURCE_HASH=\\"([0-9a-f]{16})\\"', line).group(1)
+        assert h == _lib.source_hash(extra)
+        assert f"'-DHF_BUILD_FLAGS=\"{extra}\"'" in line
+    assert _lib.source_hash("-DHF_DIAG_NOFV") != _lib.source_hash()
+    v = "hybridflux 0.2 gfx950 src:0123456789abcdef flags:-DHF_DIAG_NOFV"
+    assert _lib.build_hash(v) == "0123456789abcdef" and _lib.build_flags(v) == "-DHF_DIAG_NOFV"
+    assert _lib.diagnostic_build(v) and not _lib.diagnostic_build(v.split(" flags:")[0])
+
+
+def test_no_switch_defined_in_source():
+    """The HF_DIAG_* / HF_EXP_* switches are set only from the command line
+    (CXXFLAGS_EXTRA, covered by the hash and the version string); a source that
+    #defines one would ship a diagnostic kernel under a clean version.  The one
+    exception is HF_EXP_VFIRST's default of 0 (off)."""
+    for f in os.listdir(_lib.CSRC):
+        if not f.endswith((".hip", ".h", ".cpp")):
+            continue
+        for ln in open(os.path.join(_lib.CSRC, f)):
+            m = re.match(r"\s*#\s*define\s+(HF_(?:DIAG|EXP)_\w+)(.*)", ln)
+            if m:
+                assert m.group(1) == "HF_EXP_VFIRST" and m.group(2).strip() == "0", f"{f}: {ln.strip()}"
 
 
 def test_param_count_matches_reference_model():

@@ -70,19 +70,21 @@ def _worker(rank, world, port, out_dir):
     summ = torch.arange(lo * 8, hi * 8, dtype=torch.float32).reshape(-1, 8)
     ser = torch.arange(lo * (T + 1) * 3, hi * (T + 1) * 3, dtype=torch.float32).reshape(-1, T + 1, 3)
     g_summ, g_ser = gather_ic_rows(summ, N_TOTAL), gather_ic_rows(ser, N_TOTAL)
-    from hybridflux.rollout import max_over_ranks
+    from hybridflux.rollout import COLLECTIVES, max_over_ranks
     mx = max_over_ranks(0.25 * (rank + 1))               # bench.py's max-over-ranks timing
     torch.save({"gathered": gathered, "max": mx, "local_n": res["metrics"].shape[0], "summ": g_summ,
-                "series": g_ser}, os.path.join(out_dir, f"rank{rank}.pt"))
+                "series": g_ser, "calls": COLLECTIVES["calls"], "backend": COLLECTIVES["backend"],
+                "received": COLLECTIVES["bytes_received"]}, os.path.join(out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_gloo_sharded_rollout(tmp_path, world):
-    """world 2: shards 3 + 2; world 4 (a rehearsal of more ranks than the GPU
-    test's 2): 2 + 1 + 1 + 1; world 8: 1 x 5 then three EMPTY shards (more
-    ranks than ICs), which still take part in the gather."""
+    """world 1: a one-rank group still runs every collective (as bench.py's
+    one-rank RCCL group does); world 2: shards 3 + 2; world 4 (a rehearsal of
+    more ranks than the GPU test's 2): 2 + 1 + 1 + 1; world 8: 1 x 5 then three
+    EMPTY shards (more ranks than ICs), which still take part in the gather."""
     port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     want, _ = _oracle_local(list(range(1000, 1000 + N_TOTAL)))
@@ -96,6 +98,10 @@ def test_gloo_sharded_rollout(tmp_path, world):
         assert torch.equal(d["summ"], torch.arange(N_TOTAL * 8, dtype=torch.float32).reshape(N_TOTAL, 8))
         assert torch.equal(d["series"], torch.arange(N_TOTAL * (T + 1) * 3, dtype=torch.float32)
                            .reshape(N_TOTAL, T + 1, 3))
+        # 3 all_gathers + 1 all_reduce, each counted with what it moved
+        cap = -(-N_TOTAL // world)
+        assert d["calls"] == 4 and d["backend"] == "gloo"
+        assert d["received"] == world * cap * ((T + 1) * 4 + 8 + (T + 1) * 3) * 4 + 8
 
 
 def test_gather_single_process_passthrough():

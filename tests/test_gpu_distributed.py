@@ -30,14 +30,15 @@ def _port():
         return s.getsockname()[1]
 
 
-def _env():
+def _env(**extra):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.update(extra)
     return env
 
 
-def _run(cmd, timeout):
-    p = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+def _run(cmd, timeout, **extra):
+    p = subprocess.run(cmd, env=_env(**extra), capture_output=True, text=True, timeout=timeout, cwd=ROOT)
     assert p.returncode == 0, f"{cmd}\nrc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
     return p
 
@@ -50,6 +51,7 @@ def test_two_ranks_equal_one_rank_bitwise(tmp_path):
           "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(two)], 300)
     a, b = np.load(one), np.load(two)
     assert int(a["world"]) == 1 and int(b["world"]) == 2
+    assert int(a["grouped"]) == 0 and int(a["collective_calls"]) == 0 and str(b["backend"]) == "gloo"
     assert float(b["max_over_ranks"]) == 2.0
     for label in ("fused64_f32", "generic256_bf16", "one_ic"):
         for key in ("metrics", "summary", "final", "cmp_mse", "cmp_summary"):
@@ -74,3 +76,49 @@ def test_bench_self_launches_ranks():
     assert d["n_gpus"] == 2 and d["config"]["global_ics"] == 8192 and d["config"]["ics_per_gpu"] == 4096
     assert d["finite_fraction"] == 1.0 and d["value"] > 0
     assert "gloo" in d["config"]["collective"]
+
+
+N_CASES = 3  # dist_rollout_worker.CASES
+
+
+@pytest.mark.timeout(400)
+def test_rccl_one_rank_equals_no_group_bitwise(tmp_path):
+    """RCCL on this engine's data path: a one-rank nccl
+    group (the box has one GPU; RCCL needs one per rank) runs the same
+    end-of-rollout exchange as the 8-GPU job — device all_gather_into_tensor of
+    the metric series, summaries, MSE series and final states, and the device
+    all_reduce MAX of max_over_ranks — and must give exactly the no-group run's
+    tensors (reference workload scripts/evaluation/evaluate_multi_ic.py:106-138)."""
+    one, rccl = tmp_path / "one.npz", tmp_path / "rccl.npz"
+    _run([sys.executable, WORKER, str(one)], 200)
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(rccl)], 300,
+         HF_DIST_BACKEND="nccl")
+    a, b = np.load(one), np.load(rccl)
+    assert int(b["grouped"]) == 1 and int(b["world"]) == 1 and str(b["backend"]) == "nccl"
+    assert float(b["max_over_ranks"]) == 1.0
+    # per case: gather_rollout x2 (metrics, summary; + mse on the compare run) and the final states
+    assert int(b["collective_calls"]) == N_CASES * (2 + 1 + 3) + 1
+    assert int(b["collective_bytes_received"]) > 0
+    for label in ("fused64_f32", "generic256_bf16", "one_ic"):
+        for key in ("metrics", "summary", "final", "cmp_mse", "cmp_summary"):
+            x, y = a[f"{label}/{key}"], b[f"{label}/{key}"]
+            assert x.shape == y.shape, (label, key, x.shape, y.shape)
+            assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), (label, key)
+
+
+@pytest.mark.timeout(400)
+def test_bench_one_gpu_runs_rccl_exchange():
+    """A plain `python bench.py` (N = 1, default backend nccl) creates a
+    one-rank RCCL group and reports the all_gather it actually ran inside the
+    timed region, and the timed rollout's parity against the reference."""
+    p = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+              "--no-cpu-baseline", "--no-other-configs", "--also", ""], 300)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    c = d["config"]["collective"]
+    assert d["n_gpus"] == 1 and c["backend"] == "nccl (RCCL)" and c["world_size"] == 1
+    assert c["calls"] == 2 and c["bytes_received_per_rank"] == 4096 * (5 * 4 + 8) * 4
+    assert c["exchange_ms"] > 0
+    assert d["parity"]["within_gate"] and d["parity"]["steps_checked"] == 4

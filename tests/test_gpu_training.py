@@ -102,7 +102,9 @@ def test_backward_deterministic_and_chain_batch_vs_oracle(hf):
 
 @pytest.mark.parametrize("nx,B,layers,hidden,kinkfree", [(64, 5, 4, 128, False), (1, 3, 2, 128, False),
                                                           (2, 4, 1, 64, False), (7, 6, 0, 32, False),
-                                                          (100, 3, 3, 128, False), (64, 300, 4, 128, True)])
+                                                          (100, 3, 3, 128, False), (64, 300, 4, 128, True),
+                                                          (64, 4, 3, 16, False), (16, 3, 2, 8, False),
+                                                          (8, 2, 1, 4, False), (64, 3, 2, 256, False)])
 def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden, kinkfree):
     """The chain training path (train_chain.hip: stencil-loader GEMMs, P/Q
     readout, split-K weight gradients) on tagged chains of any nx, layer count
@@ -116,7 +118,9 @@ def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden, kinkfree):
     tiles and weight-gradient splits) therefore uses weights whose every
     pre-activation is bounded away from 0 (positive biases of 4 against
     products below 3), so its ReLU derivatives are unambiguous and the gate
-    stays the gradient gate; the small cases exercise the masks."""
+    stays the gradient gate; the small cases exercise the masks.  Widths 4, 8
+    and 16 are below the GEMM's 32-wide reduction chunk: tagged chains of those
+    widths take the generic CSR path and must give the same answers."""
     rng = np.random.default_rng(nx * 100 + layers)
     if kinkfree:
         u = lambda a, shape: rng.uniform(-a, a, shape)  # noqa: E731
@@ -216,6 +220,31 @@ def test_ablation_loss_grads_vs_reference(hf):
     assert abs(loss.item() - want) <= 1e-5 * abs(want)
     for k, p in m.named_parameters():
         grads_close(p.grad, np.mean([g[f"loss{j}_grad.{k}"] for j in range(3)], axis=0))
+
+
+def test_loss_gradient_without_state_term(hf):
+    """lambda_state = 0 ('baseline' config): the loss has no state term
+    (train_ablation.py:132 gates it), so neither may its gradient — a
+    non-finite target density n'_t must leave loss and d loss/d params equal to
+    the finite target's (no 0 * NaN in the continuity adjoint)."""
+    from hybridflux.training import ablation_loss
+    m = _w1_model(hf)
+    solver = hf.BaselineSolver(64, device=DEV)
+    x = torch.as_tensor(solver.x, dtype=torch.float32, device=DEV)
+    st, ft, sn = (torch.as_tensor(np.stack(a), device=DEV) for a in zip(_sample(0, 3), _sample(5, 17)))
+    out = []
+    for poison in (False, True):
+        sn_p = sn.clone()
+        if poison:
+            sn_p[:, 0, ::7] = float("nan")
+        m.zero_grad()
+        loss, _ = ablation_loss(m, st, ft, sn_p, x, solver.dt, solver.dx, hf.ABLATION_CONFIGS["baseline"],
+                                solver.grid)
+        loss.backward()
+        out.append((loss.item(), {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}))
+    assert np.isfinite(out[1][0]) and out[0][0] == out[1][0]
+    for k in out[0][1]:
+        assert np.isfinite(out[1][1][k]).all() and np.array_equal(out[0][1][k], out[1][1][k]), k
 
 
 def test_adam_steps_vs_reference(hf):
