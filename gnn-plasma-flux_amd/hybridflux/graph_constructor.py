@@ -1,7 +1,9 @@
 """Chain-graph construction with the reference's API (src/graph_constructor.py:6-39).
 
 The MI355X kernels never materialise this graph — the chain's +-1 neighbours
-are lane shifts inside chain_gnn.hip — but FluxGNN.forward keeps the
+are lane shifts inside the chain kernels (chain_common.h with the f32 /
+f16x3 / bf16 cores of chain_f32.hip, chain_k32.hip, chain_bf16.hip) — but
+FluxGNN.forward keeps the
 (node_features, edge_index) signature, so these builders produce exactly the
 reference tensors and TAG the edge index so FluxGNN can dispatch to the chain
 kernel without inspecting its contents.

@@ -3,9 +3,10 @@
 One step = FluxGNN edge fluxes on the periodic chain -> F = (F_fwd + F_bwd)/2
 -> continuity n' = n - dt/dx (F - F_left) -> Burgers u' (no viscosity) + dt E
 -> spectral Poisson E'.  On the MI355X the whole step is ONE kernel per IC
-wave (chain_gnn.hip), and `run` is ONE persistent kernel for the whole
-rollout when nx is 16/32/48/64; other nx use the windowed chain kernel + the
-FV/Poisson kernel per step.  Nothing crosses PCIe inside a rollout.
+wave (chain_rollout_kernel, chain_common.h), and `run` is ONE persistent
+kernel for the whole rollout when nx is 16/32/48/64; other nx use the
+windowed / super-window chain kernel + the FV/Poisson kernel per step
+(fv_poisson.hip).  Nothing crosses PCIe inside a rollout.
 
 `step`/`run` keep the reference's numpy [3,nx] shapes; `step_batch`/`run_batch`
 take [B,3,nx] device tensors (batched independent ICs) and return device

@@ -2,7 +2,9 @@
 
 Mirrors scripts/training/train_ablation.py (FluxDataset, train_model and the
 per-sample ablation loss of :107-200).  FluxGNN's forward and backward run in
-the HIP training kernels (graph.hip through FluxGNN's autograd Function); the
+the HIP training kernels through FluxGNN's autograd Function (on tagged
+chains the chain-layout MFMA GEMMs of train_chain.hip / tgemm.h, on other
+graphs the generic kernels of graph.hip); the
 loss assembly, the finite-volume update it differentiates through and Adam are
 the reference trainer's own torch expressions, executed on the device.
 

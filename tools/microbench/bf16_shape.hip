@@ -29,6 +29,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
 
 constexpr int kNW = 8;
 
@@ -432,6 +433,96 @@ __global__ __launch_bounds__(64 * kNW, 1) void layer_ring(const u4 *__restrict__
   out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
 }
 
+
+// ------------------------------------------------- C: weight-stationary
+// The dataflow the ring replaces: each wave keeps its slice of the layer's
+// weights in registers for the whole pass and the ACTIVATIONS stream through
+// LDS.  A workgroup of 4 waves (two per CU, so two waves per SIMD as in A)
+// owns 128 cells; wave w holds output features 32w..32w+31 of A = W_a h + b
+// and of G = (W_b/2) h (4 output tiles x 4 k-blocks = 64 VGPRs of bf16
+// weights) and, per 16-cell n-tile, reads the 4 k-block fragments of bf16(h)
+// once from LDS and feeds each to its 4 output tiles (256 B of LDS per MFMA,
+// as A's weight fragments over 4 m-tiles).  Cells are interleaved over the
+// n-tiles (cell 8j + nt on lane column j), so 7 of 8 neighbour sums are
+// plain adds and one per side a DPP row shift, as in A.  After its 8 n-tiles
+// a wave forms z = A + (G(i-1) + G(i+1)), ReLU, bf16, and writes its 32
+// features of every cell to the other activation buffer; one barrier per
+// layer.  The 16-byte chunks of a cell's 256-byte row are XOR-swizzled by
+// (cell >> 3) so both the fragment reads and the writes are conflict-free.
+// This is the upper bound of the form: the weights are loaded ONCE (a real
+// 5-layer pass reloads 64 VGPRs per wave per layer, and prefetching them would
+// need 64 more than the 256 a wave has at two waves per SIMD).
+__device__ __forceinline__ int ws_off(int cell, int chunk) {  // u4 index into one buffer
+  return cell * 16 + (chunk ^ ((cell >> 3) & 15));
+}
+__global__ __launch_bounds__(256, 2) void layer_ws(const u4 *__restrict__ wsrc, const u4 *__restrict__ xsrc,
+                                                   float *__restrict__ out, int iters) {
+  __shared__ u4 act[2][128 * 16];  // 2 buffers x 128 cells x 256 B (64 KiB)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 15, g = lane >> 4;
+  u4 W[4][4];  // [tile: A0 A1 G0 G1][k-block]
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) W[t][kb] = wsrc[((wave * 16 + t * 4 + kb) * 64) + lane];
+  for (int i = threadIdx.x; i < 128 * 16; i += blockDim.x) act[0][i] = xsrc[(size_t)(blockIdx.x % 4096) * 2048 + i];
+  __syncthreads();
+  const float bias = 0.01f * lane;
+  int cur = 0;
+  for (int it = 0; it < iters; ++it) {
+    f4 acc[4][8];
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t][nt] = t < 2 ? f4{bias, bias, bias, bias} : f4{0.f, 0.f, 0.f, 0.f};
+    const u4 *src = act[cur];
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      u4 B[4];
+      const int cell = 8 * j + nt;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) B[kb] = src[ws_off(cell, kb * 4 + g)];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t][nt] = mma16(W[t][kb], B[kb], acc[t][nt]);
+    }
+    u4 *dst = reinterpret_cast<u4 *>(act[cur ^ 1]);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) {
+        float z[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float s;
+          if (nt == 0) {  // left neighbour = nt 7 of lane j-1, right = nt 1 of this lane
+            s = acc[2 + p][1][r];
+            asm("v_add_f32_dpp %0, %1, %2 row_shr:1 row_mask:0xf bank_mask:0xf"
+                : "+v"(s) : "v"(acc[2 + p][7][r]), "v"(acc[2 + p][1][r]));
+          } else if (nt == 7) {  // right neighbour = nt 0 of lane j+1
+            s = acc[2 + p][6][r];
+            asm("v_add_f32_dpp %0, %1, %2 row_shl:1 row_mask:0xf bank_mask:0xf"
+                : "+v"(s) : "v"(acc[2 + p][0][r]), "v"(acc[2 + p][6][r]));
+          } else {
+            s = __fadd_rn(acc[2 + p][nt - 1][r], acc[2 + p][nt + 1][r]);
+          }
+          z[r] = __fadd_rn(acc[p][nt][r], s);
+        }
+        const unsigned lo = pk_relu(z[0], z[1]), hi = pk_relu(z[2], z[3]);
+        // features 32w + 16p + 4g .. +3 of cell 8j + nt: chunk (32w + 16p + 4g) / 8, half g & 1
+        const int cell = 8 * j + nt, chunk = 4 * wave + 2 * p + (g >> 1);
+        unsigned *d = reinterpret_cast<unsigned *>(dst + ws_off(cell, chunk)) + 2 * (g & 1);
+        *reinterpret_cast<u2 *>(d) = u2{lo, hi};
+      }
+    __syncthreads();
+    cur ^= 1;
+  }
+  unsigned s = 0;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) s ^= act[cur][ws_off(8 * j, kb * 4 + g)][0];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)s;
+}
+
 #define CK(x)                                                                      \
   do {                                                                             \
     hipError_t e_ = (x);                                                           \
@@ -468,12 +559,16 @@ int main(int argc, char **argv) {
   const double flop = 2.0 * 64 * 128 * 256 * kNW * (double)grid * iters;  // per launch
   // 8 warm-up launches (the clock ramps under load), then the variants in
   // turn, 6 rounds, so all see the same clock history
-  const char *names[6] = {"16x16x32 static LDS weights", "32x32x16 static LDS weights", "16x16x32 ring, DMA at barrier",
+  const char *names[7] = {"16x16x32 static LDS weights", "32x32x16 static LDS weights", "16x16x32 ring, DMA at barrier",
                           "16x16x32 ring, DMA after unit 0 (kept form)", "16x16x32 ring, DMA by 4 waves",
-                          "16x16x32 ring barriers, no DMA"};
-  for (int step = 0; step < 8 + 6 * 6; ++step) {
-    const int variant = step < 8 ? 0 : (step - 8) % 6;
-    const int rep = step < 8 ? -1 : (step - 8) / 6;
+                          "16x16x32 ring barriers, no DMA",
+                          "16x16x32 weight-stationary (weights in VGPRs, activations through LDS; upper bound)"};
+  constexpr int kV = 7;
+  // C: two 4-wave workgroups per CU, each 128 cells x 64 outputs x K 128 per
+  // layer = half of A's per-CU work per iteration, so it runs 2 x iters
+  for (int step = 0; step < 8 + kV * 6; ++step) {
+    const int variant = step < 8 ? 0 : (step - 8) % kV;
+    const int rep = step < 8 ? -1 : (step - 8) / kV;
     CK(hipEventRecord(e0, 0));
     switch (variant) {
       case 0: hipLaunchKernelGGL(layer_a, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters); break;
@@ -481,7 +576,8 @@ int main(int argc, char **argv) {
       case 2: hipLaunchKernelGGL(layer_ring<0>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
       case 3: hipLaunchKernelGGL(layer_ring<1>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
       case 4: hipLaunchKernelGGL(layer_ring<2>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
-      default: hipLaunchKernelGGL(layer_ring<3>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
+      case 5: hipLaunchKernelGGL(layer_ring<3>, dim3(grid), dim3(64 * kNW), 0, 0, dw, dx, dout, iters, chunks); break;
+      default: hipLaunchKernelGGL(layer_ws, dim3(2 * grid), dim3(256), 0, 0, dw, dx, dout, 2 * iters); break;
     }
     CK(hipGetLastError());
     CK(hipEventRecord(e1, 0));
