@@ -311,7 +311,7 @@ def main():
                             out=warm_final, ws=ws)
     gather_rollout(warm, n_total)
     ev_g = torch.cuda.Event(enable_timing=True)
-    if grouped:
+    if world > 1:  # a one-rank group has no one to wait for
         dist.barrier()
     torch.cuda.synchronize(dev)
     reset_collective_stats()
@@ -326,7 +326,7 @@ def main():
     gathered = gather_rollout(res, n_total)
     ev_g.record(stream)
     torch.cuda.synchronize(dev)
-    if grouped:
+    if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1)

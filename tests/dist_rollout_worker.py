@@ -33,6 +33,9 @@ import torch.distributed as dist  # noqa: E402
 CASES = [("fused64_f32", 37, 64, 12, "f32", "W1_r2"),
          ("generic256_bf16", 9, 256, 6, "bf16", "W1_r2"),
          ("one_ic", 1, 64, 5, "f32", "W1_r2")]  # at 2 ranks rank 1's shard is EMPTY
+# HF_DIST_CASES=cfg5: BASELINE.json configs[4] at its full size — 32,768 ICs of
+# 64 cells, r = 2 weights, f32 — sharded over the launched ranks (4,096 each at 8)
+CASES_CFG5 = [("cfg5_32768_f32", 32768, 64, 5, "f32", "W1_r2")]
 
 
 def main(out):
@@ -51,7 +54,8 @@ def main(out):
     from hybridflux.rollout import COLLECTIVES, gather_ic_rows, gather_rollout, max_over_ranks, shard_seeds
 
     res = {"world": np.int64(world), "grouped": np.int64(grouped)}
-    for label, n_total, nx, T, prec, w in CASES:
+    cases = CASES_CFG5 if os.environ.get("HF_DIST_CASES") == "cfg5" else CASES
+    for label, n_total, nx, T, prec, w in cases:
         weights = dict(np.load(os.path.join(ROOT, "tests", "golden", f"weights_{w}.npz"), allow_pickle=False))
         solver = HybridSolver(weights, radius=2, nx=nx, dt=5e-3 * 64.0 / nx, device=dev, precision=prec)
         ics = solver.baseline.initial_conditions(shard_seeds(1000, n_total, world, rank), as_tensor=True)

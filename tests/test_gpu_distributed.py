@@ -75,7 +75,9 @@ def test_bench_self_launches_ranks():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["global_ics"] == 8192 and d["config"]["ics_per_gpu"] == 4096
     assert d["finite_fraction"] == 1.0 and d["value"] > 0
-    assert "gloo" in d["config"]["collective"]
+    c = d["config"]["collective"]
+    assert c["backend"] == "gloo" and c["world_size"] == 2 and c["calls"] == 2
+    assert c["bytes_received_per_rank"] == 2 * c["bytes_sent_per_rank"] == 2 * 4096 * (5 * 4 + 8) * 4
 
 
 N_CASES = 3  # dist_rollout_worker.CASES
@@ -122,3 +124,26 @@ def test_bench_one_gpu_runs_rccl_exchange():
     assert c["calls"] == 2 and c["bytes_received_per_rank"] == 4096 * (5 * 4 + 8) * 4
     assert c["exchange_ms"] > 0
     assert d["parity"]["within_gate"] and d["parity"]["steps_checked"] == 4
+
+
+@pytest.mark.timeout(600)
+def test_cfg5_full_size_eight_ranks_equal_one_rank_bitwise(tmp_path):
+    """BASELINE.json configs[4] at its full size: 32,768 ICs of 64 cells (r = 2
+    weights, f32) sharded over 8 rank processes — 4,096 ICs each, as on the
+    8-GPU node — sharing this box's one GPU over gloo (RCCL needs one GPU per
+    rank; the RCCL exchange itself is test_rccl_one_rank_equals_no_group_bitwise).
+    The gathered metric series, summaries, final states and the compare path's
+    MSE equal one process running all 32,768 ICs bit for bit."""
+    one, eight = tmp_path / "one.npz", tmp_path / "eight.npz"
+    _run([sys.executable, WORKER, str(one)], 300, HF_DIST_CASES="cfg5")
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, str(eight)], 500,
+         HF_DIST_CASES="cfg5")
+    a, b = np.load(one), np.load(eight)
+    assert int(a["world"]) == 1 and int(b["world"]) == 8 and str(b["backend"]) == "gloo"
+    assert int(b["cfg5_32768_f32/local_n"]) == 4096
+    for key in ("metrics", "summary", "final", "cmp_mse", "cmp_summary"):
+        x, y = a[f"cfg5_32768_f32/{key}"], b[f"cfg5_32768_f32/{key}"]
+        assert x.shape == y.shape and x.shape[0] == 32768, (key, x.shape, y.shape)
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), key
+    assert np.isfinite(a["cfg5_32768_f32/final"]).all()

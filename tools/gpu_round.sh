@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 TAG=${1:-r02}
 EXTRA=${2:-}
 mkdir -p gpurun_out; export TMPDIR=/tmp
-HF_PARITY_RECORD=gpurun_out/parity_errors_$TAG.json timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1
+HF_PARITY_RECORD=gpurun_out/parity_errors_$TAG.json timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1
 prc=$?
 echo "pytest rc=$prc"
 tail -1 gpurun_out/pytest_gpu_$TAG.log; grep -E "^FAILED|^ERROR" gpurun_out/pytest_gpu_$TAG.log | head -20
