@@ -130,6 +130,11 @@ BF16_FLUX_WBF16 = 7.5e-3   # edge flux vs WBF16
 BF16_STATE_WBF16 = 1e-2    # 30-step state vs WBF16
 BF16_FLUX_EMUL_RAND = 4e-3    # edge flux vs EMUL, random weights: max (a few flips)
 BF16_FLUX_EMUL_RAND_MEAN = 5e-5  # ... and mean |error|
+# With at most one update layer the only bf16 roundings of accumulated values
+# are h0 and h1, and these cases show no flip (max 4.2e-7 = a few f32 ulps of
+# the readout sum, identical in every recorded pass since round 2): they are
+# held to an f32-accumulation-order gate instead of the flip-sized one.
+BF16_FLUX_EMUL_RAND_NOFLIP = 1e-5
 
 
 def _bf16_solver(hf, nx, dt):
@@ -312,5 +317,5 @@ def test_bf16_flux_layers_and_nx(hf, record, layers, nx):
         fe = m(nf, ei).cpu().numpy().reshape(5, 2 * nx)
     record(f"bf16_flux_L{layers}_nx{nx}", "max_abs_vs_emul", np.abs(fe - want).max())
     record(f"bf16_flux_L{layers}_nx{nx}", "mean_abs_vs_emul", np.abs(fe - want).mean())
-    close(fe, want, BF16_FLUX_EMUL_RAND)
+    close(fe, want, BF16_FLUX_EMUL_RAND_NOFLIP if layers <= 1 else BF16_FLUX_EMUL_RAND)
     assert np.abs(fe - want).mean() <= BF16_FLUX_EMUL_RAND_MEAN
