@@ -303,10 +303,16 @@ def main():
         for t in (final, traj_buf, met_buf):
             if t is not None:
                 t.zero_()
+    if grouped:
+        # RCCL sets up its communicator and channels on the first collective
+        # (hundreds of ms with the GPU idle): do that here, in the setup, so the
+        # timed rollout follows the warmup rollout with no idle gap in between
+        # (the clock ramps down when the GPU idles, MI355X_MICROARCH.md DVFS)
+        dist.all_reduce(torch.zeros(1, device=dev if args.dist_backend == "nccl" else "cpu"))
     torch.cuda.synchronize(dev)
 
     # warmup: one rollout of W steps (compiles nothing; faults the code objects
-    # in) and its metric exchange (RCCL sets up its channels on first use)
+    # in) and its metric exchange
     warm = solver.run_batch(ics, Wr, traj=warm_traj if warm_traj is not None else False, metrics=warm_met,
                             out=warm_final, ws=ws)
     gather_rollout(warm, n_total)

@@ -702,6 +702,44 @@ constexpr int kMaxLanes = 4;
 constexpr int kDefaultLanes = 3;  // profiles/r02_lanes_ab.json: 1 / 2 / 3 / 4 lanes = 1.141 / 1.129 / 1.119 / 1.118 ms per cfg4 step
 constexpr int64_t kLaneMinCells = 1 << 20;  // each slice still fills the chip for several rounds
 
+// Where hf_run's lanes cut a batch.  The persistent flux kernel of a lane
+// runs its units (super-windows) in rounds of one unit per resident
+// workgroup, so a lane of u units takes ceil(u / per_round) rounds; slices of
+// B/lanes ICs each leave a partly filled last round (cfg4: 3 x 2844 units =
+// 3 x 12 rounds of 256 for 33.3 rounds of work), and the lanes' kernels mostly
+// run one after another (profiles/r03_v9_bench_kernel_stats.md: the lone
+// dispatches take the 12 rounds' time).  When the kernel's units are known,
+// every lane but the last gets the most ICs that fill whole rounds (floor of
+// the batch's rounds / lanes each: 1352 + 1352 + 1392 ICs = 11 + 11 + 12
+// rounds at cfg4), and the last lane the rest; otherwise an even split.
+// Which lane steps an IC changes none of its arithmetic.  HF_LANE_CUTS=even
+// in the environment selects the even split (A/B timing).
+bool lane_cuts_even() {
+  static const bool even = [] {
+    const char *v = std::getenv("HF_LANE_CUTS");
+    return v && std::strcmp(v, "even") == 0;
+  }();
+  return even;
+}
+void lane_cuts(const hf_model *m, int B, int nx, int lanes, int64_t *cut) {
+  for (int i = 0; i <= lanes; ++i) cut[i] = (int64_t)B * i / lanes;
+  if (!m || lanes < 2 || lane_cuts_even()) return;
+  const hf::FluxWork all = hf::chain_flux_work(m->chain, B, nx);
+  if (all.per_round <= 0) return;
+  const int64_t k = all.units / all.per_round / lanes;  // whole rounds per leading lane
+  if (k < 1) return;
+  int64_t o = 0;
+  for (int i = 0; i + 1 < lanes; ++i) {
+    // the most ICs whose units fit k rounds (units grow by at most
+    // ceil(P / faces) per IC, so step down from the even share's estimate)
+    int64_t n = (int64_t)B / lanes + 1;
+    while (n > 1 && hf::chain_flux_work(m->chain, n, nx).units > k * all.per_round) --n;
+    if (o + n >= B) return;  // keep the even split: nothing left for the last lane
+    cut[i + 1] = o += n;
+  }
+  cut[lanes] = B;
+}
+
 int run_lanes() {
   static const int lanes = [] {
     const char *v = std::getenv("HF_RUN_LANES");
@@ -893,7 +931,9 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
                  "hf_run");
     return HF_OK;
   }
-  // lane i steps ICs [B*i/lanes, B*(i+1)/lanes); lane 0 on the caller's stream
+  // lane i steps ICs [cut[i], cut[i+1]); lane 0 on the caller's stream
+  int64_t cut[kMaxLanes + 1];
+  lane_cuts(m, B, nx, lanes, cut);
   hipStream_t ls[kMaxLanes] = {s};
   bool granted = false;
   HF_CHECK_HIP(lane_streams(s, lanes, ls, &granted), "hf_run lane stream");
@@ -915,7 +955,7 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   if (e == hipSuccess) e = hipEventRecord(fork, s);
   bool used[kMaxLanes] = {};  // lane streams that received work
   for (int i = lanes - 1; i >= 0 && e == hipSuccess; --i) {
-    const int64_t o = (int64_t)B * i / lanes, n = (int64_t)B * (i + 1) / lanes - o;
+    const int64_t o = cut[i], n = cut[i + 1] - o;
     if (i > 0) e = hipStreamWaitEvent(ls[i], fork, 0);
     if (e != hipSuccess) break;
     used[i] = true;

@@ -970,6 +970,18 @@ hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float 
   return launch_flux_sw<CoreBF16<8, 4, 4, false, 3, 1, HF_SW_DMAU, true>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
+FluxWork chain_flux_work(const ChainW &w, int64_t B, int nx) {
+  FluxWork fw;
+  if (w.prec != kPrecBF16 || B <= 0 || nx == 16 || nx == 32 || nx == 48 || nx == 64 ||
+      chain_rollout_prefers_cells(w, (int)B, nx))
+    return fw;  // not the super-window kernel
+  constexpr int NW = 8;  // launch_chain_flux_bf16's super-window core
+  const int64_t faces = 63 * NW - 2 * w.layers, P = nx + 2 * w.layers + 1;
+  fw.units = (B * P + faces - 1) / faces;   // super-windows (launch_flux_sw)
+  fw.per_round = resident_groups();         // one per persistent workgroup per round
+  return fw;
+}
+
 hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float *state_final, const float *x,
                                      const double *pc, int B, int nx, int T, float c, float dt, float *traj,
                                      float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {

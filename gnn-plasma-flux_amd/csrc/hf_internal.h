@@ -149,6 +149,15 @@ inline hipError_t launch_chain_flux(const ChainW &w, const float *nf, const floa
                             : launch_chain_flux_k32(w, nf, state, ld_state, x, B, nx, flux_edge, flux_face, s);
 }
 
+// Work of one step of the per-step flux kernel for B ICs of nx cells, in the
+// persistent kernel's own units, and how many units one round of its resident
+// workgroups takes (hf_run's lanes cut the batch at whole rounds).  Known for
+// the bf16 super-window kernel (chain_bf16.hip); per_round = 0 otherwise.
+struct FluxWork {
+  int64_t units = 0, per_round = 0;
+};
+FluxWork chain_flux_work(const ChainW &w, int64_t B, int nx);
+
 // Persistent fused rollout for nx in {16,32,48,64}.
 inline hipError_t launch_chain_rollout(const ChainW &w, const float *state0, float *state_final,
                                        const float *x, const double *pc, int B, int nx, int T, float c,
