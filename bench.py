@@ -143,6 +143,49 @@ def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=Non
     return out
 
 
+def other_models(dev, B, K, warm_s=0.3):
+    """The reference's comparison models (scripts/training/
+    train_pure_gnn.py:35-76 PureGNN(4,128,4), train_pinn.py:36-61 PINN(192,256,4))
+    as one-launch batched rollouts of B ICs x 64 cells, K steps with the
+    trajectory recorded (evaluate_multi_ic.py:45-83), weights from the
+    committed fixture tests/golden/baselines.npz; warmed for warm_s of their
+    own rollout, then one timed rollout each (HIP events + wall clock).
+    Reported next to the headline, never as it."""
+    from hybridflux import BaselineSolver
+    from hybridflux.baselines import PINN, PureGNN
+    b = np.load(os.path.join(ROOT, "tests", "golden", "baselines.npz"))
+    solver = BaselineSolver(64, device=dev)
+    ics = solver.initial_conditions(range(1000, 1000 + B), as_tensor=True)
+    pg = PureGNN(4, 128, 4)
+    pg.load_state_dict({k[9:]: torch.from_numpy(b[k]) for k in b.files if k.startswith("pure_gnn.")})
+    pn = PINN(3 * 64, 256, 4)
+    pn.load_state_dict({k[5:]: torch.from_numpy(b[k]) for k in b.files if k.startswith("pinn.")})
+    pg, pn = pg.to(dev), pn.to(dev)
+    H, L, nx = 128, 4, 64
+    flop = {"pure_gnn": nx * 2 * (4 * H + L * 2 * H * H + H * H + 3 * H),       # tools/bench_models.py
+            "pinn": 2 * (3 * nx * 256 + 2 * 256 * 256 + 256 * 3 * nx)}
+    fns = {"pure_gnn": lambda: pg.rollout(ics, K, solver.x), "pinn": lambda: pn.rollout(ics, K)}
+    out = {}
+    stream = torch.cuda.current_stream(dev)
+    for name, fn in fns.items():
+        t_end = time.perf_counter() + warm_s
+        while time.perf_counter() < t_end:
+            fn()
+            torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        kms = e0.elapsed_time(e1)
+        out[name] = {"value": round(B * K / wall, 1), "unit": "IC-steps/s", "ics": B, "nx": nx, "steps": K,
+                     "kernel_ms": round(kms, 3), "flop_per_ic_step": flop[name],
+                     "mfma_frac": round(flop[name] * B * K / (kms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)}
+    return out
+
+
 def pmc_traffic(K, B, nx, traj, build):
     """HBM bytes per launch of the headline kernel from the committed PMC passes
     (tools/gpu_pmc_traffic.sh + tools/pmc_traffic.py): FETCH_SIZE / WRITE_SIZE at two
@@ -189,6 +232,28 @@ def headline_parity(traj_buf, nx, K, weights_path, precision):
             "reference": "tests/golden/hybrid_W1_r3_nx64.npz (seeds 1000..1015, reference CPU HybridSolver)"}
 
 
+class _StdoutToStderr:
+    """fd-level redirect of stdout to stderr: RCCL prints its version banner to
+    stdout when it sets up (RCCL version / HIP version / ... lines), and this
+    script's stdout carries exactly one JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        import ctypes
+        try:
+            ctypes.CDLL(None).fflush(None)  # C stdio buffers written while redirected go to stderr too
+        except (OSError, AttributeError):
+            pass
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def init_group(backend, world, dev):
     """The process group of this job.  RCCL (backend nccl) gets a group at every
     world size, one rank included, so the end-of-rollout metric exchange is a
@@ -205,10 +270,17 @@ def init_group(backend, world, dev):
             os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", str(world))
-    if backend == "nccl":
-        dist.init_process_group("nccl", device_id=dev)
-    else:
-        dist.init_process_group("gloo")
+    with _StdoutToStderr():
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        # RCCL sets up its communicator and channels on the first collective
+        # (hundreds of ms with the GPU idle): do that here, in the setup, so the
+        # timed rollout follows the warmup rollout with no idle gap in between
+        # (the clock ramps down when the GPU idles, MI355X_MICROARCH.md DVFS)
+        dist.all_reduce(torch.zeros(1, device=dev if backend == "nccl" else "cpu"))
+        torch.cuda.synchronize(dev)
     return True
 
 
@@ -303,12 +375,6 @@ def main():
         for t in (final, traj_buf, met_buf):
             if t is not None:
                 t.zero_()
-    if grouped:
-        # RCCL sets up its communicator and channels on the first collective
-        # (hundreds of ms with the GPU idle): do that here, in the setup, so the
-        # timed rollout follows the warmup rollout with no idle gap in between
-        # (the clock ramps down when the GPU idles, MI355X_MICROARCH.md DVFS)
-        dist.all_reduce(torch.zeros(1, device=dev if args.dist_backend == "nccl" else "cpu"))
     torch.cuda.synchronize(dev)
 
     # warmup: one rollout of W steps (compiles nothing; faults the code objects
@@ -412,6 +478,8 @@ def main():
                   other_config(w_r2, dev, "cfg4: 1024-cell chain, 4096-IC batch, r=2, bf16 MLP weights, dt=3.125e-4",
                                4096, 1024, "bf16", 30, 30, 2, fixture=fx)]
 
+    models = other_models(dev, 4096, 30) if world == 1 and not args.no_other_configs else None
+
     wall_max = max_over_ranks(wall)
     finite = float(gathered["metrics"][:, -1, 2].float().mean().item())
     exploded = int((gathered["summary"][:, 0] >= 0).sum().item())
@@ -489,6 +557,8 @@ def main():
             "alt": alt or None,
             "radii": radii,
             "other_configs": others,
+            # the reference's PureGNN / PINN rollouts, 4096 ICs x 64 cells, T = 30
+            "other_models": models,
         }
         print(json.dumps(line), flush=True)
     if grouped:

@@ -116,8 +116,9 @@ def test_bench_one_gpu_runs_rccl_exchange():
     timed region, and the timed rollout's parity against the reference."""
     p = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
               "--no-cpu-baseline", "--no-other-configs", "--also", ""], 300)
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, p.stdout[-2000:]
+    # stdout is exactly the one JSON line (RCCL's version banner goes to stderr)
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-2000:]
     d = json.loads(lines[0])
     c = d["config"]["collective"]
     assert d["n_gpus"] == 1 and c["backend"] == "nccl (RCCL)" and c["world_size"] == 1

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-4 full GPU pass: every GPU test (parity errors recorded), smoke, the
+# default bench, the driver's 20/5 bench, rocprofv3 kernel traces of both
+# bench commands, then the FETCH_SIZE / WRITE_SIZE passes that bind
+# profiles/pmc_traffic.json to this library's hash.  TAG names the outputs.
+set -o pipefail
+cd "$(dirname "$0")/.."
+TAG=${1:-r04_final}
+mkdir -p gpurun_out; export TMPDIR=/tmp
+HF_PARITY_RECORD=gpurun_out/parity_errors_$TAG.json timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1
+prc=$?
+echo "pytest rc=$prc"; tail -1 gpurun_out/pytest_gpu_$TAG.log; grep -E "^FAILED|^ERROR" gpurun_out/pytest_gpu_$TAG.log | head -20
+grep -qE "Fatal|core dumped|Aborted|Segmentation" gpurun_out/pytest_gpu_$TAG.log && exit 3
+timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 && cat gpurun_out/smoke_$TAG.log || exit 4
+timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 5
+wc -l gpurun_out/bench_$TAG.json; cut -c1-400 gpurun_out/bench_$TAG.json
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_$TAG.json 2> gpurun_out/bench_driver_$TAG.err || exit 6
+cut -c1-400 gpurun_out/bench_driver_$TAG.json
+bash tools/gpu_bench_prof.sh $TAG || exit 7
+bash tools/gpu_pmc_traffic.sh $TAG || exit 8
+exit $prc
