@@ -23,6 +23,15 @@ def main(path):
     print("\nDispatches of the top kernel (us):",
           ", ".join(f"{d / 1e3:.1f}" for (d,) in c.execute(
               "select duration from kernels where name = ? order by start", (rows[0][0],))))
+    # the bench line's headline kernel (cfg3 f32 rollout), whatever its rank in
+    # the table: its dispatches in launch order are warmup, TIMED, next rollout,
+    # then the radii lines' warmup + rollout pairs (bench.py)
+    head = [(n, d) for n, d in c.execute("select name, duration from kernels order by start")
+            if "chain_rollout_kernel" in n and "CoreF32T<2, 4, false, true>" in n.replace("(anonymous namespace)::", "")]
+    if head:
+        print("\nDispatches of the headline kernel `chain_rollout_kernel<CoreF32T<2, 4, false, true>, 4>` "
+              "in launch order (us; bench.py: warmup, timed, next rollout, then the radii's warmup + rollout pairs):",
+              ", ".join(f"{d / 1e3:.1f}" for _, d in head))
 
 
 if __name__ == "__main__":
