@@ -16,6 +16,8 @@ Every collective issued here is counted in `COLLECTIVES` (backend, calls, bytes
 each rank received), so a benchmark line reports the transfer that happened,
 not one computed from tensor shapes.
 """
+import math
+
 import torch
 import torch.distributed as dist
 
@@ -87,6 +89,25 @@ def gather_ic_rows(local, n_total, group=None):
     return out.to(local.device) if stage else out
 
 
+def gather_ic_rows_packed(tensors, n_total, group=None):
+    """gather_ic_rows of several per-IC tensors [b_local, ...] (same leading
+    size, dtype and device) in ONE collective: their rows are packed side by
+    side into one [b_local, sum of row sizes] buffer, gathered, and split back
+    into [n_total, ...] tensors.  One RCCL call instead of one per tensor (each
+    call pays the collective's latency across the ranks)."""
+    if not dist.is_initialized():
+        return list(tensors)
+    b = tensors[0].shape[0]
+    widths = [int(math.prod(t.shape[1:])) for t in tensors]
+    packed = torch.cat([t.reshape(b, w) for t, w in zip(tensors, widths)], dim=1)
+    flat = gather_ic_rows(packed, n_total, group)
+    out, o = [], 0
+    for t, w in zip(tensors, widths):
+        out.append(flat[:, o:o + w].reshape((flat.shape[0],) + tuple(t.shape[1:])))
+        o += w
+    return out
+
+
 def max_over_ranks(value, group=None, device=None):
     """The job's wall time: the MAX of each rank's value (bench.py's timing rule:
     the slowest shard ends the job).  A float64 all_reduce whenever a group is
@@ -109,15 +130,14 @@ def gather_rollout(res, n_total, group=None):
     metric series res['metrics'] [b, T+1, K] (and the MSE series res['mse']
     [b, T+1, 3] when the rollout was scored against the classical twin) are
     summarised on the device (hf_rollout_summary: first non-finite step, drifts,
-    MSE totals), then series and summaries are all_gathered in global IC order.
+    MSE totals), then series and summaries are all_gathered in global IC order,
+    packed into ONE collective.
     Returns dict(metrics [n_total, T+1, K], summary [n_total, 8], mse or None)."""
     from . import engine
     summ, _ = engine.rollout_summary(res["metrics"], res.get("mse"), res.get("metrics_classical"))
-    out = {"metrics": gather_ic_rows(res["metrics"], n_total, group),
-           "summary": gather_ic_rows(summ, n_total, group), "mse": None}
-    if res.get("mse") is not None:
-        out["mse"] = gather_ic_rows(res["mse"], n_total, group)
-    return out
+    parts = [res["metrics"], summ] + ([res["mse"]] if res.get("mse") is not None else [])
+    got = gather_ic_rows_packed(parts, n_total, group)  # one collective for all of them
+    return {"metrics": got[0], "summary": got[1], "mse": got[2] if len(got) > 2 else None}
 
 
 def sharded_rollout(run_local, make_ics, seed0, n_total, T, group=None, summarize=True):

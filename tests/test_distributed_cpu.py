@@ -107,3 +107,27 @@ def test_gloo_sharded_rollout(tmp_path, world):
 def test_gather_single_process_passthrough():
     x = torch.arange(12.0).reshape(3, 4)
     assert gather_ic_rows(x, 3) is x
+
+
+def _packed_worker(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hybridflux.rollout import COLLECTIVES, gather_ic_rows_packed
+    n = 5
+    lo, hi = shard_bounds(n, world, rank)
+    a = torch.arange(lo * 12, hi * 12, dtype=torch.float32).reshape(-1, 3, 4)
+    b = torch.arange(lo * 8, hi * 8, dtype=torch.float32).reshape(-1, 8) + 1000
+    ga, gb = gather_ic_rows_packed([a, b], n)
+    assert torch.equal(ga, torch.arange(60.0).reshape(5, 3, 4))
+    assert torch.equal(gb, torch.arange(40.0).reshape(5, 8) + 1000)
+    assert COLLECTIVES["calls"] == 1
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_packed_gather_one_collective(world):
+    """gather_rollout's packed exchange: a [b, 3, 4] series and [b, 8] summaries
+    gathered in ONE collective, split back in global IC order (world 8: three
+    empty shards)."""
+    mp.spawn(_packed_worker, args=(world, _free_port()), nprocs=world, join=True)

@@ -76,7 +76,7 @@ def test_bench_self_launches_ranks():
     assert d["n_gpus"] == 2 and d["config"]["global_ics"] == 8192 and d["config"]["ics_per_gpu"] == 4096
     assert d["finite_fraction"] == 1.0 and d["value"] > 0
     c = d["config"]["collective"]
-    assert c["backend"] == "gloo" and c["world_size"] == 2 and c["calls"] == 2
+    assert c["backend"] == "gloo" and c["world_size"] == 2 and c["calls"] == 1  # metrics + summaries packed
     assert c["bytes_received_per_rank"] == 2 * c["bytes_sent_per_rank"] == 2 * 4096 * (5 * 4 + 8) * 4
 
 
@@ -99,8 +99,8 @@ def test_rccl_one_rank_equals_no_group_bitwise(tmp_path):
     a, b = np.load(one), np.load(rccl)
     assert int(b["grouped"]) == 1 and int(b["world"]) == 1 and str(b["backend"]) == "nccl"
     assert float(b["max_over_ranks"]) == 1.0
-    # per case: gather_rollout x2 (metrics, summary; + mse on the compare run) and the final states
-    assert int(b["collective_calls"]) == N_CASES * (2 + 1 + 3) + 1
+    # per case: gather_rollout of the run and of the compare (one packed call each) and the final states
+    assert int(b["collective_calls"]) == N_CASES * 3 + 1
     assert int(b["collective_bytes_received"]) > 0
     for label in ("fused64_f32", "generic256_bf16", "one_ic"):
         for key in ("metrics", "summary", "final", "cmp_mse", "cmp_summary"):
@@ -122,7 +122,7 @@ def test_bench_one_gpu_runs_rccl_exchange():
     d = json.loads(lines[0])
     c = d["config"]["collective"]
     assert d["n_gpus"] == 1 and c["backend"] == "nccl (RCCL)" and c["world_size"] == 1
-    assert c["calls"] == 2 and c["bytes_received_per_rank"] == 4096 * (5 * 4 + 8) * 4
+    assert c["calls"] == 1 and c["bytes_received_per_rank"] == 4096 * (5 * 4 + 8) * 4
     assert c["exchange_ms"] > 0
     assert d["parity"]["within_gate"] and d["parity"]["steps_checked"] == 4
 
