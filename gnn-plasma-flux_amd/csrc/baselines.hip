@@ -224,11 +224,6 @@ constexpr int kPinnIcs = 16;
 // waves per workgroup: 16 (four per SIMD, one output tile each) measured 7 %
 // faster than 4 and 3 % faster than 8 (profiles/r03_pinn_ab.txt)
 constexpr int kPinnWaves = HF_PINN_WAVES;
-#ifndef HF_PINN_AHEAD
-#define HF_PINN_AHEAD 4
-#endif
-// weight k-blocks a wave keeps in flight (f4 per lane each)
-constexpr int kPinnAhead = HF_PINN_AHEAD;
 
 // One layer on this wave's output tiles t = wave + kPinnWaves * j (j < NT) of
 // NTILES: out = act(W in + b) (ACT 0: tanh; 1: the last layer, state += W in + b).
@@ -236,7 +231,7 @@ template <int K, int NTILES, int ACT>
 __device__ __forceinline__ void pinn_layer(const float *__restrict__ W, const float *__restrict__ bias,
                                            const float *in, float *out, int wave, int lane) {
   constexpr int NT = (NTILES + kPinnWaves - 1) / kPinnWaves;
-  constexpr int KB = K / 16, P = kPinnAhead;
+  constexpr int KB = K / 16, P = 4;
   const int m = lane & 15, g = lane >> 4;
   f4v acc[NT];
   const float *wrow[NT];
