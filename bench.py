@@ -342,7 +342,18 @@ def main():
         raise SystemExit(f"LOCAL_RANK {local} but only {ndev} visible GPU(s); RCCL needs one GPU per rank")
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    grouped = init_group(args.dist_backend, world, dev)
+    group_error = None
+    try:
+        grouped = init_group(args.dist_backend, world, dev)
+    except Exception as e:  # noqa: BLE001
+        if world > 1:
+            raise
+        # one rank: the rollout needs no peer; report the failed RCCL setup
+        # instead of a collective rather than losing the measurement
+        grouped, group_error = False, f"{type(e).__name__}: {e}"
+        print(f"bench.py: no process group at N = 1 ({group_error})", file=sys.stderr, flush=True)
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
     from hybridflux import HybridSolver, engine
     from hybridflux._lib import HF_OP_RUN, build_hash, diagnostic_build, version
@@ -532,7 +543,8 @@ def main():
                                        "bytes_sent_per_rank": coll["bytes_sent"],
                                        "bytes_received_per_rank": coll["bytes_received"],
                                        "exchange_ms": round(exchange_ms, 4)}
-                                      if coll["calls"] else None)},
+                                      if coll["calls"] else
+                                      ({"backend": "none", "error": group_error} if group_error else None))},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "traffic": traffic["traffic_bytes"] if traffic else None,
