@@ -81,6 +81,7 @@ struct PureW {
   const float *w_o2, *b_o2;  // [3][H], [3]
   int in_dim, H, L;
   int64_t ls;
+  const float *w_lp, *w_o1p;  // the one-launch rollout's packed copies: [l][u][P|Q][kb][lane][4], [u][kb][lane][4]
 };
 
 PureW pure_view(const float *p, int in_dim, int H, int L) {
@@ -188,6 +189,7 @@ hipError_t pure_forward(const PureW &w, const float *nf, int64_t N, const int64_
 struct PinnW {
   const float *w[kMaxChainLayers], *b[kMaxChainLayers];
   int D, H, L;
+  const float *wp[kMaxChainLayers];  // the one-launch rollout's packed copies of w (pinn_pack_kernel)
 };
 PinnW pinn_view(const float *p, int D, int H, int L) {
   PinnW w{};
@@ -208,8 +210,9 @@ PinnW pinn_view(const float *p, int D, int H, int L) {
 // evaluate_multi_ic.py:75-81): a workgroup owns 16 ICs for all T steps, with
 // their state and the hidden activations in LDS, and runs every layer as
 // v_mfma_f32_16x16x4_f32 tiles (16 output features x 16 ICs) whose weight
-// operand comes straight from nn.Linear's [out][in] rows in global memory
-// (L2-resident: 0.9 MB), four k-blocks in flight.  The k order inside a
+// operand is read from a packed copy of nn.Linear's rows in the caller's
+// workspace (pinn_pack_kernel: each wave's k-block one contiguous 1 KiB;
+// L2-resident: 0.9 MB), four k-blocks in flight.  The k order inside a
 // 16-block is permuted so that a lane's four MFMA steps read one float4 of its
 // weight row (k = 16 kb + 4 (lane >> 4) + step); the activations use the same
 // order, so LDS holds them as [k-block][lane][4]: an MFMA output tile is
@@ -232,21 +235,21 @@ __device__ __forceinline__ void pinn_layer(const float *__restrict__ W, const fl
                                            const float *in, float *out, int wave, int lane) {
   constexpr int NT = (NTILES + kPinnWaves - 1) / kPinnWaves;
   constexpr int KB = K / 16, P = 4;
-  const int m = lane & 15, g = lane >> 4;
+  const int g = lane >> 4;
   f4v acc[NT];
   const float *wrow[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
     const int t = wave + kPinnWaves * j < NTILES ? wave + kPinnWaves * j : NTILES - 1;  // a spare tile: not stored
-    wrow[j] = W + (int64_t)(16 * t + m) * K + 4 * g;
+    wrow[j] = W + ((int64_t)t * KB * 64 + lane) * 4;  // packed: k-block kb at + 256 kb, one contiguous 1 KiB per wave
   }
   f4v wq[P][NT];  // k-blocks c .. c + P - 1 in flight while c is multiplied
 #pragma unroll
   for (int kb = 0; kb < KB + P - 1; ++kb) {
     if (kb < KB) {  // slot kb % P held k-block kb - P, consumed last iteration
 #pragma unroll
-      for (int j = 0; j < NT; ++j) wq[kb % P][j] = *reinterpret_cast<const f4v *>(wrow[j] + 16 * kb);
+      for (int j = 0; j < NT; ++j) wq[kb % P][j] = *reinterpret_cast<const f4v *>(wrow[j] + 256 * kb);
     }
     if (kb >= P - 1) {
       const int c = kb - (P - 1);
@@ -304,13 +307,14 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
   __syncthreads();
   const int L = w.L;
   for (int t = 0; t < T; ++t) {
-    pinn_layer<D, H / 16, 0>(w.w[0], w.b[0], s_state, act0, wave, lane);
+    const float *const *WW = w.wp;  // packed weights
+    pinn_layer<D, H / 16, 0>(WW[0], w.b[0], s_state, act0, wave, lane);
     __syncthreads();
     for (int l = 1; l < L - 1; ++l) {
-      pinn_layer<H, H / 16, 0>(w.w[l], w.b[l], (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane);
+      pinn_layer<H, H / 16, 0>(WW[l], w.b[l], (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane);
       __syncthreads();
     }
-    pinn_layer<H, D / 16, 1>(w.w[L - 1], w.b[L - 1], (L & 1) ? act1 : act0, s_state, wave, lane);
+    pinn_layer<H, D / 16, 1>(WW[L - 1], w.b[L - 1], (L & 1) ? act1 : act0, s_state, wave, lane);
     __syncthreads();
     if (traj) {
       for (int idx = tid; idx < kPinnIcs * D; idx += NTH) {
@@ -390,10 +394,58 @@ __device__ __forceinline__ void pure_tiles(const RowPtr &rowptr, const float *ac
   }
 }
 
+// pure_tiles on packed weights (pure_pack_kernel): row tile j's k-block kb is
+// the contiguous 1 KiB at base + (j * KB + kb) * 256 — whole 128-B lines per
+// load, where nn.Linear's rows give a load 16 rows x 64 B (half lines)
+template <int K, int NC, int NR>
+__device__ __forceinline__ void pure_tiles_packed(const float *base, const float *act, int lane, f4v (&acc)[NR][NC]) {
+  constexpr int KB = K / 16, P = 3;
+  const float *wr[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    wr[j] = base + (int64_t)j * KB * 256 + lane * 4;
+#pragma unroll
+    for (int g = 0; g < NC; ++g) acc[j][g] = f4v{0.f, 0.f, 0.f, 0.f};
+  }
+  f4v wq[P][NR];
+#pragma unroll
+  for (int kb = 0; kb < KB + P - 1; ++kb) {
+    if (kb < KB) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j) wq[kb % P][j] = *reinterpret_cast<const f4v *>(wr[j] + 256 * kb);
+    }
+    if (kb >= P - 1) {
+      const int c = kb - (P - 1);
+#pragma unroll
+      for (int g = 0; g < NC; ++g) {
+        const f4v bv = *reinterpret_cast<const f4v *>(act + ((c * NC + g) * 64 + lane) * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            acc[j][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j][g], 0, 0, 0);
+      }
+    }
+  }
+}
+// rows r0 + 16 u + (lane & 15), columns c0 + 16 kb + 4 (lane >> 4) + e of a row-major [*][ld] matrix
+__global__ void pure_pack_kernel(const float *__restrict__ W, int64_t ld, int rows, int K, int nj, int64_t jcol,
+                                 float *__restrict__ P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int KB = K / 16;
+  if (i >= (int64_t)rows * K * nj) return;
+  const int e = (int)(i & 3), lane = (int)((i >> 2) & 63);
+  int64_t r = i >> 8;  // ((u * nj + j) * KB + kb)
+  const int kb = (int)(r % KB);
+  r /= KB;
+  const int j = (int)(r % nj), u = (int)(r / nj);
+  P[i] = W[(int64_t)(16 * u + (lane & 15)) * ld + j * jcol + 16 * kb + 4 * (lane >> 4) + e];
+}
+
 #ifndef HF_PURE_WG
 #define HF_PURE_WG 2
 #endif
-template <int H, int NC>
+template <int H, int NC, bool PACKED>
 __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(PureW w, const float *__restrict__ state0,
                                                                     float *__restrict__ final_state,
                                                                     const float *__restrict__ x,
@@ -428,7 +480,10 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
     for (int l = 0; l < w.L; ++l) {
       const float *W = w.w_l + l * w.ls, *bl = w.b_l + l * w.ls;
       f4v acc[2][NC];  // [P | Q][cell group]
-      pure_tiles<H, NC, 2>([&](int j, int m) { return W + (int64_t)(16 * u + m) * 2 * H + j * H; }, act, lane, acc);
+      if constexpr (PACKED)
+        pure_tiles_packed<H, NC, 2>(w.w_lp + ((int64_t)l * (H / 16) + u) * 2 * (H / 16) * 256, act, lane, acc);
+      else
+        pure_tiles<H, NC, 2>([&](int j, int m) { return W + (int64_t)(16 * u + m) * 2 * H + j * H; }, act, lane, acc);
       __syncthreads();  // every wave's reads of h are done: h is rewritten in place below
       f4v bq;
 #pragma unroll
@@ -454,7 +509,10 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
     // output_mlp.0: o = tanh(W_o1 h + b_o1), written over h once every wave has read it
     {
       f4v acc[1][NC];
-      pure_tiles<H, NC, 1>([&](int, int m) { return w.w_o1 + (int64_t)(16 * u + m) * H; }, act, lane, acc);
+      if constexpr (PACKED)
+        pure_tiles_packed<H, NC, 1>(w.w_o1p + (int64_t)u * (H / 16) * 256, act, lane, acc);
+      else
+        pure_tiles<H, NC, 1>([&](int, int m) { return w.w_o1 + (int64_t)(16 * u + m) * H; }, act, lane, acc);
       f4v bo;
 #pragma unroll
       for (int i = 0; i < 4; ++i) bo[i] = w.b_o1[16 * u + q4 + i];
@@ -488,14 +546,39 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
 #endif
 bool pure_fused_ok(int H, int nx) { return (H == 64 || H == 128) && nx % 16 == 0 && nx >= 16 && nx <= 64; }
 
-template <int H>
-hipError_t pure_fused_h(const PureW &w, const float *state0, float *final_state, const float *x, int B, int nx, int T,
-                        float *traj, hipStream_t s) {
+// floats of the one-launch PureGNN rollout's packed weights (L layers, width H)
+int64_t pure_packed_floats(int H, int L) { return (int64_t)L * 2 * H * H + (int64_t)H * H; }
+
+template <int H, bool PACKED>
+void pure_fused_launch(const PureW &w, const float *state0, float *final_state, const float *x, int B, int nx, int T,
+                       float *traj, hipStream_t s) {
   switch (nx / 16) {
-    case 1: hipLaunchKernelGGL((pure_run_kernel<H, 1>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
-    case 2: hipLaunchKernelGGL((pure_run_kernel<H, 2>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
-    case 3: hipLaunchKernelGGL((pure_run_kernel<H, 3>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
-    default: hipLaunchKernelGGL((pure_run_kernel<H, 4>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
+    case 1: hipLaunchKernelGGL((pure_run_kernel<H, 1, PACKED>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
+    case 2: hipLaunchKernelGGL((pure_run_kernel<H, 2, PACKED>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
+    case 3: hipLaunchKernelGGL((pure_run_kernel<H, 3, PACKED>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
+    default: hipLaunchKernelGGL((pure_run_kernel<H, 4, PACKED>), dim3(B), dim3(64 * (H / 16)), 0, s, w, state0, final_state, x, traj, B, T); break;
+  }
+}
+
+// ws: the packed copy (pure_packed_floats(H, kMaxChainLayers) floats, hf_pure_gnn_run_workspace_bytes),
+// made here from the state-dict-order weights; more layers than that run on nn.Linear's rows
+template <int H>
+hipError_t pure_fused_h(const PureW &w0, const float *state0, float *final_state, const float *x, int B, int nx, int T,
+                        float *traj, void *ws, hipStream_t s) {
+  PureW w = w0;
+  if (ws && w.L <= kMaxChainLayers) {
+    float *packed = static_cast<float *>(ws);
+    const int64_t nl = (int64_t)w.L * 2 * H * H, no = (int64_t)H * H;
+    for (int l = 0; l < w.L; ++l)
+      hipLaunchKernelGGL(pure_pack_kernel, dim3((unsigned)((2LL * H * H + 255) / 256)), dim3(256), 0, s,
+                         w.w_l + l * w.ls, (int64_t)2 * H, H, H, 2, (int64_t)H, packed + (int64_t)l * 2 * H * H);
+    hipLaunchKernelGGL(pure_pack_kernel, dim3((unsigned)((no + 255) / 256)), dim3(256), 0, s, w.w_o1, (int64_t)H, H, H,
+                       1, (int64_t)0, packed + nl);
+    w.w_lp = packed;
+    w.w_o1p = packed + nl;
+    pure_fused_launch<H, true>(w, state0, final_state, x, B, nx, T, traj, s);
+  } else {
+    pure_fused_launch<H, false>(w, state0, final_state, x, B, nx, T, traj, s);
   }
   return hipGetLastError();
 }
@@ -503,10 +586,54 @@ hipError_t pure_fused_h(const PureW &w, const float *state0, float *final_state,
 // the one-launch rollout's shapes: the reference's PINN(3 * 64, 256, L)
 bool pinn_fused_ok(int D, int H, int L) { return D == 192 && H == 256 && L >= 2 && L <= kMaxChainLayers; }
 
-hipError_t pinn_fused(const PinnW &w, const float *state0, float *final_state, int64_t B, int T, float *traj,
-                      hipStream_t s) {
+// The one-launch rollout's weight layout.  nn.Linear's [out][in] rows give a
+// wave's float4-per-lane k-block 16 rows x 64 B: half of each 128-B line per
+// load, the other half re-requested by the next k-block's load.  Packed as
+// [tile][k-block][lane][4] (element (t, kb, lane, e) = W[16t + (lane & 15)][16kb
+// + 4(lane >> 4) + e]) a k-block is one contiguous 1 KiB: 8 whole lines.  One
+// launch packs every layer (thread i of the concatenated packed arrays finds
+// its layer in the table); the packed copy lives in the caller's workspace.
+struct PinnPack {
+  const float *w[kMaxChainLayers];
+  int64_t off[kMaxChainLayers + 1];  // packed float offsets, off[L] = total
+  int in[kMaxChainLayers];
+  int L;
+};
+__global__ void pinn_pack_kernel(PinnPack pk, float *__restrict__ P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= pk.off[pk.L]) return;
+  int l = 0;
+  while (l + 1 < pk.L && i >= pk.off[l + 1]) ++l;
+  const int64_t q = i - pk.off[l];
+  const int in = pk.in[l], KB = in / 16;
+  const int e = (int)(q & 3), lane = (int)((q >> 2) & 63);
+  const int64_t r = q >> 8;  // t * KB + kb
+  const int kb = (int)(r % KB), t = (int)(r / KB);
+  P[i] = pk.w[l][(int64_t)(16 * t + (lane & 15)) * in + 16 * kb + 4 * (lane >> 4) + e];
+}
+
+// floats of the packed copy for L layers (pinn_fused_ok shapes)
+int64_t pinn_packed_floats(int D, int H, int L) {
+  int64_t n = 0;
+  for (int l = 0; l < L; ++l) n += (int64_t)(l == 0 ? D : H) * (l == L - 1 ? D : H);
+  return n;
+}
+
+hipError_t pinn_fused(const PinnW &w0, const float *state0, float *final_state, int64_t B, int T, float *traj,
+                      void *ws, hipStream_t s) {
   const int64_t blocks = (B + kPinnIcs - 1) / kPinnIcs;
   if (blocks > 0x7fffffff) return hipErrorInvalidValue;
+  PinnW w = w0;
+  PinnPack pk{};
+  pk.L = w.L;
+  float *packed = static_cast<float *>(ws);  // >= pinn_packed_floats(D, H, kMaxChainLayers) floats (caller-checked)
+  for (int l = 0; l < w.L; ++l) {
+    pk.w[l] = w.w[l];
+    pk.in[l] = l == 0 ? w.D : w.H;
+    pk.off[l + 1] = pk.off[l] + (int64_t)pk.in[l] * (l == w.L - 1 ? w.D : w.H);
+    w.wp[l] = packed + pk.off[l];
+  }
+  hipLaunchKernelGGL(pinn_pack_kernel, dim3((unsigned)((pk.off[w.L] + 255) / 256)), dim3(256), 0, s, pk, packed);
   hipLaunchKernelGGL((pinn_run_kernel<192, 256>), dim3((unsigned)blocks), dim3(64 * kPinnWaves), 0, s, w, state0, final_state,
                      traj, B, T);
   return hipGetLastError();
@@ -537,9 +664,9 @@ hipError_t launch_pure_gnn_run(const float *params, int H, int L, const float *s
   const int64_t N = (int64_t)B * nx, S = 3LL * nx;
   const int64_t ldt = (T + 1) * S;
   hipError_t e;
-  if (HF_PURE_FUSED && T > 0 && pure_fused_ok(H, nx))  // one launch (it writes trajectory row 0 itself; no workspace)
-    return H == 64 ? pure_fused_h<64>(w, state0, final_state, x, B, nx, T, traj, s)
-                   : pure_fused_h<128>(w, state0, final_state, x, B, nx, T, traj, s);
+  if (HF_PURE_FUSED && T > 0 && pure_fused_ok(H, nx))  // one launch (it writes trajectory row 0 itself; ws: packed weights)
+    return H == 64 ? pure_fused_h<64>(w, state0, final_state, x, B, nx, T, traj, ws, s)
+                   : pure_fused_h<128>(w, state0, final_state, x, B, nx, T, traj, ws, s);
   if (traj && (e = hipMemcpy2DAsync(traj, sizeof(float) * ldt, state0, sizeof(float) * S, sizeof(float) * S, B,
                                     hipMemcpyDeviceToDevice, s)))
     return e;
@@ -565,19 +692,23 @@ int64_t pinn_ws_bytes(int D, int H, int64_t B) {
 }
 
 int64_t pure_gnn_run_ws_bytes(int H, int B, int nx, int T) {
-  if (B == 0 || T == 0 || (HF_PURE_FUSED && pure_fused_ok(H, nx))) return 0;
+  if (B == 0 || T == 0) return 0;
+  if (HF_PURE_FUSED && pure_fused_ok(H, nx))  // the packed weights, for up to kMaxChainLayers layers
+    return (int64_t)a256(sizeof(float) * pure_packed_floats(H, kMaxChainLayers));
   return pure_gnn_ws_bytes(H, (int64_t)B * nx, 2LL * B * nx);
 }
 
 int64_t pinn_run_ws_bytes(int D, int H, int64_t B) {
-  // the one-launch shape needs no scratch for any layer count the ABI admits
-  return (B == 0 || pinn_fused_ok(D, H, 2)) ? 0 : pinn_ws_bytes(D, H, B);
+  // the one-launch shape: the packed weight copy, sized for the most layers the ABI admits
+  if (B == 0) return 0;
+  return pinn_fused_ok(D, H, 2) ? (int64_t)a256(sizeof(float) * pinn_packed_floats(D, H, kMaxChainLayers))
+                                : pinn_ws_bytes(D, H, B);
 }
 
 hipError_t launch_pinn_forward(const float *params, int D, int H, int L, const float *state, float *out, int64_t B,
                                void *ws, hipStream_t s) {
   const PinnW w = pinn_view(params, D, H, L);
-  if (pinn_fused_ok(D, H, L)) return B > 0 ? pinn_fused(w, state, out, B, 1, nullptr, s) : hipSuccess;
+  if (pinn_fused_ok(D, H, L)) return B > 0 ? pinn_fused(w, state, out, B, 1, nullptr, ws, s) : hipSuccess;
   float *buf[2] = {static_cast<float *>(ws),
                    reinterpret_cast<float *>(static_cast<char *>(ws) + a256(sizeof(float) * B * H))};
   const float *in = state;
@@ -599,8 +730,9 @@ hipError_t launch_pinn_run(const float *params, int D, int H, int L, const float
                            int64_t B, int T, float *traj, void *ws, hipStream_t s) {
   const size_t row = sizeof(float) * D, ldt = row * (T + 1);
   hipError_t e;
-  // one launch (the kernel writes trajectory row 0 itself; no workspace)
-  if (T > 0 && pinn_fused_ok(D, H, L)) return pinn_fused(pinn_view(params, D, H, L), state0, final_state, B, T, traj, s);
+  // one launch (the kernel writes trajectory row 0 itself; the workspace holds the packed weights)
+  if (T > 0 && pinn_fused_ok(D, H, L))
+    return B > 0 ? pinn_fused(pinn_view(params, D, H, L), state0, final_state, B, T, traj, ws, s) : hipSuccess;
   if (traj && (e = hipMemcpy2DAsync(traj, ldt, state0, row, row, B, hipMemcpyDeviceToDevice, s))) return e;
   if (T == 0) return hipMemcpyAsync(final_state, state0, row * B, hipMemcpyDeviceToDevice, s);
   char *p = static_cast<char *>(ws) + 2 * a256(sizeof(float) * B * H);  // non-NULL here: hf_pinn_run checks

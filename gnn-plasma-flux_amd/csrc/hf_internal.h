@@ -99,7 +99,7 @@ hipError_t launch_pure_gnn_forward(const float *params, int in_dim, int H, int L
 hipError_t launch_pure_gnn_run(const float *params, int H, int L, const float *state0, float *final_state,
                                const float *x, int B, int nx, int T, float *traj, void *ws, hipStream_t s);
 int64_t pinn_ws_bytes(int D, int H, int64_t B);
-// scratch the rollouts actually use: 0 on their one-launch paths (baselines.hip)
+// scratch the rollouts actually use: the packed weights on their one-launch paths (baselines.hip)
 int64_t pure_gnn_run_ws_bytes(int H, int B, int nx, int T);
 int64_t pinn_run_ws_bytes(int D, int H, int64_t B);
 hipError_t launch_pinn_forward(const float *params, int D, int H, int L, const float *state, float *out, int64_t B,

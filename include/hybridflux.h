@@ -194,10 +194,12 @@ int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const
  * (state <- state + delta, node features [n,u,E,x]) for B ICs on chains of nx
  * cells: state0/final [B][3][nx], traj [B][T+1][3][nx] or NULL; x [nx].
  * Workspace: hf_pure_gnn_workspace_bytes(H, N, E) for hf_pure_gnn_forward;
- * hf_pure_gnn_run_workspace_bytes(H, B, nx, T) for hf_pure_gnn_run, which is 0
- * (dev_workspace may then be NULL) where the rollout is ONE launch for all T
- * steps: nx in {16, 32, 48, 64} with H in {64, 128} (one IC per workgroup,
- * activations in LDS).  Otherwise, on chains whose nx divides 128 with H a multiple of 64,
+ * hf_pure_gnn_run_workspace_bytes(H, B, nx, T) for hf_pure_gnn_run.  The
+ * rollout is ONE launch for all T steps for nx in {16, 32, 48, 64} with H in
+ * {64, 128} (one IC per workgroup, activations in LDS); its workspace holds a
+ * packed copy of the message/output weights made at the start of the call (the
+ * copy for up to 8 layers; with more layers the launch reads nn.Linear's rows
+ * in place).  Otherwise, on chains whose nx divides 128 with H a multiple of 64,
  * each message layer is one f32 MFMA GEMM that forms the messages and the
  * residual in its epilogue (csrc/tgemm.h EpiMsg); other shapes run the generic
  * linear + gather kernels.
@@ -207,9 +209,11 @@ int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const
  * on states flattened to D = 3*nx.  hf_pinn_run = evaluate_multi_ic.py:70-83
  * for B ICs: state0/final [B][D], traj [B][T+1][D] or NULL.  The reference's
  * shape (D = 192, H = 256, 2 <= layers <= 8) runs as ONE launch for all T steps
- * (16 ICs per workgroup, activations in LDS; hf_pinn_forward is its T = 1):
- * hf_pinn_workspace_bytes is 0 for it and dev_workspace may be NULL; other
- * shapes run per-layer GEMMs through the workspace.
+ * (16 ICs per workgroup, activations in LDS; hf_pinn_forward is its T = 1),
+ * whose workspace holds a packed copy of the weights made at the start of the
+ * call (hf_pinn_workspace_bytes: the copy for the largest layer count, 8);
+ * other shapes run per-layer GEMMs through the workspace.  B = 0 or T = 0
+ * needs none.
  */
 int64_t hf_pure_gnn_param_count(int in_dim, int hidden, int layers);
 int64_t hf_pure_gnn_workspace_bytes(int hidden, int64_t N, int64_t E);

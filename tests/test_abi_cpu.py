@@ -224,17 +224,20 @@ def test_workspace_need_classical():
 
 
 def test_baseline_rollout_workspace_queries():
-    """hf_pure_gnn_run_workspace_bytes / hf_pinn_workspace_bytes: 0 on the
-    one-launch rollouts (the workspace may then be NULL), the per-step GEMMs'
-    scratch otherwise, -1 on bad arguments (no GPU needed)."""
+    """hf_pure_gnn_run_workspace_bytes / hf_pinn_workspace_bytes: the packed
+    weight copy (for up to 8 layers) of the one-launch PureGNN and PINN
+    rollouts, the per-step GEMMs' scratch otherwise, -1 on bad arguments (no
+    GPU needed)."""
     from hybridflux._lib import lib
     L = lib()
     for H, nx in ((64, 16), (128, 64), (64, 48)):
-        assert L.hf_pure_gnn_run_workspace_bytes(H, 4096, nx, 50) == 0
+        assert L.hf_pure_gnn_run_workspace_bytes(H, 4096, nx, 50) == 4 * (8 * 2 * H * H + H * H)
     assert L.hf_pure_gnn_run_workspace_bytes(128, 7, 100, 5) == L.hf_pure_gnn_workspace_bytes(128, 700, 1400) > 0
     assert L.hf_pure_gnn_run_workspace_bytes(96, 7, 64, 5) > 0      # H not in {64, 128}: per-step path
     assert L.hf_pure_gnn_run_workspace_bytes(128, 7, 100, 0) == 0   # T = 0 only copies
     assert L.hf_pure_gnn_run_workspace_bytes(0, 7, 64, 5) == -1
-    assert L.hf_pinn_workspace_bytes(192, 256, 4096) == 0
+    # the one-launch PINN rollout: a packed copy of the weights for up to 8 layers
+    assert L.hf_pinn_workspace_bytes(192, 256, 4096) == 4 * (192 * 256 + 6 * 256 * 256 + 256 * 192)
+    assert L.hf_pinn_workspace_bytes(192, 256, 0) == 0
     assert L.hf_pinn_workspace_bytes(96, 128, 7) > 0
     assert L.hf_pinn_workspace_bytes(0, 128, 7) == -1

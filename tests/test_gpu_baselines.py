@@ -85,11 +85,12 @@ def test_pure_gnn_rollout_vs_reference(models):
 
 
 @pytest.mark.parametrize("H,nx,L,B", [(128, 64, 4, 3), (64, 64, 3, 2), (128, 32, 2, 5), (64, 16, 1, 3),
-                                       (128, 48, 0, 2), (64, 100, 2, 2)])
+                                       (128, 48, 0, 2), (64, 100, 2, 2), (64, 32, 8, 2), (64, 32, 10, 2)])
 def test_pure_gnn_rollout_shapes_vs_oracle(H, nx, L, B):
     """PureGNN(4, H, L) rollouts vs the oracle restatement (evaluate_multi_ic.py:45-66):
     nx in {16, 32, 48, 64} with H in {64, 128} run the one-launch kernel (one IC per
-    workgroup), nx = 100 the per-step GEMMs; T = 0 returns the initial state."""
+    workgroup) on packed weights (L <= 8) or nn.Linear's rows (L = 10), nx = 100
+    the per-step GEMMs; T = 0 returns the initial state."""
     import hybridflux as hf
     torch.manual_seed(H + nx + L)
     pg = hf.PureGNN(4, H, L).to(DEV)
