@@ -212,7 +212,7 @@ PinnW pinn_view(const float *p, int D, int H, int L) {
 // v_mfma_f32_16x16x4_f32 tiles (16 output features x 16 ICs) whose weight
 // operand is read from a packed copy of nn.Linear's rows in the caller's
 // workspace (pinn_pack_kernel: each wave's k-block one contiguous 1 KiB;
-// L2-resident: 0.9 MB), four k-blocks in flight.  The k order inside a
+// L2-resident: 0.9 MB), kPinnAhead k-blocks in flight.  The k order inside a
 // 16-block is permuted so that a lane's four MFMA steps read one float4 of its
 // weight row (k = 16 kb + 4 (lane >> 4) + step); the activations use the same
 // order, so LDS holds them as [k-block][lane][4]: an MFMA output tile is
@@ -227,57 +227,68 @@ constexpr int kPinnIcs = 16;
 // waves per workgroup: 16 (four per SIMD, one output tile each) measured 7 %
 // faster than 4 and 3 % faster than 8 (profiles/r03_pinn_ab.txt)
 constexpr int kPinnWaves = HF_PINN_WAVES;
+#ifndef HF_PINN_AHEAD
+#define HF_PINN_AHEAD 4
+#endif
+// weight k-blocks in flight per wave (pinn_layer's software pipeline)
+constexpr int kPinnAhead = HF_PINN_AHEAD;
 
-// One layer on this wave's output tiles t = wave + kPinnWaves * j (j < NT) of
-// NTILES: out = act(W in + b) (ACT 0: tanh; 1: the last layer, state += W in + b).
-template <int K, int NTILES, int ACT>
-__device__ __forceinline__ void pinn_layer(const float *__restrict__ W, const float *__restrict__ bias,
-                                           const float *in, float *out, int wave, int lane) {
-  constexpr int NT = (NTILES + kPinnWaves - 1) / kPinnWaves;
-  constexpr int KB = K / 16, P = 4;
-  const int g = lane >> 4;
-  f4v acc[NT];
-  const float *wrow[NT];
+// One layer on this wave's output tile t = min(wave, NTILES - 1) (a spare
+// tile's result is not stored): out = act(W in + b) (ACT 0: tanh; 1: the last
+// layer, state += W in + b).  wrow / nrow: this wave's packed weight row of
+// this layer / of the layer after it (KBN k-blocks; the next step's layer 0
+// after the last layer).
+//
+// The weight stream of a step is one software pipeline over all its layers:
+// wq holds k-blocks c .. c+P-1 of the stream, the last P-1 iterations of a
+// layer load the next layer's first P-1 k-blocks (so no layer starts on an L2
+// round trip; loads stay in flight across the workgroup barrier, which waits
+// on LDS only), and each iteration ends in a scheduling barrier, so the
+// compiler cannot sink a load down to its use (left to itself it issued each
+// load right before its MFMAs and waited for it there).  The B fragment of
+// k-block c+1 is read from LDS under c's MFMAs; the bias comes from LDS too
+// (copied there once: a global bias load would be sunk into the store's branch
+// and waited for there behind the next layer's k-blocks, vmcnt being in order).
+template <int K, int NTILES, int ACT, int KBN>
+__device__ __forceinline__ void pinn_layer(const float *__restrict__ wrow, const float *bias,
+                                           const float *in, float *out, int wave, int lane, f4v (&wq)[kPinnAhead],
+                                           const float *__restrict__ nrow) {
+  constexpr int KB = K / 16, P = kPinnAhead;
+  static_assert(KB % P == 0 && KBN >= P - 1, "a layer's k-blocks fill whole rounds of the ring");
+  const int t = wave < NTILES ? wave : NTILES - 1;
+  f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+  f4v bv = *reinterpret_cast<const f4v *>(in + lane * 4);
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
-    const int t = wave + kPinnWaves * j < NTILES ? wave + kPinnWaves * j : NTILES - 1;  // a spare tile: not stored
-    wrow[j] = W + ((int64_t)t * KB * 64 + lane) * 4;  // packed: k-block kb at + 256 kb, one contiguous 1 KiB per wave
+  for (int c = 0; c < KB; ++c) {
+    constexpr int kAhead = P - 1;
+    const int s = c + kAhead;  // slot s % P held k-block c - 1, consumed last iteration
+    if (s < KB)
+      wq[s % P] = *reinterpret_cast<const f4v *>(wrow + 256 * s);
+    else
+      wq[s % P] = *reinterpret_cast<const f4v *>(nrow + 256 * (s - KB));
+    f4v bn = bv;
+    if (c + 1 < KB) bn = *reinterpret_cast<const f4v *>(in + (c + 1) * 256 + lane * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][e], bv[e], acc, 0, 0, 0);
+    bv = bn;
+    __builtin_amdgcn_sched_barrier(0);
   }
-  f4v wq[P][NT];  // k-blocks c .. c + P - 1 in flight while c is multiplied
+  if (NTILES % kPinnWaves != 0 && wave >= NTILES) return;
+  float *o = out + t * 256 + lane * 4;
+  const f4v bq = *reinterpret_cast<const f4v *>(bias + 16 * t + 4 * (lane >> 4));
+  f4v v;
 #pragma unroll
-  for (int kb = 0; kb < KB + P - 1; ++kb) {
-    if (kb < KB) {  // slot kb % P held k-block kb - P, consumed last iteration
+  for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(acc[i], bq[i]);
+  if (ACT == 0) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) wq[kb % P][j] = *reinterpret_cast<const f4v *>(wrow[j] + 256 * kb);
-    }
-    if (kb >= P - 1) {
-      const int c = kb - (P - 1);
-      const f4v bv = *reinterpret_cast<const f4v *>(in + c * 256 + lane * 4);
+    for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+  } else {
+    const f4v st = *reinterpret_cast<const f4v *>(o);
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j], 0, 0, 0);
-    }
+    for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(st[i], v[i]);
   }
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int t = wave + kPinnWaves * j;
-    if (NTILES % kPinnWaves != 0 && t >= NTILES) break;
-    float *o = out + t * 256 + lane * 4;
-    f4v v;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(acc[j][i], bias[16 * t + 4 * g + i]);
-    if (ACT == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
-    } else {
-      const f4v st = *reinterpret_cast<const f4v *>(o);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(st[i], v[i]);
-    }
-    *reinterpret_cast<f4v *>(o) = v;
-  }
+  *reinterpret_cast<f4v *>(o) = v;
 }
 
 // LDS index of feature k of IC n in the [k-block][lane][4] order above
@@ -288,9 +299,11 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
                                                           float *__restrict__ final_state, float *__restrict__ traj,
                                                           int64_t B, int T) {
   static_assert(D % 16 == 0 && H % 16 == 0, "16-feature tiles");
+  static_assert(kPinnWaves >= H / 16 && kPinnWaves >= D / 16, "one output tile per wave");
   constexpr int NTH = 64 * kPinnWaves;
   __shared__ f4v s_state4[D * kPinnIcs / 4];
   __shared__ f4v s_act4[2][H * kPinnIcs / 4];
+  __shared__ f4v s_bias4[kMaxChainLayers * H / 4];  // layer l's bias at l * H
   float *s_state = reinterpret_cast<float *>(s_state4);
   float *const act0 = reinterpret_cast<float *>(s_act4[0]), *const act1 = reinterpret_cast<float *>(s_act4[1]);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -304,17 +317,32 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
     s_state[pinn_at(d, n)] = v;
     if (traj && b0 + n < B) traj[b * ldt + d] = v;
   }
-  __syncthreads();
   const int L = w.L;
+  float *const s_bias = reinterpret_cast<float *>(s_bias4);
+  for (int l = 0; l < L; ++l)
+    for (int i = tid; i < (l == L - 1 ? D : H); i += NTH) s_bias[l * H + i] = w.b[l][i];
+  __syncthreads();
+  // this wave's packed weight row of layer l: output tile min(wave, tiles - 1), k-block 0
+  auto row = [&](int l) {
+    const int tiles = l == L - 1 ? D / 16 : H / 16, kb = l == 0 ? D / 16 : H / 16;
+    return w.wp[l] + ((int64_t)(wave < tiles ? wave : tiles - 1) * kb * 64 + lane) * 4;
+  };
+  f4v wq[kPinnAhead];
+  {
+    const float *r0 = row(0);
+#pragma unroll
+    for (int kb = 0; kb < kPinnAhead - 1; ++kb) wq[kb] = *reinterpret_cast<const f4v *>(r0 + 256 * kb);
+  }
   for (int t = 0; t < T; ++t) {
-    const float *const *WW = w.wp;  // packed weights
-    pinn_layer<D, H / 16, 0>(WW[0], w.b[0], s_state, act0, wave, lane);
+    pinn_layer<D, H / 16, 0, H / 16>(row(0), s_bias, s_state, act0, wave, lane, wq, row(1));
     __syncthreads();
     for (int l = 1; l < L - 1; ++l) {
-      pinn_layer<H, H / 16, 0>(WW[l], w.b[l], (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane);
+      pinn_layer<H, H / 16, 0, H / 16>(row(l), s_bias + l * H, (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane, wq,
+                                       row(l + 1));
       __syncthreads();
     }
-    pinn_layer<H, D / 16, 1>(WW[L - 1], w.b[L - 1], (L & 1) ? act1 : act0, s_state, wave, lane);
+    pinn_layer<H, D / 16, 1, D / 16>(row(L - 1), s_bias + (L - 1) * H, (L & 1) ? act1 : act0, s_state, wave, lane, wq,
+                                     row(0));
     __syncthreads();
     if (traj) {
       for (int idx = tid; idx < kPinnIcs * D; idx += NTH) {
@@ -407,25 +435,30 @@ __device__ __forceinline__ void pure_tiles_packed(const float *base, const float
 #pragma unroll
     for (int g = 0; g < NC; ++g) acc[j][g] = f4v{0.f, 0.f, 0.f, 0.f};
   }
+  // explicit software pipeline, as pinn_layer: k-blocks c+1 .. c+P-1 in flight
+  // while c is multiplied, one scheduling region per k-block
   f4v wq[P][NR];
 #pragma unroll
-  for (int kb = 0; kb < KB + P - 1; ++kb) {
-    if (kb < KB) {
+  for (int kb = 0; kb < P - 1; ++kb)
 #pragma unroll
-      for (int j = 0; j < NR; ++j) wq[kb % P][j] = *reinterpret_cast<const f4v *>(wr[j] + 256 * kb);
+    for (int j = 0; j < NR; ++j) wq[kb][j] = *reinterpret_cast<const f4v *>(wr[j] + 256 * kb);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < KB; ++c) {
+    if (c + P - 1 < KB) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j) wq[(c + P - 1) % P][j] = *reinterpret_cast<const f4v *>(wr[j] + 256 * (c + P - 1));
     }
-    if (kb >= P - 1) {
-      const int c = kb - (P - 1);
 #pragma unroll
-      for (int g = 0; g < NC; ++g) {
-        const f4v bv = *reinterpret_cast<const f4v *>(act + ((c * NC + g) * 64 + lane) * 4);
+    for (int g = 0; g < NC; ++g) {
+      const f4v bv = *reinterpret_cast<const f4v *>(act + ((c * NC + g) * 64 + lane) * 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+      for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int j = 0; j < NR; ++j)
-            acc[j][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j][g], 0, 0, 0);
-      }
+        for (int j = 0; j < NR; ++j)
+          acc[j][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j][g], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 // rows r0 + 16 u + (lane & 15), columns c0 + 16 kb + 4 (lane >> 4) + e of a row-major [*][ld] matrix

@@ -683,7 +683,12 @@ struct CoreBF16 {
       pair0_first<MT>(R, F, X, S.bl, g4, acc0);
       pairs_rest<MT>(R, F, X, S.bl, g4, acc0, pend, park, lane, sm);
     }
-    for (int l = 1; l < W.layers; ++l) {
+    // the layer count as a scalar: read from W as is, the compiler kept the
+    // loop's trip counter in a VGPR, spilled it (256 VGPRs are in use) and
+    // reloaded it with a scratch load whose s_waitcnt vmcnt(0) at the loop
+    // latch also waited out the ring's in-flight DMA every layer
+    const int nl = __builtin_amdgcn_readfirstlane(W.layers);
+    for (int l = 1; l < nl; ++l) {
       const float *bias = S.bl + l * kH;
       Pair<MT> acc0;
       pair0_after<MT>(R, F, X, bias, g4, acc0, pend, park, lane, sm);

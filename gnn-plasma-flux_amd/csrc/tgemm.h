@@ -68,6 +68,10 @@ struct VPlain {
     c = c < cols ? c : cols - 4;
     return *reinterpret_cast<const f4 *>(p + (unsigned)(w.off + c));
   }
+  // two-phase form (tgemm_kernel): load2 issues the loads, combine forms the value
+  static constexpr bool kTwo = false;
+  __device__ void load2(const Row &w, int c, f4 &a, f4 &) const { a = load4(w, c); }
+  __device__ f4 combine(int, const f4 &a, const f4 &) const { return a; }
   bool fits32() const { return rows * ld + cols + (rows >> hshift) * hoff < (int64_t(1) << 31); }
 };
 constexpr int kNoSplit = 62;
@@ -88,12 +92,22 @@ struct VStencil {
     const int64_t nr = r + (i == nx - 1 ? 1 - nx : 1), pr = r + (i == 0 ? nx - 1 : -1);
     return Row{(int)(r * C), (int)(nr * C - C), (int)(pr * C - C)};
   }
-  __device__ f4 load4(const Row &w, int c) const {
+  // Two-phase: load2 issues two loads (the two neighbour rows, or the row
+  // itself twice for c < C: branch-free, the second is an L1 hit), combine forms
+  // (a + b) * 0.5 later, when the stage is written to LDS.  The one-call form
+  // made the compiler wait for both loads right where they were issued, at the
+  // start of the stage, before its MFMAs; a branch on c < C (uniform only when
+  // C is a multiple of the stage depth) spilled the pair to scratch.
+  static constexpr bool kTwo = true;
+  __device__ void load2(const Row &w, int c, f4 &a, f4 &b) const {
     c = c < 2 * C ? c : 2 * C - 4;
-    if (c < C) return *reinterpret_cast<const f4 *>(X + (unsigned)(w.self + c));
-    const f4 a = *reinterpret_cast<const f4 *>(X + (unsigned)(w.nxt + c));
-    const f4 b = *reinterpret_cast<const f4 *>(X + (unsigned)(w.prv + c));
-    return (a + b) * 0.5f;
+    const bool self = c < C;
+    a = *reinterpret_cast<const f4 *>(X + (unsigned)((self ? w.self : w.nxt) + c));
+    b = *reinterpret_cast<const f4 *>(X + (unsigned)((self ? w.self : w.prv) + c));
+  }
+  __device__ f4 combine(int c, const f4 &a, const f4 &b) const {
+    c = c < 2 * C ? c : 2 * C - 4;
+    return c < C ? a : (a + b) * 0.5f;
   }
   bool fits32() const { return rows * C + C < (int64_t(1) << 31); }
 };
@@ -167,6 +181,9 @@ struct VPQ {
     c = c < H ? c : H - 4;
     return *reinterpret_cast<const f4 *>(W + (unsigned)(w.off + c));
   }
+  static constexpr bool kTwo = false;
+  __device__ void load2(const Row &w, int c, f4 &a, f4 &) const { a = load4(w, c); }
+  __device__ f4 combine(int, const f4 &a, const f4 &) const { return a; }
   bool fits32() const { return 2LL * H * H < (int64_t(1) << 31); }
 };
 
@@ -252,6 +269,8 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
   constexpr int kDepth = HF_TG_DEPTH;  // stages of loads in flight: 1 (double buffer) and 2 measured equal
   // (profiles/r03_train_gemm_depth_ab.txt); 1 holds ~30 fewer registers
   f4 ra[kDepth][kNQ], rbv[kDepth][kNQ], csum = f4{0.f, 0.f, 0.f, 0.f};
+  // second loads of two-phase views (the stencil's neighbour rows)
+  f4 ra2[LA::kTwo ? kDepth : 1][kNQ], rb2[LB::kTwo ? kDepth : 1][kNQ];
   // thread -> (global row, col) of its 4 float4 per operand per stage.  The
   // rows of an [i][r] operand are the same every stage: their handles are made once.
   typename LA::Row rowa[kNQ];
@@ -267,40 +286,44 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
   // Branch-free loads: addresses clamped by the views; only reduction rows
   // past the split's end (RM operands) are zeroed, by select.  [i][r]
   // operands need R % kKC == 0 (host-checked), so their r never runs past re.
+  // operand column of load q of the stage at r0 (the view's c)
+  auto col_a = [&](int q, int64_t r0) {
+    const int idx = t + 256 * q;
+    return ARM ? (int)(i0 + 4 * (idx & 31)) : (int)(r0 + 4 * (idx & ((1 << kIMSh) - 1)));
+  };
+  auto col_b = [&](int q, int64_t r0) {
+    const int idx = t + 256 * q;
+    return BRM ? (int)(j0 + 4 * (idx & 31)) : (int)(r0 + 4 * (idx & ((1 << kIMSh) - 1)));
+  };
+  // issues the stage's loads only; lstore forms the values (view combine, the
+  // zeroed reduction rows past the split's end) when it writes them to LDS
   auto gload = [&](int set, int64_t r0) {
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
       const int idx = t + 256 * q;
-      if (ARM) {
-        const f4 v = ga.load4(ga.row(r0 + (idx >> 5)), (int)(i0 + 4 * (idx & 31)));
-        const bool in = r0 + (idx >> 5) < re;
-        ra[set][q] = f4{in ? v[0] : 0.f, in ? v[1] : 0.f, in ? v[2] : 0.f, in ? v[3] : 0.f};
-      } else {
-        ra[set][q] = ga.load4(rowa[q], (int)(r0 + 4 * (idx & ((1 << kIMSh) - 1))));
-      }
-      if (BRM) {
-        const f4 v = gb.load4(gb.row(r0 + (idx >> 5)), (int)(j0 + 4 * (idx & 31)));
-        const bool in = r0 + (idx >> 5) < re;
-        rbv[set][q] = f4{in ? v[0] : 0.f, in ? v[1] : 0.f, in ? v[2] : 0.f, in ? v[3] : 0.f};
-      } else {
-        rbv[set][q] = gb.load4(rowb[q], (int)(r0 + 4 * (idx & ((1 << kIMSh) - 1))));
-      }
+      ga.load2(ARM ? ga.row(r0 + (idx >> 5)) : rowa[q], col_a(q, r0), ra[set][q], ra2[LA::kTwo ? set : 0][q]);
+      gb.load2(BRM ? gb.row(r0 + (idx >> 5)) : rowb[q], col_b(q, r0), rbv[set][q], rb2[LB::kTwo ? set : 0][q]);
     }
   };
-  auto lstore = [&](int buf, int set) {
+  auto lstore = [&](int buf, int set, int64_t r0) {
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
       const int idx = t + 256 * q, im = (1 << kIMSh) - 1;
+      f4 va = ga.combine(col_a(q, r0), ra[set][q], ra2[LA::kTwo ? set : 0][q]);
+      f4 vb = gb.combine(col_b(q, r0), rbv[set][q], rb2[LB::kTwo ? set : 0][q]);
+      const bool in = r0 + (idx >> 5) < re;
+      if (ARM) va = f4{in ? va[0] : 0.f, in ? va[1] : 0.f, in ? va[2] : 0.f, in ? va[3] : 0.f};
+      if (BRM) vb = f4{in ? vb[0] : 0.f, in ? vb[1] : 0.f, in ? vb[2] : 0.f, in ? vb[3] : 0.f};
       float *pa = ARM ? &sA[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sA[buf][(idx >> kIMSh) * kStrIM + 4 * (idx & im)];
       float *pb = BRM ? &sB[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sB[buf][(idx >> kIMSh) * kStrIM + 4 * (idx & im)];
-      *reinterpret_cast<f4 *>(pa) = ra[set][q];
-      *reinterpret_cast<f4 *>(pb) = rbv[set][q];
-      if (COLSUM) csum += ra[set][q];
+      *reinterpret_cast<f4 *>(pa) = va;
+      *reinterpret_cast<f4 *>(pb) = vb;
+      if (COLSUM) csum += va;
     }
   };
   if (rb < re) {
     gload(0, rb);
-    lstore(0, 0);
+    lstore(0, 0, rb);
     if (kDepth == 2 && rb + kKC < re) gload(kDepth - 1, rb + kKC);
   }
   __syncthreads();
@@ -344,7 +367,7 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
 #pragma unroll
           for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][s], bv[b][s], acc[a][b], 0, 0, 0);
     }
-    if (r0 + kKC < re) lstore(cur ^ 1, (cur ^ 1) % kDepth);
+    if (r0 + kKC < re) lstore(cur ^ 1, (cur ^ 1) % kDepth, r0 + kKC);
     __syncthreads();
   };
   for (int64_t r0 = rb; r0 < re;) {
