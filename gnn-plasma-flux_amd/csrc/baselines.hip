@@ -282,7 +282,7 @@ __device__ __forceinline__ void pinn_layer(const float *__restrict__ wrow, const
   for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(acc[i], bq[i]);
   if (ACT == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+    for (int i = 0; i < 4; ++i) v[i] = tanh_fast(v[i]);
   } else {
     const f4v st = *reinterpret_cast<const f4v *>(o);
 #pragma unroll
@@ -507,7 +507,7 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
       v = __fmaf_rn(wi[1], s_st[NX + c], v);
       v = __fmaf_rn(wi[2], s_st[2 * NX + c], v);
       v = __fmaf_rn(wi[3], s_x[c], v);
-      act[pure_act_idx<NC>(f, c)] = tanhf(__fadd_rn(v, w.b_in[f]));
+      act[pure_act_idx<NC>(f, c)] = tanh_fast(__fadd_rn(v, w.b_in[f]));
     }
     __syncthreads();
     for (int l = 0; l < w.L; ++l) {
@@ -531,8 +531,8 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
           const float pl = g > 0 ? acc[0][g - 1][i] : dpp_ror(acc[0][NC - 1][i], 0);
           const float pr = g < NC - 1 ? acc[0][g + 1][i] : dpp_ror(acc[0][0][i], 1);
           const float qv = acc[1][g][i];
-          float m = tanhf(__fadd_rn(__fadd_rn(pl, qv), bq[i]));
-          m = __fadd_rn(m, tanhf(__fadd_rn(__fadd_rn(pr, qv), bq[i])));
+          float m = tanh_fast(__fadd_rn(__fadd_rn(pl, qv), bq[i]));
+          m = __fadd_rn(m, tanh_fast(__fadd_rn(__fadd_rn(pr, qv), bq[i])));
           h[i] = __fadd_rn(h[i], m);
         }
         *reinterpret_cast<f4v *>(hp) = h;
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
       for (int g = 0; g < NC; ++g) {
         f4v o;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = tanhf(__fadd_rn(acc[0][g][i], bo[i]));
+        for (int i = 0; i < 4; ++i) o[i] = tanh_fast(__fadd_rn(acc[0][g][i], bo[i]));
         *reinterpret_cast<f4v *>(act + ((u * NC + g) * 64 + lane) * 4) = o;
       }
     }

@@ -22,6 +22,25 @@ namespace hf {
 // one gfx950 v_maximum3_f32, which propagates NaN.
 __device__ __forceinline__ float relu(float x) { return __builtin_elementwise_maximum(x, 0.0f); }
 
+// tanh in f32 for the comparison models' one-launch rollouts (PureGNN, PINN):
+// |x| < 0.55: x + x^3 P(x^2), a degree-4 fit of (tanh x - x) / x^3 (<= 0.8 ulp
+// evaluated in f32); otherwise 1 - 2 / (1 + 2^(2|x|/ln 2)) on the hardware
+// v_exp_f32 / v_rcp_f32 (<= 2 ulp), sign restored.  About 15 VALU against the
+// device libm tanhf's 22 (with its exact division); NaN propagates.
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float ax = __builtin_fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(ax * 2.88539008177792681f);
+  const float big = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
+  const float x2 = x * x;
+  float p = -0.006287517491728067f;
+  p = __builtin_fmaf(p, x2, 0.02108195051550865f);
+  p = __builtin_fmaf(p, x2, -0.05385509133338928f);
+  p = __builtin_fmaf(p, x2, 0.13332617282867432f);
+  p = __builtin_fmaf(p, x2, -0.33333319425582886f);
+  const float small = __builtin_fmaf(x * x2, p, x);
+  return ax < 0.55f ? small : __builtin_copysignf(big, x);
+}
+
 // F = f32(0.5 * f32(F_fwd + F_bwd))                 src/hybrid_solver.py:45-48
 __device__ __forceinline__ float face_flux(float ffwd, float fbwd) {
   return __fmul_rn(0.5f, __fadd_rn(ffwd, fbwd));
