@@ -241,3 +241,10 @@ def test_baseline_rollout_workspace_queries():
     assert L.hf_pinn_workspace_bytes(192, 256, 0) == 0
     assert L.hf_pinn_workspace_bytes(96, 128, 7) > 0
     assert L.hf_pinn_workspace_bytes(0, 128, 7) == -1
+    # the one-launch rollouts need their workspace (the packed weights): a NULL
+    # one is refused before any device call
+    dummy = ctypes.c_void_p(1)
+    assert L.hf_pure_gnn_run(dummy, 128, 4, dummy, dummy, dummy, 4096, 64, 50, None, None, None) == _lib.HF_EINVAL
+    assert b"NULL workspace" in L.hf_last_error()
+    assert L.hf_pinn_run(dummy, 192, 256, 4, dummy, dummy, 4096, 50, None, None, None) == _lib.HF_EINVAL
+    assert b"NULL workspace" in L.hf_last_error()
