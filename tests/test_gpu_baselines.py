@@ -117,12 +117,14 @@ def test_pinn_forward_and_rollout_vs_reference(models):
     assert torch.equal(r0["final"], torch.as_tensor(b["ics"], device=DEV))
 
 
-@pytest.mark.parametrize("nx,H,L,B", [(64, 256, 2, 5), (64, 256, 3, 33), (64, 256, 5, 16), (32, 128, 3, 7)])
+@pytest.mark.parametrize("nx,H,L,B", [(64, 256, 2, 5), (64, 256, 3, 33), (64, 256, 5, 16), (64, 256, 8, 17),
+                                       (32, 128, 3, 7)])
 def test_pinn_shapes_vs_oracle(nx, H, L, B):
     """PINN(3 nx, H, L) rollouts vs the oracle restatement (train_pinn.py:48-61):
     the reference's shape (3*64, 256) runs the one-launch kernel (16 ICs per
-    workgroup; B = 5, 33 leave a partial workgroup), other shapes the per-layer
-    GEMMs.  T = 0 returns the initial state; forward() is one rollout step."""
+    workgroup; B = 5, 33, 17 leave a partial workgroup; L = 2 .. 8, the
+    weight pipeline crossing every layer and step boundary), other shapes the
+    per-layer GEMMs.  T = 0 returns the initial state; forward() is one rollout step."""
     import hybridflux as hf
     torch.manual_seed(nx + H + L)
     pn = hf.PINN(3 * nx, H, L).to(DEV)
