@@ -28,12 +28,16 @@ def _coeffs():
 
 
 def _tanh_fast(x, exp_ulp=0, rcp_ulp=0):
+    with np.errstate(all="ignore"):  # inf / NaN inputs: both branches are evaluated, as on the GPU
+        return _tanh_fast_eval(x, exp_ulp, rcp_ulp)
+
+
+def _tanh_fast_eval(x, exp_ulp, rcp_ulp):
     scale, (p0, p1, p2, p3, p4), thr = _coeffs()
     x = x.astype(np.float32)
     ax = np.abs(x)
     arg = (ax * scale).astype(np.float32)
-    with np.errstate(over="ignore"):                                  # 2^(2|x|/ln 2) -> inf for large |x|, as on the GPU
-        e = np.exp2(arg.astype(np.float64)).astype(np.float32)
+    e = np.exp2(arg.astype(np.float64)).astype(np.float32)  # -> inf for large |x|, as on the GPU
     e = (e.astype(np.float64) * (1 + exp_ulp * 2.0 ** -23)).astype(np.float32)
     d = (np.float32(1) + e).astype(np.float32)
     r = (1.0 / d.astype(np.float64)).astype(np.float32)
