@@ -222,10 +222,13 @@ PinnW pinn_view(const float *p, int D, int H, int L) {
 constexpr int kPinnIcs = 16;
 
 #ifndef HF_PINN_WAVES
-#define HF_PINN_WAVES 16
+#define HF_PINN_WAVES 8
 #endif
-// waves per workgroup: 16 (four per SIMD, one output tile each) measured 7 %
-// faster than 4 and 3 % faster than 8 (profiles/r03_pinn_ab.txt)
+// waves per workgroup: 8 (two per SIMD, two output tiles each, sharing each B
+// fragment read).  With the loads serialised (round 3) 16 waves of one tile
+// measured 3 % faster than 8 (profiles/r03_pinn_ab.txt); with the weight
+// stream pipelined 8 waves measure 1.5-2.5 % faster than 16
+// (profiles/r04_pinn_waves_ab.jsonl).
 constexpr int kPinnWaves = HF_PINN_WAVES;
 #ifndef HF_PINN_AHEAD
 #define HF_PINN_AHEAD 4
@@ -233,11 +236,17 @@ constexpr int kPinnWaves = HF_PINN_WAVES;
 // weight k-blocks in flight per wave (pinn_layer's software pipeline)
 constexpr int kPinnAhead = HF_PINN_AHEAD;
 
-// One layer on this wave's output tile t = min(wave, NTILES - 1) (a spare
-// tile's result is not stored): out = act(W in + b) (ACT 0: tanh; 1: the last
-// layer, state += W in + b).  wrow / nrow: this wave's packed weight row of
-// this layer / of the layer after it (KBN k-blocks; the next step's layer 0
-// after the last layer).
+// This wave's packed weight rows of one layer: output tiles wave + kPinnWaves j
+// (j < NT; a spare tile past the layer's last is clamped to it and not stored)
+template <int NT>
+struct PinnRows {
+  const float *p[NT];
+};
+
+// One layer on this wave's NT output tiles: out = act(W in + b) (ACT 0: tanh;
+// 1: the last layer, state += W in + b).  wrow / nrow: this wave's packed
+// weight rows of this layer / of the layer after it (KBN k-blocks; the next
+// step's layer 0 after the last layer).
 //
 // The weight stream of a step is one software pipeline over all its layers:
 // wq holds k-blocks c .. c+P-1 of the stream, the last P-1 iterations of a
@@ -246,49 +255,60 @@ constexpr int kPinnAhead = HF_PINN_AHEAD;
 // on LDS only), and each iteration ends in a scheduling barrier, so the
 // compiler cannot sink a load down to its use (left to itself it issued each
 // load right before its MFMAs and waited for it there).  The B fragment of
-// k-block c+1 is read from LDS under c's MFMAs; the bias comes from LDS too
-// (copied there once: a global bias load would be sunk into the store's branch
-// and waited for there behind the next layer's k-blocks, vmcnt being in order).
-template <int K, int NTILES, int ACT, int KBN>
-__device__ __forceinline__ void pinn_layer(const float *__restrict__ wrow, const float *bias,
-                                           const float *in, float *out, int wave, int lane, f4v (&wq)[kPinnAhead],
-                                           const float *__restrict__ nrow) {
+// k-block c+1 is read from LDS under c's MFMAs (and feeds all NT tiles); the
+// bias comes from LDS too (copied there once: a global bias load would be sunk
+// into the store's branch and waited for there behind the next layer's
+// k-blocks, vmcnt being in order).
+template <int K, int NTILES, int ACT, int KBN, int NT>
+__device__ __forceinline__ void pinn_layer(const PinnRows<NT> &wrow, const float *bias, const float *in, float *out,
+                                           int wave, int lane, f4v (&wq)[kPinnAhead][NT],
+                                           const PinnRows<NT> &nrow) {
   constexpr int KB = K / 16, P = kPinnAhead;
   static_assert(KB % P == 0 && KBN >= P - 1, "a layer's k-blocks fill whole rounds of the ring");
-  const int t = wave < NTILES ? wave : NTILES - 1;
-  f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+  f4v acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
   f4v bv = *reinterpret_cast<const f4v *>(in + lane * 4);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int c = 0; c < KB; ++c) {
     constexpr int kAhead = P - 1;
     const int s = c + kAhead;  // slot s % P held k-block c - 1, consumed last iteration
-    if (s < KB)
-      wq[s % P] = *reinterpret_cast<const f4v *>(wrow + 256 * s);
-    else
-      wq[s % P] = *reinterpret_cast<const f4v *>(nrow + 256 * (s - KB));
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      if (s < KB)
+        wq[s % P][j] = *reinterpret_cast<const f4v *>(wrow.p[j] + 256 * s);
+      else
+        wq[s % P][j] = *reinterpret_cast<const f4v *>(nrow.p[j] + 256 * (s - KB));
+    }
     f4v bn = bv;
     if (c + 1 < KB) bn = *reinterpret_cast<const f4v *>(in + (c + 1) * 256 + lane * 4);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][e], bv[e], acc, 0, 0, 0);
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j], 0, 0, 0);
     bv = bn;
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (NTILES % kPinnWaves != 0 && wave >= NTILES) return;
-  float *o = out + t * 256 + lane * 4;
-  const f4v bq = *reinterpret_cast<const f4v *>(bias + 16 * t + 4 * (lane >> 4));
-  f4v v;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(acc[i], bq[i]);
-  if (ACT == 0) {
+  for (int j = 0; j < NT; ++j) {
+    const int t = wave + kPinnWaves * j;
+    if (NTILES % kPinnWaves != 0 && t >= NTILES) break;
+    float *o = out + t * 256 + lane * 4;
+    const f4v bq = *reinterpret_cast<const f4v *>(bias + 16 * t + 4 * (lane >> 4));
+    f4v v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = tanh_fast(v[i]);
-  } else {
-    const f4v st = *reinterpret_cast<const f4v *>(o);
+    for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(acc[j][i], bq[i]);
+    if (ACT == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(st[i], v[i]);
+      for (int i = 0; i < 4; ++i) v[i] = tanh_fast(v[i]);
+    } else {
+      const f4v st = *reinterpret_cast<const f4v *>(o);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(st[i], v[i]);
+    }
+    *reinterpret_cast<f4v *>(o) = v;
   }
-  *reinterpret_cast<f4v *>(o) = v;
 }
 
 // LDS index of feature k of IC n in the [k-block][lane][4] order above
@@ -299,7 +319,8 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
                                                           float *__restrict__ final_state, float *__restrict__ traj,
                                                           int64_t B, int T) {
   static_assert(D % 16 == 0 && H % 16 == 0, "16-feature tiles");
-  static_assert(kPinnWaves >= H / 16 && kPinnWaves >= D / 16, "one output tile per wave");
+  constexpr int NT = (H / 16 + kPinnWaves - 1) / kPinnWaves;  // output tiles per wave (H >= D)
+  static_assert(H >= D, "the widest layer sets the tiles per wave");
   constexpr int NTH = 64 * kPinnWaves;
   __shared__ f4v s_state4[D * kPinnIcs / 4];
   __shared__ f4v s_act4[2][H * kPinnIcs / 4];
@@ -322,26 +343,34 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
   for (int l = 0; l < L; ++l)
     for (int i = tid; i < (l == L - 1 ? D : H); i += NTH) s_bias[l * H + i] = w.b[l][i];
   __syncthreads();
-  // this wave's packed weight row of layer l: output tile min(wave, tiles - 1), k-block 0
+  // this wave's packed weight rows of layer l: output tiles min(wave + kPinnWaves j, tiles - 1), k-block 0
   auto row = [&](int l) {
     const int tiles = l == L - 1 ? D / 16 : H / 16, kb = l == 0 ? D / 16 : H / 16;
-    return w.wp[l] + ((int64_t)(wave < tiles ? wave : tiles - 1) * kb * 64 + lane) * 4;
-  };
-  f4v wq[kPinnAhead];
-  {
-    const float *r0 = row(0);
+    PinnRows<NT> r;
 #pragma unroll
-    for (int kb = 0; kb < kPinnAhead - 1; ++kb) wq[kb] = *reinterpret_cast<const f4v *>(r0 + 256 * kb);
+    for (int j = 0; j < NT; ++j) {
+      const int t = wave + kPinnWaves * j;
+      r.p[j] = w.wp[l] + ((int64_t)(t < tiles ? t : tiles - 1) * kb * 64 + lane) * 4;
+    }
+    return r;
+  };
+  f4v wq[kPinnAhead][NT];
+  {
+    const PinnRows<NT> r0 = row(0);
+#pragma unroll
+    for (int kb = 0; kb < kPinnAhead - 1; ++kb)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) wq[kb][j] = *reinterpret_cast<const f4v *>(r0.p[j] + 256 * kb);
   }
   for (int t = 0; t < T; ++t) {
-    pinn_layer<D, H / 16, 0, H / 16>(row(0), s_bias, s_state, act0, wave, lane, wq, row(1));
+    pinn_layer<D, H / 16, 0, H / 16, NT>(row(0), s_bias, s_state, act0, wave, lane, wq, row(1));
     __syncthreads();
     for (int l = 1; l < L - 1; ++l) {
-      pinn_layer<H, H / 16, 0, H / 16>(row(l), s_bias + l * H, (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane, wq,
+      pinn_layer<H, H / 16, 0, H / 16, NT>(row(l), s_bias + l * H, (l & 1) ? act0 : act1, (l & 1) ? act1 : act0, wave, lane, wq,
                                        row(l + 1));
       __syncthreads();
     }
-    pinn_layer<H, D / 16, 1, D / 16>(row(L - 1), s_bias + (L - 1) * H, (L & 1) ? act1 : act0, s_state, wave, lane, wq,
+    pinn_layer<H, D / 16, 1, D / 16, NT>(row(L - 1), s_bias + (L - 1) * H, (L & 1) ? act1 : act0, s_state, wave, lane, wq,
                                      row(0));
     __syncthreads();
     if (traj) {

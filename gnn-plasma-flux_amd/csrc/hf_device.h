@@ -25,7 +25,8 @@ __device__ __forceinline__ float relu(float x) { return __builtin_elementwise_ma
 // tanh in f32 for the comparison models' one-launch rollouts (PureGNN, PINN):
 // |x| < 0.55: x + x^3 P(x^2), a degree-4 fit of (tanh x - x) / x^3 (<= 0.8 ulp
 // evaluated in f32); otherwise 1 - 2 / (1 + 2^(2|x|/ln 2)) on the hardware
-// v_exp_f32 / v_rcp_f32 (<= 2 ulp), sign restored.  About 15 VALU against the
+// v_exp_f32 / v_rcp_f32 (<= 2 ulp with both correctly rounded, <= 4 with
+// both one ulp off; tests/test_tanh_fast_cpu.py), sign restored.  About 15 VALU against the
 // device libm tanhf's 22 (with its exact division); NaN propagates.
 __device__ __forceinline__ float tanh_fast(float x) {
   const float ax = __builtin_fabsf(x);
