@@ -22,8 +22,9 @@ FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "--offl
 K32 = ["-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]  # Makefile: K32 cores
 
 
-def scan(path):
-    out = os.path.join("/tmp", os.path.basename(path) + ".s")
+def scan(path, out_dir="/tmp"):
+    """{kernel symbol: {loads, waited_at_issue, loop_vmcnt0, scratch, mfma}} of one .hip file."""
+    out = os.path.join(out_dir, os.path.basename(path) + ".s")
     extra = K32 if os.path.basename(path) in ("chain_k32.hip", "chain_bf16.hip") else []
     subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *extra, path, "-o", out], check=True, cwd=CSRC,
                    stderr=subprocess.DEVNULL)
@@ -50,11 +51,11 @@ def scan(path):
             st["scratch"] += 1
         if "v_mfma" in ln:
             st["mfma"] += 1
-    for k, st in stats.items():
-        if st["mfma"] or st["waited_at_issue"] or st["loop_vmcnt0"] or st["scratch"]:
-            print(os.path.basename(path), k[:100], " ".join(f"{a}={b}" for a, b in st.items()))
+    return stats
 
 
 if __name__ == "__main__":
     for p in sys.argv[1:] or sorted(glob.glob(os.path.join(CSRC, "*.hip"))):
-        scan(os.path.abspath(p))
+        for k, st in scan(os.path.abspath(p)).items():
+            if st["mfma"] or st["waited_at_issue"] or st["loop_vmcnt0"] or st["scratch"]:
+                print(os.path.basename(p), k[:100], " ".join(f"{a}={b}" for a, b in st.items()))
