@@ -17,6 +17,7 @@ and a library built with diagnostic flags is refused.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--ics-per-gpu B] [--no-cpu-baseline]
 """
 import argparse
+import datetime
 import json
 import math
 import os
@@ -26,6 +27,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gnn-plasma-flux_amd"))
 sys.path.insert(0, ROOT)
+# RCCL / CUDA-tensor sharing between processes needs dmabuf IPC on this host
+# driver: set before torch is imported and before anything touches the GPU,
+# whoever launched this process (bench.py's own launcher, torchrun, the
+# driver; tests/test_distributed_cpu.py::test_bench_sets_ipc_mode_torchrun_style)
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -65,17 +71,43 @@ def pinned(n):
     return set(avail[:n])
 
 
-def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=None, also=None, reps=1, warm_s=0.3):
+def timed(fn, dev, reps=1, warm_s=0.3):
+    """Warm `fn` (one rollout / step) back to back for warm_s of wall time, so the
+    timed calls run at the clock the chip sustains on this workload (after the
+    host-side setup the GPU has idled and the clock ramps again,
+    MI355X_MICROARCH.md DVFS), then time `reps` calls back to back: HIP events on
+    the launch stream and the wall clock around them.  Returns (wall s, event ms)."""
+    torch.cuda.synchronize(dev)
+    t_end = time.perf_counter() + warm_s
+    while time.perf_counter() < t_end:
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(reps):  # back to back: only the first pays the launch latency
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0, e0.elapsed_time(e1)
+
+
+def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=None, also=None, reps=1, warm_s=0.3,
+                 tridiag=False):
     """Time one more BASELINE.json single-GPU config the same way as the
     headline (preallocated outputs and workspace, HIP events on the launch
     stream, wall clock around the launches).  Reported next to the headline,
     never as it.  W untimed warmup steps run first as one rollout, then the
-    timed workload itself back to back for warm_s seconds, so the timed
-    rollouts run at the sustained clock rather than in the clock ramp after
-    the host-side setup (the headline keeps the driver's --warmup).  also: the same workload in another precision,
-    timed the same way and reported under alt_<precision>.  fixture: {label: states [n, K+1, 3, nx]} of the batch's first
-    n ICs (committed test vectors); the final states' max |error| against each
-    is reported."""
+    timed workload itself back to back for warm_s seconds (timed()), so the
+    timed rollouts run at the sustained clock (the headline keeps the driver's
+    --warmup).  also: the same workload in another precision, reported under
+    alt_<precision>; tridiag: the same workload with the opt-in tridiagonal
+    Poisson (not the reference's operator), under alt_poisson_tridiagonal.
+    fixture: {label: states [n, K+1, 3, nx]} of the batch's first n ICs
+    (committed test vectors); the final states' max |error| against each is
+    reported."""
     from hybridflux import HybridSolver, engine
     from hybridflux._lib import HF_OP_RUN
     dt = 5e-3 * 64.0 / nx
@@ -84,60 +116,36 @@ def other_config(weights, dev, name, B, nx, precision, K, W, radius, fixture=Non
     ws, _ = engine.workspace(HF_OP_RUN, B, nx, K, dev, model=solver._dm())
     final = torch.empty_like(ics)
     met = torch.empty(B, K + 1, 4, device=dev)
-    # warm-up: the W-step rollout, then the timed workload back to back for at
-    # least warm_s of wall time, so the timed rollouts run at the clock the chip
-    # sustains on this workload (after the host-side setup above the GPU has
-    # idled and the clock ramps again, MI355X_MICROARCH.md DVFS)
     solver.run_batch(ics, max(W, 1), traj=False, ws=ws)
-    torch.cuda.synchronize(dev)
-    t_end = time.perf_counter() + warm_s
-    while time.perf_counter() < t_end:
-        for _ in range(reps):
-            solver.run_batch(ics, K, traj=False, metrics=met, out=final, ws=ws)
-        torch.cuda.synchronize(dev)
-    stream = torch.cuda.current_stream(dev)
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(reps):  # back-to-back rollouts: only the first pays the launch latency
-        solver.run_batch(ics, K, traj=False, metrics=met, out=final, ws=ws)
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    kms = e0.elapsed_time(e1)
-    K = K * reps  # IC-steps timed
-    flop = GNN_FLOP_PER_CELL_STEP * B * nx * K
+    wall, kms = timed(lambda: solver.run_batch(ics, K, traj=False, metrics=met, out=final, ws=ws), dev, reps, warm_s)
+    flop = GNN_FLOP_PER_CELL_STEP * B * nx * K * reps
     peak = PEAK_F32_MFMA_TFLOPS if precision == "f32" else PEAK_F16_MFMA_TFLOPS
-    out = {"workload": name, "ics": B, "nx": nx, "dt": dt, "precision": precision, "steps": K // reps,
+    out = {"workload": name, "ics": B, "nx": nx, "dt": dt, "precision": precision, "steps": K,
            "rollouts": reps,
            "weights": f"W1_r{radius}",
-           "value": round(B * K / wall, 1), "unit": "IC-steps/s", "ms_per_step": round(wall / K * 1e3, 4),
+           "value": round(B * K * reps / wall, 1), "unit": "IC-steps/s", "ms_per_step": round(wall / (K * reps) * 1e3, 4),
            "kernel_ms": round(kms, 3), "mfma_frac": round(flop / (kms * 1e-3) / 1e12 / peak, 4),
            "finite_fraction": float(met[:, -1, 2].float().mean().item())}
+    alts = []
     if also:  # the same workload in another precision (reported beside, not instead)
-        s2 = HybridSolver(weights, radius=radius, nx=nx, dt=dt, device=dev, precision=also)
+        alts.append((f"alt_{also}", "max_abs_diff_vs_f32_final_state", also,
+                     HybridSolver(weights, radius=radius, nx=nx, dt=dt, device=dev, precision=also)))
+    if tridiag:  # the opt-in tridiagonal Poisson, same precision (NOT the reference's operator)
+        alts.append(("alt_poisson_tridiagonal", "max_abs_diff_vs_spectral_final_state", precision,
+                     HybridSolver(weights, radius=radius, nx=nx, dt=dt, device=dev, precision=precision,
+                                  poisson="tridiagonal")))
+    for key, diff_key, prec, s2 in alts:
         final2 = torch.empty_like(ics)
         s2.run_batch(ics, max(W, 1), traj=False, ws=ws)
-        torch.cuda.synchronize(dev)
-        t_end = time.perf_counter() + warm_s
-        while time.perf_counter() < t_end:
-            for _ in range(reps):
-                s2.run_batch(ics, K // reps, traj=False, metrics=met, out=final2, ws=ws)
-            torch.cuda.synchronize(dev)
-        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ta = time.perf_counter()
-        a0.record(stream)
-        for _ in range(reps):
-            s2.run_batch(ics, K // reps, traj=False, metrics=met, out=final2, ws=ws)
-        a1.record(stream)
-        torch.cuda.synchronize(dev)
-        wall2 = time.perf_counter() - ta
-        out[f"alt_{also}"] = {"value": round(B * K / wall2, 1), "kernel_ms": round(a0.elapsed_time(a1), 3),
-                              "max_abs_diff_vs_f32_final_state": float((final2 - final).abs().max().item())}
+        wall2, kms2 = timed(lambda: s2.run_batch(ics, K, traj=False, metrics=met, out=final2, ws=ws), dev, reps,
+                            warm_s)
+        pk = PEAK_F32_MFMA_TFLOPS if prec == "f32" else PEAK_F16_MFMA_TFLOPS
+        out[key] = {"value": round(B * K * reps / wall2, 1), "kernel_ms": round(kms2, 3),
+                    "mfma_frac": round(flop / (kms2 * 1e-3) / 1e12 / pk, 4),
+                    diff_key: float((final2 - final).abs().max().item())}
     for label, want in (fixture or {}).items():
         n = want.shape[0]
-        if want.shape[1] == K // reps + 1:
+        if want.shape[1] == K + 1:
             got = final[:n].cpu().numpy()
             out[f"max_err_vs_{label}"] = float(np.abs(got.astype(np.float64) - want[:, -1]).max())
     return out
@@ -183,6 +191,56 @@ def other_models(dev, B, K, warm_s=0.3):
         out[name] = {"value": round(B * K / wall, 1), "unit": "IC-steps/s", "ics": B, "nx": nx, "steps": K,
                      "kernel_ms": round(kms, 3), "flop_per_ic_step": flop[name],
                      "mfma_frac": round(flop[name] * B * K / (kms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)}
+    return out
+
+
+def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
+    """SURVEY.md 8(f2), timed inside the driver's bench: one optimizer step of
+    the reference trainer's loop (scripts/training/train_ablation.py:119-206:
+    the cfg_name ablation loss, loss.backward(), Adam) on `batch` samples of
+    the reference dataset recipe (DATASET_CONFIG: 50 ICs x 40 steps, nx = 64,
+    generated on the GPU by hybridflux.datagen), FluxGNN(4,128,4) random-init
+    (torch.manual_seed(0)).  Eager, and replaying the captured step
+    (hybridflux.training.GraphedStep); each warmed for warm_s, then `steps`
+    steps timed with HIP events + the wall clock.  FLOPs per sample: FluxGNN
+    forward + backward (tools/bench_train.py flop_per_sample); the loss terms,
+    FV updates and Adam are inside the timed step but not counted."""
+    from hybridflux import ABLATION_CONFIGS, BaselineSolver, FluxGNN
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import FluxDataset, GraphedStep, train_steps
+    from tools.bench_train import flop_per_sample
+    st, ft, sn, x, dt, dx, nu = generate_dataset(out_path=None, device=dev, num_initial_conditions=50,
+                                                 steps_per_ic=40)
+    data = FluxDataset(st, ft, sn, dev)
+    solver = BaselineSolver(64, device=dev)
+    x_dev = torch.as_tensor(x, device=dev)
+    cfg = ABLATION_CONFIGS[cfg_name]
+    fps = flop_per_sample(cfg_name)
+    out = {"metric": f"FluxGNN training samples/s ('{cfg_name}' ablation loss, Adam)", "unit": "samples/s",
+           "batch": batch, "steps": steps, "flop_per_sample": fps,
+           "dataset": "DATASET_CONFIG recipe: 50 ICs x 40 steps, nx=64 (GPU classical rollout)"}
+    best = None
+    for mode in ("eager", "graphed"):
+        graphed = mode == "graphed"
+        torch.manual_seed(0)
+        m = FluxGNN(4, 128, 4).to(dev)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=graphed)
+        gs = GraphedStep(m, opt, data, batch, x_dev, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
+        gen = torch.Generator().manual_seed(1)
+        order = torch.randint(0, len(data), (steps * batch,), generator=gen).to(dev)
+        warm = torch.randint(0, len(data), (8 * batch,), generator=gen).to(dev)
+        train_steps(m, opt, data, warm, batch, x_dev, solver.dt, solver.dx, cfg, solver.grid, graphed=gs)  # + capture
+        wall, kms = timed(lambda: train_steps(m, opt, data, order, batch, x_dev, solver.dt, solver.dx, cfg,
+                                              solver.grid, graphed=gs), dev, 1, warm_s)
+        rate = steps * batch / wall
+        out[mode] = {"value": round(rate, 1), "ms_per_step": round(wall / steps * 1e3, 4),
+                     "kernel_ms": round(kms, 3),
+                     "mfma_frac": round(fps * steps * batch / (kms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)}
+        if best is None or rate > best[1]:
+            best = (mode, rate)
+        del m, opt, gs
+    out["value"] = round(best[1], 1)
+    out["best"] = best[0]
     return out
 
 
@@ -270,17 +328,21 @@ def init_group(backend, world, dev):
             os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", str(world))
+    # a rank that dies before the first collective ends the job within this
+    # bound instead of the 10-minute default (tests/test_distributed_cpu.py)
+    timeout = datetime.timedelta(seconds=float(os.environ.get("HF_DIST_TIMEOUT_S", "120")))
     with _StdoutToStderr():
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         # RCCL sets up its communicator and channels on the first collective
         # (hundreds of ms with the GPU idle): do that here, in the setup, so the
         # timed rollout follows the warmup rollout with no idle gap in between
         # (the clock ramps down when the GPU idles, MI355X_MICROARCH.md DVFS)
         dist.all_reduce(torch.zeros(1, device=dev if backend == "nccl" else "cpu"))
-        torch.cuda.synchronize(dev)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
     return True
 
 
@@ -324,6 +386,7 @@ def main():
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the other single-GPU BASELINE configs (cfg2: 256 ICs f32; cfg4: 4096 ICs x 1024 "
                          "cells bf16), reported under 'other_configs' at N=1")
+    ap.add_argument("--no-train", action="store_true", help="skip the training side line (SURVEY 8(f2))")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -342,6 +405,11 @@ def main():
         raise SystemExit(f"LOCAL_RANK {local} but only {ndev} visible GPU(s); RCCL needs one GPU per rank")
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
+    if os.environ.get("HF_BENCH_EXIT_RANK") == str(rank):
+        # fault injection (tests/test_gpu_distributed.py): this rank vanishes
+        # before the group forms; its peers must fail within HF_DIST_TIMEOUT_S
+        print(f"bench.py: rank {rank} exiting early (HF_BENCH_EXIT_RANK)", file=sys.stderr, flush=True)
+        raise SystemExit(0)
     group_error = None
     try:
         grouped = init_group(args.dist_backend, world, dev)
@@ -448,6 +516,30 @@ def main():
                      "kernel_ms": round(a0.elapsed_time(a1), 3),
                      "max_abs_diff_vs_headline_final_state": dev_err}
         del s2, r2
+    # the north star's tridiagonal Poisson (opt-in, NOT the reference's operator:
+    # include/hybridflux.h HF_POISSON_TRIDIAG), fused into the same persistent
+    # kernel, same ICs / K / precision, timed the same way
+    if not args.no_other_configs:
+        s2 = HybridSolver(weights, radius=3, nx=nx, dt=dt, device=dev, precision=args.precision,
+                          poisson="tridiagonal")
+        s2.run_batch(ics, max(W, 1), traj=not args.no_traj)
+        final2 = torch.empty_like(ics)
+        torch.cuda.synchronize(dev)
+        a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ta = time.perf_counter()
+        a0.record(stream)
+        s2.run_batch(ics, K, traj=traj_buf if traj_buf is not None else False, metrics=met_buf, out=final2)
+        a1.record(stream)
+        torch.cuda.synchronize(dev)
+        wall2 = time.perf_counter() - ta
+        kt = a0.elapsed_time(a1)
+        pk = PEAK_F32_MFMA_TFLOPS if args.precision == "f32" else PEAK_F16_MFMA_TFLOPS
+        alt["poisson_tridiagonal"] = {
+            "value": round(B * K / wall2, 1), "ms_per_step": round(wall2 / K * 1e3, 4), "kernel_ms": round(kt, 3),
+            "mfma_frac": round(GNN_FLOP_PER_CELL_STEP * B * nx * K / (kt * 1e-3) / 1e12 / pk, 4),
+            "max_abs_diff_vs_headline_final_state": float((final2 - final).abs().max().item()),
+            "note": "opt-in cyclic-reduction tridiagonal Poisson (not the reference's spectral operator)"}
+        del s2
 
     # cfg3 names "all ablation radii": the other two checkpoints (W1_r1, W1_r2)
     # on the same ICs, timed the same way (the radius only selects the weights)
@@ -487,9 +579,10 @@ def main():
         others = [other_config(w_r1, dev, "cfg2: 64-cell chain, 256-IC batch, r=1, f32", 256, 64, "f32", 30, 30, 1,
                                also="f16x3", reps=20),
                   other_config(w_r2, dev, "cfg4: 1024-cell chain, 4096-IC batch, r=2, bf16 MLP weights, dt=3.125e-4",
-                               4096, 1024, "bf16", 30, 30, 2, fixture=fx)]
+                               4096, 1024, "bf16", 30, 30, 2, fixture=fx, tridiag=True)]
 
     models = other_models(dev, 4096, 30) if world == 1 and not args.no_other_configs else None
+    train = train_line(dev) if world == 1 and not args.no_other_configs and not args.no_train else None
 
     wall_max = max_over_ranks(wall)
     finite = float(gathered["metrics"][:, -1, 2].float().mean().item())
@@ -571,6 +664,8 @@ def main():
             "other_configs": others,
             # the reference's PureGNN / PINN rollouts, 4096 ICs x 64 cells, T = 30
             "other_models": models,
+            # the batched training step (reference trainer's loop), B = 2000
+            "train": train,
         }
         print(json.dumps(line), flush=True)
     if grouped:

@@ -760,6 +760,8 @@ int64_t pure_gnn_run_ws_bytes(int H, int B, int nx, int T) {
   return pure_gnn_ws_bytes(H, (int64_t)B * nx, 2LL * B * nx);
 }
 
+bool pure_gnn_run_ws_optional(int H, int nx, int T) { return HF_PURE_FUSED && T > 0 && pure_fused_ok(H, nx); }
+
 int64_t pinn_run_ws_bytes(int D, int H, int64_t B) {
   // the one-launch shape: the packed weight copy, sized for the most layers the ABI admits
   if (B == 0) return 0;

@@ -504,7 +504,9 @@ int hf_pure_gnn_run(const float *params, int hidden, int layers, const float *st
   if (hidden < 1 || layers < 0 || B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_pure_gnn_run: bad argument");
   if (B == 0) return HF_OK;
   if (!params || !state0 || !final_state || !x) return fail(HF_EINVAL, "hf_pure_gnn_run: NULL pointer");
-  if (!ws && hf::pure_gnn_run_ws_bytes(hidden, B, nx, T) > 0)
+  // the one-launch rollout runs on nn.Linear's rows without a workspace (its
+  // packed copy is an optimisation); the per-step path needs its scratch
+  if (!ws && !hf::pure_gnn_run_ws_optional(hidden, nx, T) && hf::pure_gnn_run_ws_bytes(hidden, B, nx, T) > 0)
     return fail(HF_EINVAL, "hf_pure_gnn_run: NULL workspace (hf_pure_gnn_run_workspace_bytes > 0 for this shape)");
   HF_CHECK_HIP(hf::launch_pure_gnn_run(params, hidden, layers, state0, final_state, x, B, nx, T, traj, ws,
                                        as_stream(stream)),
@@ -596,13 +598,51 @@ int hf_poisson_coeffs(int nx, double length, double *c) {
   return HF_OK;
 }
 
-int hf_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B, int nx,
-               void *stream) {
+int hf_poisson_plan_size(int mode, int nx) {
+  if (nx < 1) return -1;
+  switch (mode) {
+    case HF_POISSON_SPECTRAL: return hf::poisson_plan_len(nx);
+    case HF_POISSON_TRIDIAG: return nx <= hf::kTriMaxNx ? 1 : -1;
+    default: return -1;
+  }
+}
+
+int hf_poisson_plan(int mode, int nx, double length, double *plan) {
+  if (mode == HF_POISSON_SPECTRAL) return hf_poisson_coeffs(nx, length, plan);
+  if (mode != HF_POISSON_TRIDIAG) return fail(HF_EINVAL, "hf_poisson_plan: unknown Poisson mode");
+  if (nx < 1 || !(length > 0) || !plan) return fail(HF_EINVAL, "hf_poisson_plan: bad argument");
+  if (nx > hf::kTriMaxNx) return fail(HF_EUNSUPPORTED, "hf_poisson_plan: tridiagonal mode needs nx <= 16384");
+  plan[0] = 0.5 * (length / nx);  // h = dx/2: E[i] = h (psi[i-1] - psi[i+1]) (hf_device.h)
+  return HF_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// The Poisson mode argument of every *_ex entry point.
+int check_mode(int pm, int nx, const char *fn) {
+  if (pm != HF_POISSON_SPECTRAL && pm != HF_POISSON_TRIDIAG)
+    return fail(HF_EINVAL, std::string(fn) + ": unknown Poisson mode");
+  if (!hf::poisson_mode_ok(pm, nx))
+    return fail(HF_EUNSUPPORTED, std::string(fn) + ": tridiagonal Poisson needs nx <= 16384");
+  return HF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int hf_poisson_ex(const float *n, int ld_n, float *E, int ld_E, const double *pc, int pm, int B, int nx,
+                  void *stream) {
   if (B < 0 || nx < 1 || ld_n < nx || ld_E < nx) return fail(HF_EINVAL, "hf_poisson: bad shape");
+  if (int rc = check_mode(pm, nx, "hf_poisson")) return rc;
   if (B == 0) return HF_OK;
   if (!n || !E || !pc) return fail(HF_EINVAL, "hf_poisson: NULL pointer");
-  HF_CHECK_HIP(hf::launch_poisson(n, ld_n, E, ld_E, pc, B, nx, as_stream(stream)), "hf_poisson");
+  HF_CHECK_HIP(hf::launch_poisson(n, ld_n, E, ld_E, pc, B, nx, pm, as_stream(stream)), "hf_poisson");
   return HF_OK;
+}
+
+int hf_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B, int nx, void *stream) {
+  return hf_poisson_ex(n, ld_n, E, ld_E, pc, HF_POISSON_SPECTRAL, B, nx, stream);
 }
 
 int64_t hf_run_workspace_bytes(int op, int B, int nx, int T) {
@@ -656,8 +696,8 @@ struct Scratch {
 // the trajectory).  ldT / ldM / ldFT are the per-IC strides of traj, metrics
 // and flux_traj, so a slice is the same call on offset pointers.
 hipError_t run_steps(const hf_model *m, const float *state0, float *state_final, const float *x, const double *pc,
-                     int B, int nx, int T, float c, float dt, float nu, float dx2, float *traj, float *flux_traj,
-                     float *metrics, float *buf0, float *buf1, float *F, hipStream_t s) {
+                     int pm, int B, int nx, int T, float c, float dt, float nu, float dx2, float *traj,
+                     float *flux_traj, float *metrics, float *buf0, float *buf1, float *F, hipStream_t s) {
   const int64_t S = 3LL * nx, ldT = (T + 1) * S, ldM = (int64_t)(T + 1) * HF_NUM_METRICS;
   float *buf[2] = {buf0, buf1};
   hipError_t e = hipSuccess;
@@ -680,7 +720,7 @@ hipError_t run_steps(const hf_model *m, const float *state0, float *state_final,
     if (e == hipSuccess)
       e = hf::launch_fv_step(cur, ld_cur, dst, ld_dst, F, pc, B, nx, c, dt, nu, dx2,
                              flux_traj ? flux_traj + (int64_t)t * nx : nullptr, (int64_t)T * nx,
-                             metrics ? metrics + (int64_t)(t + 1) * HF_NUM_METRICS : nullptr, ldM, s);
+                             metrics ? metrics + (int64_t)(t + 1) * HF_NUM_METRICS : nullptr, ldM, pm, s);
     cur = dst;
     ld_cur = ld_dst;
   }
@@ -728,6 +768,8 @@ void lane_cuts(const hf_model *m, int B, int nx, int lanes, int64_t *cut) {
   if (all.per_round <= 0) return;
   const int64_t k = all.units / all.per_round / lanes;  // whole rounds per leading lane
   if (k < 1) return;
+  // computed whole into a local set, copied over the even split only when every lane is placed
+  int64_t c[kMaxLanes + 1] = {0};
   int64_t o = 0;
   for (int i = 0; i + 1 < lanes; ++i) {
     // the most ICs whose units fit k rounds (units grow by at most
@@ -735,9 +777,10 @@ void lane_cuts(const hf_model *m, int B, int nx, int lanes, int64_t *cut) {
     int64_t n = (int64_t)B / lanes + 1;
     while (n > 1 && hf::chain_flux_work(m->chain, n, nx).units > k * all.per_round) --n;
     if (o + n >= B) return;  // keep the even split: nothing left for the last lane
-    cut[i + 1] = o += n;
+    c[i + 1] = o += n;
   }
-  cut[lanes] = B;
+  c[lanes] = B;
+  for (int i = 0; i <= lanes; ++i) cut[i] = c[i];
 }
 
 int run_lanes() {
@@ -838,24 +881,27 @@ int64_t hf_workspace_need(hf_model_t m, int op, int B, int nx, int T, int flags)
   }
 }
 
-int hf_step(hf_model_t m, const float *in, float *out, const float *x, const double *pc, int B, int nx,
-            float c, float dt, float nu, float dx2, float *ff, float *metrics, void *ws, int64_t ws_bytes,
-            void *stream) {
+int hf_step_ex(hf_model_t m, const float *in, float *out, const float *x, const double *pc, int pm, int B, int nx,
+               float c, float dt, float nu, float dx2, float *ff, float *metrics, void *ws, int64_t ws_bytes,
+               void *stream) {
   if (B < 0 || nx < 1) return fail(HF_EINVAL, "hf_step: need B >= 0, nx >= 1");
+  if (int rc = check_mode(pm, nx, "hf_step")) return rc;
   if (B == 0) return HF_OK;
   if (!in || !out || !pc) return fail(HF_EINVAL, "hf_step: NULL state or Poisson coefficients");
   if (in == out) return fail(HF_EINVAL, "hf_step: state_in and state_out must not alias");
   hipStream_t s = as_stream(stream);
   if (!m) {  // BaselineSolver.step
     HF_CHECK_HIP(hf::launch_fv_step(in, 3LL * nx, out, 3LL * nx, nullptr, pc, B, nx, c, dt, nu, dx2, ff,
-                                    nx, metrics, HF_NUM_METRICS, s),
+                                    nx, metrics, HF_NUM_METRICS, pm, s),
                  "hf_step(classical)");
     return HF_OK;
   }
   if (!x) return fail(HF_EINVAL, "hf_step: NULL x");
   if (int rc = chain_usable(m)) return rc;
   if (fused_nx(nx)) {
-    HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, in, out, x, pc, B, nx, 1, c, dt, nullptr, ff, nullptr, s),
+    hf::RolloutExtras ex;
+    ex.poisson = pm;
+    HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, in, out, x, pc, B, nx, 1, c, dt, nullptr, ff, nullptr, s, ex),
                  "hf_step(hybrid fused)");
     if (metrics)
       HF_CHECK_HIP(hf::launch_state_metrics(out, 3LL * nx, B, nx, metrics, HF_NUM_METRICS, s), "hf_step metrics");
@@ -867,15 +913,22 @@ int hf_step(hf_model_t m, const float *in, float *out, const float *x, const dou
   float *F = ff ? ff : sc.take(sizeof(float) * (int64_t)B * nx);
   HF_CHECK_HIP(hf::launch_chain_flux(m->chain, nullptr, in, 3LL * nx, x, B, nx, nullptr, F, s), "hf_step(flux)");
   HF_CHECK_HIP(hf::launch_fv_step(in, 3LL * nx, out, 3LL * nx, F, pc, B, nx, c, dt, nu, dx2, nullptr, nx, metrics,
-                                  HF_NUM_METRICS, s),
+                                  HF_NUM_METRICS, pm, s),
                "hf_step(fv)");
   return HF_OK;
 }
 
-int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B,
-           int nx, int T, float c, float dt, float nu, float dx2, float *traj, float *flux_traj,
-           float *metrics, void *ws, int64_t ws_bytes, void *stream) {
+int hf_step(hf_model_t m, const float *in, float *out, const float *x, const double *pc, int B, int nx, float c,
+            float dt, float nu, float dx2, float *ff, float *metrics, void *ws, int64_t ws_bytes, void *stream) {
+  return hf_step_ex(m, in, out, x, pc, HF_POISSON_SPECTRAL, B, nx, c, dt, nu, dx2, ff, metrics, ws, ws_bytes,
+                    stream);
+}
+
+int hf_run_ex(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int pm,
+              int B, int nx, int T, float c, float dt, float nu, float dx2, float *traj, float *flux_traj,
+              float *metrics, void *ws, int64_t ws_bytes, void *stream) {
   if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run: need B >= 0, nx >= 1, T >= 0");
+  if (int rc = check_mode(pm, nx, "hf_run")) return rc;
   if (B == 0) return HF_OK;
   if (!state0 || !state_final || !pc) return fail(HF_EINVAL, "hf_run: NULL state or Poisson coefficients");
   if (m && !x) return fail(HF_EINVAL, "hf_run: NULL x");
@@ -885,8 +938,10 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   hipStream_t s = as_stream(stream);
   const int64_t S = 3LL * nx;  // floats per state
   if (m && fused_nx(nx)) {  // the kernel reads each IC's state0 whole before writing its state_final
+    hf::RolloutExtras ex;
+    ex.poisson = pm;
     HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, state0, state_final, x, pc, B, nx, T, c, dt, traj,
-                                          flux_traj, metrics, s),
+                                          flux_traj, metrics, s, ex),
                  "hf_run(hybrid fused)");
     return HF_OK;
   }
@@ -906,7 +961,7 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   }
   if (!m && hf::fv_run_fused(nx) && fv_run_persistent()) {  // BaselineSolver.run at FFT nx <= 1024 and nx <= 64: one launch
     HF_CHECK_HIP(hf::launch_fv_run(state0, S, state_final, traj, pc, B, nx, T, c, dt, nu, dx2, flux_traj, metrics,
-                                   nullptr, nullptr, s),
+                                   nullptr, nullptr, pm, s),
                  "hf_run(classical fused)");
     return HF_OK;
   }
@@ -926,8 +981,8 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
     if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice(s, &sdev) != hipSuccess || sdev != cur) lanes = 1;
   }
   if (lanes == 1) {
-    HF_CHECK_HIP(run_steps(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics, buf0,
-                           buf1, F, s),
+    HF_CHECK_HIP(run_steps(m, state0, state_final, x, pc, pm, B, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics,
+                           buf0, buf1, F, s),
                  "hf_run");
     return HF_OK;
   }
@@ -938,8 +993,8 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   bool granted = false;
   HF_CHECK_HIP(lane_streams(s, lanes, ls, &granted), "hf_run lane stream");
   if (!granted) {
-    HF_CHECK_HIP(run_steps(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics, buf0,
-                           buf1, F, s),
+    HF_CHECK_HIP(run_steps(m, state0, state_final, x, pc, pm, B, nx, T, c, dt, nu, dx2, traj, flux_traj, metrics,
+                           buf0, buf1, F, s),
                  "hf_run");
     return HF_OK;
   }
@@ -959,7 +1014,7 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
     if (i > 0) e = hipStreamWaitEvent(ls[i], fork, 0);
     if (e != hipSuccess) break;
     used[i] = true;
-    e = run_steps(m, state0 + o * S, state_final + o * S, x, pc, (int)n, nx, T, c, dt, nu, dx2,
+    e = run_steps(m, state0 + o * S, state_final + o * S, x, pc, pm, (int)n, nx, T, c, dt, nu, dx2,
                   traj ? traj + o * ldT : nullptr, flux_traj ? flux_traj + o * T * nx : nullptr,
                   metrics ? metrics + o * ldM : nullptr, buf0 ? buf0 + o * S : nullptr,
                   buf1 ? buf1 + o * S : nullptr, F + o * nx, ls[i]);
@@ -980,11 +1035,19 @@ int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x
   return HF_OK;
 }
 
-int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B,
-                   int nx, int T, float c, float dt, float nu, float dx2, float *mse, float *metrics,
-                   float *metrics_cl, void *ws, int64_t ws_bytes, void *stream) {
+int hf_run(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B, int nx,
+           int T, float c, float dt, float nu, float dx2, float *traj, float *flux_traj, float *metrics, void *ws,
+           int64_t ws_bytes, void *stream) {
+  return hf_run_ex(m, state0, state_final, x, pc, HF_POISSON_SPECTRAL, B, nx, T, c, dt, nu, dx2, traj, flux_traj,
+                   metrics, ws, ws_bytes, stream);
+}
+
+int hf_run_compare_ex(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int pm,
+                      int B, int nx, int T, float c, float dt, float nu, float dx2, float *mse, float *metrics,
+                      float *metrics_cl, void *ws, int64_t ws_bytes, void *stream) {
   if (!m) return fail(HF_EINVAL, "hf_run_compare: NULL model");
   if (B < 0 || nx < 1 || T < 0) return fail(HF_EINVAL, "hf_run_compare: need B >= 0, nx >= 1, T >= 0");
+  if (int rc = check_mode(pm, nx, "hf_run_compare")) return rc;
   if (B == 0) return HF_OK;
   if (!state0 || !state_final || !pc || !x || !mse) return fail(HF_EINVAL, "hf_run_compare: NULL pointer");
   if (int rc = chain_usable(m)) return rc;
@@ -995,6 +1058,7 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
     ex.dx2 = dx2;
     ex.mse = mse;
     ex.metrics_cl = metrics_cl;
+    ex.poisson = pm;
     HF_CHECK_HIP(hf::launch_chain_rollout(m->chain, state0, state_final, x, pc, B, nx, T, c, dt, nullptr, nullptr,
                                           metrics, s, ex),
                  "hf_run_compare(fused)");
@@ -1012,13 +1076,14 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
     float *th = sc.take(sizeof(float) * (int64_t)B * ldT);
     const int64_t fbytes = (sizeof(float) * (int64_t)B * nx + 255) / 256 * 256;
     float *F = sc.take(fbytes);
-    int rc = hf_run(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, th, nullptr, metrics, F, fbytes, stream);
+    int rc =
+        hf_run_ex(m, state0, state_final, x, pc, pm, B, nx, T, c, dt, nu, dx2, th, nullptr, metrics, F, fbytes, stream);
     if (rc != HF_OK) return rc;
     if (metrics_cl)
       HF_CHECK_HIP(hf::launch_state_metrics(th, ldT, B, nx, metrics_cl, (int64_t)(T + 1) * HF_NUM_METRICS, s),
                    "hf_run_compare metrics[0]");
     HF_CHECK_HIP(hf::launch_fv_run(th, ldT, nullptr, nullptr, pc, B, nx, T, c, dt, nu, dx2, nullptr, metrics_cl, th, mse,
-                                   s),
+                                   pm, s),
                  "hf_run_compare(classical twin)");
     return HF_OK;
   }
@@ -1033,12 +1098,21 @@ int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const 
   const int64_t fbytes = (sizeof(float) * (int64_t)B * nx + 255) / 256 * 256;
   float *F = sc.take(fbytes);
   // with a trajectory buffer hf_run needs scratch only for the hybrid face flux
-  int rc = hf_run(nullptr, state0, fin_c, x, pc, B, nx, T, c, dt, nu, dx2, tc, nullptr, metrics_cl, nullptr, 0, stream);
+  int rc = hf_run_ex(nullptr, state0, fin_c, x, pc, pm, B, nx, T, c, dt, nu, dx2, tc, nullptr, metrics_cl, nullptr, 0,
+                     stream);
   if (rc == HF_OK)
-    rc = hf_run(m, state0, state_final, x, pc, B, nx, T, c, dt, nu, dx2, th, nullptr, metrics, F, fbytes, stream);
+    rc = hf_run_ex(m, state0, state_final, x, pc, pm, B, nx, T, c, dt, nu, dx2, th, nullptr, metrics, F, fbytes,
+                   stream);
   if (rc != HF_OK) return rc;
   HF_CHECK_HIP(hf::launch_traj_mse(th, tc, B, T + 1, nx, mse, s), "hf_run_compare mse");
   return HF_OK;
+}
+
+int hf_run_compare(hf_model_t m, const float *state0, float *state_final, const float *x, const double *pc, int B,
+                   int nx, int T, float c, float dt, float nu, float dx2, float *mse, float *metrics,
+                   float *metrics_cl, void *ws, int64_t ws_bytes, void *stream) {
+  return hf_run_compare_ex(m, state0, state_final, x, pc, HF_POISSON_SPECTRAL, B, nx, T, c, dt, nu, dx2, mse,
+                           metrics, metrics_cl, ws, ws_bytes, stream);
 }
 
 int hf_traj_metrics(const float *traj, int B, int T1, int nx, float *metrics, void *stream) {

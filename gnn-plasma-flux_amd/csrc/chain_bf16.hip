@@ -817,13 +817,20 @@ __global__ __launch_bounds__(64 * Core::kNW, 1) void chain_flux_sw_kernel(ChainW
   R.drain();
 }
 
+// Super-windows of B chains of nx cells for a core of NW waves (63 exact
+// faces per wave, less the L-layer halo): the one formula launch_flux_sw and
+// chain_flux_work (hf_run's lane cuts) share.
+inline int64_t sw_count(int NW, int layers, int64_t B, int nx) {
+  const int64_t faces = 63 * NW - 2 * layers, total = B * (nx + 2 * layers + 1);
+  return (total + faces - 1) / faces;
+}
+
 template <class Core>
 hipError_t launch_flux_sw(const ChainW &w, const float *nf, const float *state, int64_t ld_state, const float *x,
                           int B, int nx, float *fe, float *ff, hipStream_t s) {
   const int64_t total = (int64_t)B * (nx + 2 * w.layers + 1);
   if (total >= (int64_t(1) << 31) - 64 * Core::kNW) return hipErrorInvalidValue;  // 32-bit stream index
-  const int faces = 63 * Core::kNW - 2 * w.layers;
-  const int nsw = (int)((total + faces - 1) / faces);
+  const int nsw = (int)sw_count(Core::kNW, w.layers, B, nx);
   const int64_t res = resident_groups();
   const int64_t blocks = nsw < res ? nsw : res;  // persistent: one per CU
   hipLaunchKernelGGL((chain_flux_sw_kernel<Core>), dim3((unsigned)blocks), dim3(64 * Core::kNW), 0, s, w, nf, state,
@@ -953,6 +960,13 @@ using CellBF16Ld = CellBF16T<HF_CELLS_LOADER != 0>;  // with a loader wave (the 
 
 }  // namespace
 
+// ring position of the deferred DMA: 0 (pair unit 2) measured best; 1, 2, 3: +3-10 % (profiles/r02_cfg4_diag.jsonl, run D)
+#ifndef HF_SW_DMAU
+#define HF_SW_DMAU 0
+#endif
+// the super-window core (any nx other than 16..64; cfg4's 1024): 8 waves, two per SIMD
+using SwCoreBF16 = CoreBF16<8, 4, 4, false, 3, 1, HF_SW_DMAU, true>;
+
 hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float *state, int64_t ld_state,
                                   const float *x, int B, int nx, float *fe, float *ff, hipStream_t s) {
   // exact kernels (nx = 16..64, one wave per chain) and super-windows (any
@@ -968,11 +982,7 @@ hipError_t launch_chain_flux_bf16(const ChainW &w, const float *nf, const float 
   }
   if (nx == 16 || nx == 32 || nx == 48 || nx == 64)
     return chain::launch_flux_core<CoreBF16<8, 4>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
-// ring position of the deferred DMA: 0 (pair unit 2) measured best; 1, 2, 3: +3-10 % (profiles/r02_cfg4_diag.jsonl, run D)
-#ifndef HF_SW_DMAU
-#define HF_SW_DMAU 0
-#endif
-  return launch_flux_sw<CoreBF16<8, 4, 4, false, 3, 1, HF_SW_DMAU, true>>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+  return launch_flux_sw<SwCoreBF16>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
 }
 
 FluxWork chain_flux_work(const ChainW &w, int64_t B, int nx) {
@@ -980,9 +990,8 @@ FluxWork chain_flux_work(const ChainW &w, int64_t B, int nx) {
   if (w.prec != kPrecBF16 || B <= 0 || nx == 16 || nx == 32 || nx == 48 || nx == 64 ||
       chain_rollout_prefers_cells(w, (int)B, nx))
     return fw;  // not the super-window kernel
-  constexpr int NW = 8;  // launch_chain_flux_bf16's super-window core
-  const int64_t faces = 63 * NW - 2 * w.layers, P = nx + 2 * w.layers + 1;
-  fw.units = (B * P + faces - 1) / faces;   // super-windows (launch_flux_sw)
+  fw.units = sw_count(SwCoreBF16::kNW, w.layers, B, nx);  // the core launch_chain_flux_bf16 runs
+
   fw.per_round = resident_groups();         // one per persistent workgroup per round
   return fw;
 }
@@ -993,9 +1002,9 @@ hipError_t launch_chain_rollout_bf16(const ChainW &w, const float *state0, float
   // small batches: each IC over nx/16 waves (cell-split kernel, same bits)
   if (ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx)) {
     switch (nx) {
-      case 32: return chain::cells_launch<CellBF16Ld, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 48: return chain::cells_launch<CellBF16Ld, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 64: return chain::cells_launch<CellBF16Ld, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 32: return chain::cells_launch<CellBF16Ld, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex.poisson, s);
+      case 48: return chain::cells_launch<CellBF16Ld, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex.poisson, s);
+      case 64: return chain::cells_launch<CellBF16Ld, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex.poisson, s);
       default: break;
     }
   }

@@ -600,9 +600,11 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
     s_st[(i / NX) * 64 + i % NX] = v;
     if (twin) s_cl[(i / NX) * 64 + i % NX] = v;
   }
+  const bool tri = ex.poisson == HF_POISSON_TRIDIAG;  // plan = {h}: no circulant column
+  const double h = tri ? pc[0] : 0.0;
   if (lane < NX) {
     s_st[3 * 64 + lane] = x[lane];
-    s_c2[lane] = s_c2[NX + lane] = pc[lane];
+    if (!tri) s_c2[lane] = s_c2[NX + lane] = pc[lane];
   }
   __syncthreads();  // small weights + per-wave state visible (no DMA in flight yet)
   float *tj = (traj && live) ? traj + b * (int64_t)(T + 1) * 3 * NX : nullptr;
@@ -674,13 +676,22 @@ __global__ __launch_bounds__(256, 1) void chain_rollout_kernel(
       }
     }
     wave_lds_sync();
+    float E_tri = 0.f, Ec_tri = 0.f;
+    if (tri) {  // HF_POISSON_TRIDIAG: the wave's cyclic reduction over its rho row(s)
+      tridiag_psi_wave<double>(s_rho, NX, lane);
+      if (lane < NX) E_tri = (float)tri_E(s_rho, lane, NX, h);
+      if (twin) {
+        tridiag_psi_wave<double>(s_rhoc, NX, lane);
+        if (lane < NX) Ec_tri = (float)tri_E(s_rhoc, lane, NX, h);
+      }
+    }
     if (lane < NX) {
-      const float E_new = poisson_cell_nx<NX>(s_rho, s_c2, lane);
+      const float E_new = tri ? E_tri : poisson_cell_nx<NX>(s_rho, s_c2, lane);
       s_st[lane] = n_new;
       s_st[64 + lane] = u_new;
       s_st[128 + lane] = E_new;
       if (twin) {
-        const float Ec = poisson_cell_nx<NX>(s_rhoc, s_c2, lane);
+        const float Ec = tri ? Ec_tri : poisson_cell_nx<NX>(s_rhoc, s_c2, lane);
         s_cl[lane] = nc;
         s_cl[64 + lane] = uc;
         s_cl[128 + lane] = Ec;
@@ -726,8 +737,10 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
     ChainW W, const float *state0, float *state_final,  // may alias (read whole before written)
     const float *__restrict__ x,
     const double *__restrict__ pc, int B, int T, float c, float dt, float *__restrict__ traj,
-    float *__restrict__ flux_traj, float *__restrict__ metrics) {
+    float *__restrict__ flux_traj, float *__restrict__ metrics, int pm) {
   constexpr int NX = 16 * WPI;
+  const bool tri = pm == HF_POISSON_TRIDIAG;  // plan = {h}: no circulant column
+  const double h = tri ? pc[0] : 0.0;
   constexpr int IPW = kWaves / WPI;  // ICs per workgroup
   constexpr int kRingFloats = CC::kSlots * CC::kChunkFloats;
   __shared__ f4 lds4[cells_lds_floats<CC>() / 4];
@@ -769,7 +782,7 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
     for (int i = lane; i < 3 * NX; i += 64) s_st[(i / NX) * 64 + i % NX] = st0[i];
     if (lane < NX) {
       s_st[3 * 64 + lane] = x[lane];
-      s_c2[lane] = s_c2[NX + lane] = pc[lane];
+      if (!tri) s_c2[lane] = s_c2[NX + lane] = pc[lane];
     }
   }
   __syncthreads();  // small weights + IC state visible (no DMA in flight yet)
@@ -847,8 +860,13 @@ __global__ __launch_bounds__(cells_threads<CC>(), 1) void chain_rollout_cells_ke
         if (ftj) ftj[(int64_t)t * NX + lane] = Fv;
       }
       wave_lds_sync();
+      float E_tri = 0.f;
+      if (tri) {  // HF_POISSON_TRIDIAG: the lead's cyclic reduction over the IC's rho row
+        tridiag_psi_wave<double>(s_rho, NX, lane);
+        if (lane < NX) E_tri = (float)tri_E(s_rho, lane, NX, h);
+      }
       if (lane < NX) {
-        const float E_new = poisson_cell_nx<NX>(s_rho, s_c2, lane);
+        const float E_new = tri ? E_tri : poisson_cell_nx<NX>(s_rho, s_c2, lane);
         s_st[lane] = n_new;
         s_st[64 + lane] = u_new;
         s_st[128 + lane] = E_new;
@@ -936,10 +954,10 @@ hipError_t flux_cells_launch(const ChainW &w, const float *nf, const float *stat
 template <class CC, int WPI>
 hipError_t cells_launch(const ChainW &w, const float *state0, float *state_final, const float *x, const double *pc,
                         int B, int T, float c, float dt, float *traj, float *flux_traj, float *metrics,
-                        hipStream_t s) {
+                        int pm, hipStream_t s) {
   constexpr int IPW = kWaves / WPI;
   hipLaunchKernelGGL((chain_rollout_cells_kernel<CC, WPI>), dim3((B + IPW - 1) / IPW), dim3(cells_threads<CC>()), 0, s, w,
-                     state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics);
+                     state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, pm);
   return hipGetLastError();
 }
 

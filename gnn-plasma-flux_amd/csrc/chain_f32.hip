@@ -379,12 +379,12 @@ bool chain_rollout_prefers_cells(const ChainW &w, int B, int nx) {
 
 hipError_t launch_chain_rollout_cells(const ChainW &w, const float *state0, float *state_final, const float *x,
                                       const double *pc, int B, int nx, int T, float c, float dt, float *traj,
-                                      float *flux_traj, float *metrics, hipStream_t s) {
+                                      float *flux_traj, float *metrics, int pm, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (nx) {
-    case 32: return cells_launch<CellCoreLd, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 48: return cells_launch<CellCoreLd, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-    case 64: return cells_launch<CellCoreLd, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+    case 32: return cells_launch<CellCoreLd, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, pm, s);
+    case 48: return cells_launch<CellCoreLd, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, pm, s);
+    case 64: return cells_launch<CellCoreLd, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, pm, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -408,7 +408,8 @@ hipError_t launch_chain_rollout_f32(const ChainW &w, const float *state0, float 
                                     float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
   // small batches: each IC spread over nx/16 waves (cell-split kernel)
   if (ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx))
-    return launch_chain_rollout_cells(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics, s);
+    return launch_chain_rollout_cells(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj, metrics,
+                                      ex.poisson, s);
   return chain::launch_rollout_core<CoreF32>(w, state0, state_final, x, pc, B, nx, T, c, dt, traj, flux_traj,
                                              metrics, ex, s);
 }

@@ -572,9 +572,9 @@ hipError_t launch_chain_rollout_k32(const ChainW &w, const float *state0, float 
                                     float *flux_traj, float *metrics, const RolloutExtras &ex, hipStream_t s) {
   if (w.prec == kPrecF16x3 && ex.mse == nullptr && ex.metrics_cl == nullptr && chain_rollout_prefers_cells(w, B, nx)) {
     switch (nx) {  // small batches: each IC over nx/16 waves (cell-split kernel, same bits)
-      case 32: return chain::cells_launch<CellF16x3Ld, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 48: return chain::cells_launch<CellF16x3Ld, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
-      case 64: return chain::cells_launch<CellF16x3Ld, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, s);
+      case 32: return chain::cells_launch<CellF16x3Ld, 2>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex.poisson, s);
+      case 48: return chain::cells_launch<CellF16x3Ld, 3>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex.poisson, s);
+      case 64: return chain::cells_launch<CellF16x3Ld, 4>(w, state0, state_final, x, pc, B, T, c, dt, traj, flux_traj, metrics, ex.poisson, s);
       default: break;
     }
   }

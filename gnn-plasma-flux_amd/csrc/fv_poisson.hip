@@ -56,12 +56,14 @@ struct FvLds {
 };
 
 // Circulant nx (any nx that is not an FFT size): one 256-thread workgroup per IC.
+// tri (HF_POISSON_TRIDIAG, wave-uniform): the c row holds rho, then psi, and
+// wave 0 runs the cyclic reduction (hf_device.h tridiag_psi_wave); pc[0] = h.
 template <bool HYBRID>
 __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     const float *__restrict__ in, int64_t ld_in, float *__restrict__ out, int64_t ld_out,
     const float *__restrict__ face_flux, const double *__restrict__ pc, int nx, float c, float dt,
     float nu, float dx2, float *__restrict__ flux_out, int64_t ld_flux, float *__restrict__ metrics,
-    int64_t ld_metrics) {
+    int64_t ld_metrics, int tri) {
   extern __shared__ double s_dyn[];
   const FvLds L(s_dyn, nx);
   const int64_t b = blockIdx.x;
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     const float u = st[nx + i];
     L.u[i] = u;
     L.F[i] = HYBRID ? face_flux[b * nx + i] : __fmul_rn(st[i], u);  // F_n = n*u (:70-71)
-    L.c[i] = pc[i];
+    if (!tri) L.c[i] = pc[i];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
@@ -82,16 +84,23 @@ __global__ __launch_bounds__(kFvThreads) void fv_step_kernel(
     const float E = st[2 * nx + i];
     const float u_new = HYBRID ? velocity_hybrid(L.u[i], L.u[im], E, c, dt)
                                : velocity_classical(L.u[i], L.u[im], L.u[ip], E, c, dt, nu, dx2);
-    L.rho[i] = __fsub_rn(n_new, 1.0f);
+    const float rho = __fsub_rn(n_new, 1.0f);
+    if (tri) L.c[i] = (double)rho;
+    else L.rho[i] = rho;
     so[i] = n_new;
     so[nx + i] = u_new;
     if (flux_out) flux_out[b * ld_flux + i] = F;
   }
   __syncthreads();
+  if (tri) {
+    if (threadIdx.x < 64) tridiag_psi_wave<double>(L.c, nx, threadIdx.x);
+    __syncthreads();
+  }
+  const double h = tri ? pc[0] : 0.0;
   MetricAcc m;
   m.init();
   for (int i = threadIdx.x; i < nx; i += kFvThreads) {
-    const float E_new = poisson_cell(L.rho, L.c, i, nx);
+    const float E_new = tri ? (float)tri_E(L.c, i, nx, h) : poisson_cell(L.rho, L.c, i, nx);
     so[2 * nx + i] = E_new;
     if (metrics) m.add(so[i], so[nx + i], E_new);
   }
@@ -163,6 +172,23 @@ __global__ __launch_bounds__(kFvThreads) void poisson_tiled_kernel(const float *
     }
   }
   if (i < nx) E[b * ld_E + i] = (float)(a0 + a1);
+}
+
+// Tridiagonal (HF_POISSON_TRIDIAG) E for one IC per 256-thread workgroup, any
+// nx <= kTriMaxNx: rho staged as float64 in dynamic LDS, cyclic reduction by
+// wave 0 (tridiag_psi_wave), E by every thread.  hf_poisson in this mode and the
+// large-nx step (after fv_update_kernel).  pc[0] = h = dx/2.
+__global__ __launch_bounds__(kFvThreads) void poisson_tri_kernel(const float *__restrict__ n, int64_t ld_n,
+                                                                 float *__restrict__ E, int64_t ld_E,
+                                                                 const double *__restrict__ pc, int nx) {
+  extern __shared__ double s_dyn[];
+  const int64_t b = blockIdx.x;
+  for (int i = threadIdx.x; i < nx; i += kFvThreads) s_dyn[i] = (double)__fsub_rn(n[b * ld_n + i], 1.0f);
+  __syncthreads();
+  if (threadIdx.x < 64) tridiag_psi_wave<double>(s_dyn, nx, threadIdx.x);
+  __syncthreads();
+  const double h = pc[0];
+  for (int i = threadIdx.x; i < nx; i += kFvThreads) E[b * ld_E + i] = (float)tri_E(s_dyn, i, nx, h);
 }
 
 // ------------------------------------------------------------ FFT sizes
@@ -251,12 +277,37 @@ __device__ __forceinline__ void fv_update_in(const FvIn<N> &x, float *__restrict
   }
 }
 
+// The Poisson stage of the FFT-size kernels on one wave's IC pair: on entry
+// v[i] = (rho_a, rho_b) at cell lane + 64 i, on exit (E_a, E_b) there before
+// the float32 rounding.  Spectral (the reference's operator): the packed
+// transform pair (poisson_wave_tw), then / N.  TRI (HF_POISSON_TRIDIAG): the
+// pair's rows through the wave-private LDS buffer, cyclic reduction on both
+// at once (tridiag_psi_wave<double2>), E = h (psi[i-1] - psi[i+1]).
+template <int N, bool TRI>
+__device__ __forceinline__ void poisson_pair(double2 (&v)[N / 64], double2 *lds, const double2 *__restrict__ tw,
+                                             const double *__restrict__ inv_k, double h, int lane) {
+  if constexpr (TRI) {
+    wave_lds_fence();  // earlier reads of the buffer (the parked rho of IC a) are done
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) lds[lane + 64 * i] = v[i];
+    wave_lds_fence();
+    tridiag_psi_wave<double2>(lds, N, lane);
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) v[i] = tri_E(lds, lane + 64 * i, N, h);
+    wave_lds_fence();  // every lane's psi reads before the buffer is written again
+  } else {
+    poisson_wave_tw<N>(v, lds, tw, inv_k, lane);
+#pragma unroll
+    for (int i = 0; i < N / 64; ++i) v[i] = make_double2(v[i].x / N, v[i].y / N);
+  }
+}
+
 template <int N, bool IMAG>
 __device__ __forceinline__ void fv_finish_lane(float *__restrict__ so, const double2 (&v)[N / 64], MetricAcc &m,
                                                float *__restrict__ mo, int lane) {
 #pragma unroll
   for (int i = 0; i < N / 64; ++i) {
-    const float E_new = (float)((IMAG ? v[i].y : v[i].x) / N);
+    const float E_new = (float)(IMAG ? v[i].y : v[i].x);
     so[2 * N + lane + 64 * i] = E_new;
     if (mo) m.add_E(E_new);
   }
@@ -268,7 +319,7 @@ __device__ __forceinline__ void fv_finish_lane(float *__restrict__ so, const dou
 
 // N = 2048: the wave-private LDS (4 x 2176 double2, ~139 KB) admits one
 // workgroup per CU, so a min-blocks hint of 2 would only cap the VGPRs.
-template <bool HYBRID, int N>
+template <bool HYBRID, int N, bool TRI>
 __global__ __launch_bounds__(64 * kFftWaves, N >= 2048 ? 1 : 2) void fv_step_fft_kernel(
     const float *__restrict__ in, int64_t ld_in, float *__restrict__ out, int64_t ld_out,
     const float *__restrict__ face_flux, const double *__restrict__ pc, float c, float dt, float nu, float dx2,
@@ -312,7 +363,8 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 2048 ? 1 : 2) void fv_step_fft
 #pragma unroll
     for (int i = 0; i < V; ++i) v[i] = make_double2(rho_a[lane + 64 * i], two ? r[i] : 0.0);
   }
-  poisson_wave<N>(v, s_fft[wave], pc, lane);
+  poisson_pair<N, TRI>(v, s_fft[wave], reinterpret_cast<const double2 *>(pc + N), pc + 2 * N, TRI ? pc[0] : 0.0,
+                       lane);
   fv_finish_lane<N, false>(out + a * ld_out, v, ma, metrics ? metrics + a * ld_metrics : nullptr, lane);
   if (two) fv_finish_lane<N, true>(out + b * ld_out, v, mb, metrics ? metrics + b * ld_metrics : nullptr, lane);
 }
@@ -363,7 +415,7 @@ __device__ __forceinline__ void fv_run_E(float (&E)[N / 64], const double2 (&v)[
                                          MetricAcc &m, float *mo, int lane) {
 #pragma unroll
   for (int i = 0; i < N / 64; ++i) {
-    E[i] = (float)((imag ? v[i].y : v[i].x) / N);
+    E[i] = (float)(imag ? v[i].y : v[i].x);
     if (ro) ro[2 * N + lane + 64 * i] = E[i];
     if (mo) m.add_E(E[i]);
   }
@@ -415,7 +467,7 @@ __device__ __forceinline__ void mse_row(const float (&n)[N / 64], const float (&
 // the hybrid trajectory as both state0 (its row 0) and ref.  ref/mse (both or neither): the per-step channel
 // MSE [B][T+1][3] of the reference trajectory ref [B][T+1][3][N] minus this
 // rollout (hf_run_compare's classical twin, scored as it steps).
-template <int N, bool SCORE>
+template <int N, bool SCORE, bool TRI>
 __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_kernel(
     const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *__restrict__ pc, float c,
     float dt, float nu, float dx2, float *flux_traj, float *metrics, const float *ref, float *mse, int B, int T) {
@@ -425,9 +477,13 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_
   // the plan's twiddles and 1/k, staged once: the step loop then issues no
   // global load, so no vmcnt wait holds a wave until its trajectory stores
   // have drained (stores and loads share the counter)
-  __shared__ double2 s_plan[N];
-  for (int i = threadIdx.x; i < 2 * N; i += 64 * kFftWaves) reinterpret_cast<double *>(s_plan)[i] = pc[N + i];
-  __syncthreads();
+  // (TRI: the plan is h alone)
+  __shared__ double2 s_plan[TRI ? 1 : N];
+  if constexpr (!TRI) {
+    for (int i = threadIdx.x; i < 2 * N; i += 64 * kFftWaves) reinterpret_cast<double *>(s_plan)[i] = pc[N + i];
+    __syncthreads();
+  }
+  const double h = TRI ? pc[0] : 0.0;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform: scalar IC indices and bases
   const int64_t a = 2 * ((int64_t)blockIdx.x * kFftWaves + wave), b = a + 1;
   if (a >= B) return;  // a whole wave; nothing below synchronises the workgroup
@@ -471,7 +527,7 @@ __global__ __launch_bounds__(64 * kFftWaves, N >= 1024 ? 1 : 2) void fv_run_fft_
 #pragma unroll
       for (int i = 0; i < V; ++i) v[i].y = two ? r[i] : 0.0;
     }
-    poisson_wave_tw<N>(v, s_fft[wave], s_plan, reinterpret_cast<const double *>(s_plan) + N, lane);
+    poisson_pair<N, TRI>(v, s_fft[wave], s_plan, reinterpret_cast<const double *>(s_plan) + N, h, lane);
     fv_run_E<N>(Ea, v, false, ra, ma, ma_o, lane);
     if (two) fv_run_E<N>(Eb, v, true, rb, mb, mb_o, lane);
     if constexpr (SCORE) {
@@ -508,11 +564,16 @@ constexpr int kFvSmallMaxNx = 64;
 __global__ __launch_bounds__(kFvThreads) void fv_run_small_kernel(const float *state0, float *state_final,
                                                                   float *traj, const double *__restrict__ pc, int nx,
                                                                   float c, float dt, float nu, float dx2,
-                                                                  float *flux_traj, float *metrics, int B, int T) {
+                                                                  float *flux_traj, float *metrics, int B, int T,
+                                                                  int tri) {
   __shared__ double s_c[kFvSmallMaxNx];
   __shared__ float s_rho[kFvThreads / 64][kFvSmallMaxNx];
-  for (int i = threadIdx.x; i < nx; i += kFvThreads) s_c[i] = pc[i];
-  __syncthreads();
+  __shared__ double s_psi[kFvThreads / 64][kFvSmallMaxNx];  // tri: the wave's cyclic-reduction row
+  if (!tri) {
+    for (int i = threadIdx.x; i < nx; i += kFvThreads) s_c[i] = pc[i];
+    __syncthreads();
+  }
+  const double h = tri ? pc[0] : 0.0;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), i = threadIdx.x & 63;  // wave-uniform
   const int64_t b = (int64_t)blockIdx.x * (kFvThreads / 64) + wave;
   if (b >= B) return;  // a whole wave; nothing below synchronises the workgroup
@@ -528,7 +589,11 @@ __global__ __launch_bounds__(kFvThreads) void fv_run_small_kernel(const float *s
     const float n_new = continuity(n, F, Fm, c);
     const float u_new = velocity_classical(u, um, up, E, c, dt, nu, dx2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous step's rho reads are done
-    if (on) rho[i] = __fsub_rn(n_new, 1.0f);
+    if (tri) {
+      if (on) s_psi[wave][i] = (double)__fsub_rn(n_new, 1.0f);
+    } else if (on) {
+      rho[i] = __fsub_rn(n_new, 1.0f);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane's rho is in LDS
     float *row = traj ? traj + b * ldT + (int64_t)(t + 1) * S : nullptr;
     if (on) {
@@ -538,7 +603,8 @@ __global__ __launch_bounds__(kFvThreads) void fv_run_small_kernel(const float *s
       }
       if (flux_traj) flux_traj[b * (int64_t)T * nx + (int64_t)t * nx + i] = F;
     }
-    const float E_new = on ? poisson_cell(rho, s_c, i, nx) : 0.f;
+    if (tri) tridiag_psi_wave<double>(s_psi[wave], nx, i);
+    const float E_new = !on ? 0.f : tri ? (float)tri_E(s_psi[wave], i, nx, h) : poisson_cell(rho, s_c, i, nx);
     if (on && row) row[2 * nx + i] = E_new;
     n = n_new;
     u = u_new;
@@ -658,31 +724,47 @@ hipError_t launch_traj_mse(const float *a, const float *b, int B, int T1, int nx
   return hipGetLastError();
 }
 
-template <int N>
+template <int N, bool TRI>
 hipError_t fv_fft_launch(const float *in, int64_t ld_in, float *out, int64_t ld_out, const float *face_flux,
                          const double *pc, int B, float c, float dt, float nu, float dx2, float *flux_out,
                          int64_t ld_flux, float *metrics, int64_t ld_metrics, hipStream_t s) {
   const unsigned grid = (unsigned)((B + 2 * kFftWaves - 1) / (2 * kFftWaves));
   if (face_flux)
-    hipLaunchKernelGGL((fv_step_fft_kernel<true, N>), dim3(grid), dim3(64 * kFftWaves), 0, s, in, ld_in, out, ld_out,
-                       face_flux, pc, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
+    hipLaunchKernelGGL((fv_step_fft_kernel<true, N, TRI>), dim3(grid), dim3(64 * kFftWaves), 0, s, in, ld_in, out,
+                       ld_out, face_flux, pc, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
   else
-    hipLaunchKernelGGL((fv_step_fft_kernel<false, N>), dim3(grid), dim3(64 * kFftWaves), 0, s, in, ld_in, out,
+    hipLaunchKernelGGL((fv_step_fft_kernel<false, N, TRI>), dim3(grid), dim3(64 * kFftWaves), 0, s, in, ld_in, out,
                        ld_out, face_flux, pc, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, B);
   return hipGetLastError();
+}
+template <int N>
+hipError_t fv_fft_launch_pm(const float *in, int64_t ld_in, float *out, int64_t ld_out, const float *face_flux,
+                            const double *pc, int B, float c, float dt, float nu, float dx2, float *flux_out,
+                            int64_t ld_flux, float *metrics, int64_t ld_metrics, int pm, hipStream_t s) {
+  return pm == HF_POISSON_TRIDIAG
+             ? fv_fft_launch<N, true>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux,
+                                      metrics, ld_metrics, s)
+             : fv_fft_launch<N, false>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux,
+                                       metrics, ld_metrics, s);
+}
+
+bool poisson_mode_ok(int pm, int nx) {
+  return pm == HF_POISSON_SPECTRAL || (pm == HF_POISSON_TRIDIAG && nx >= 1 && nx <= kTriMaxNx);
 }
 
 hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld_out,
                           const float *face_flux, const double *pc, int B, int nx, float c,
                           float dt, float nu, float dx2, float *flux_out, int64_t ld_flux,
-                          float *metrics, int64_t ld_metrics, hipStream_t s) {
+                          float *metrics, int64_t ld_metrics, int pm, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  if (!poisson_mode_ok(pm, nx)) return hipErrorInvalidValue;
+  const int tri = pm == HF_POISSON_TRIDIAG;
   if (poisson_uses_fft(nx)) {
     switch (nx) {
-      case 256: return fv_fft_launch<256>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, s);
-      case 512: return fv_fft_launch<512>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, s);
-      case 1024: return fv_fft_launch<1024>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, s);
-      case 2048: return fv_fft_launch<2048>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, s);
+      case 256: return fv_fft_launch_pm<256>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, pm, s);
+      case 512: return fv_fft_launch_pm<512>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, pm, s);
+      case 1024: return fv_fft_launch_pm<1024>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, pm, s);
+      case 2048: return fv_fft_launch_pm<2048>(in, ld_in, out, ld_out, face_flux, pc, B, c, dt, nu, dx2, flux_out, ld_flux, metrics, ld_metrics, pm, s);
       default: return hipErrorInvalidValue;
     }
   }
@@ -694,8 +776,12 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
     else
       hipLaunchKernelGGL(fv_update_kernel<false>, grid, dim3(kFvThreads), 0, s, in, ld_in, out, ld_out, face_flux,
                          nx, c, dt, nu, dx2, flux_out, ld_flux);
-    hipLaunchKernelGGL(poisson_tiled_kernel, grid, dim3(kFvThreads), 0, s, out, ld_out, out + 2 * (int64_t)nx, ld_out,
-                       pc, nx);
+    if (tri)
+      hipLaunchKernelGGL(poisson_tri_kernel, dim3((unsigned)B), dim3(kFvThreads), sizeof(double) * nx, s, out, ld_out,
+                         out + 2 * (int64_t)nx, ld_out, pc, nx);
+    else
+      hipLaunchKernelGGL(poisson_tiled_kernel, grid, dim3(kFvThreads), 0, s, out, ld_out, out + 2 * (int64_t)nx, ld_out,
+                         pc, nx);
     if (metrics)
       hipLaunchKernelGGL(state_metrics_kernel, dim3(B), dim3(kFvThreads), 0, s, out, ld_out, nx, metrics, ld_metrics);
     return hipGetLastError();
@@ -704,46 +790,56 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
   if (face_flux)
     hipLaunchKernelGGL(fv_step_kernel<true>, dim3(B), dim3(kFvThreads), lds, s, in, ld_in, out,
                        ld_out, face_flux, pc, nx, c, dt, nu, dx2, flux_out, ld_flux, metrics,
-                       ld_metrics);
+                       ld_metrics, tri);
   else
     hipLaunchKernelGGL(fv_step_kernel<false>, dim3(B), dim3(kFvThreads), lds, s, in, ld_in, out,
                        ld_out, face_flux, pc, nx, c, dt, nu, dx2, flux_out, ld_flux, metrics,
-                       ld_metrics);
+                       ld_metrics, tri);
   return hipGetLastError();
 }
 
-template <int N>
+template <int N, bool TRI>
 hipError_t fv_run_fft_launch(const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *pc,
                              int B, int T, float c, float dt, float nu, float dx2, float *flux_traj, float *metrics,
                              const float *ref, float *mse, hipStream_t s) {
   const unsigned grid = (unsigned)((B + 2 * kFftWaves - 1) / (2 * kFftWaves));
   if (mse)
-    hipLaunchKernelGGL((fv_run_fft_kernel<N, true>), dim3(grid), dim3(64 * kFftWaves), 0, s, state0, ld_s0,
+    hipLaunchKernelGGL((fv_run_fft_kernel<N, true, TRI>), dim3(grid), dim3(64 * kFftWaves), 0, s, state0, ld_s0,
                        state_final, traj, pc, c, dt, nu, dx2, flux_traj, metrics, ref, mse, B, T);
   else
-    hipLaunchKernelGGL((fv_run_fft_kernel<N, false>), dim3(grid), dim3(64 * kFftWaves), 0, s, state0, ld_s0,
+    hipLaunchKernelGGL((fv_run_fft_kernel<N, false, TRI>), dim3(grid), dim3(64 * kFftWaves), 0, s, state0, ld_s0,
                        state_final, traj, pc, c, dt, nu, dx2, flux_traj, metrics, ref, mse, B, T);
   return hipGetLastError();
+}
+template <int N>
+hipError_t fv_run_fft_launch_pm(const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *pc,
+                                int B, int T, float c, float dt, float nu, float dx2, float *flux_traj, float *metrics,
+                                const float *ref, float *mse, int pm, hipStream_t s) {
+  return pm == HF_POISSON_TRIDIAG
+             ? fv_run_fft_launch<N, true>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj,
+                                          metrics, ref, mse, s)
+             : fv_run_fft_launch<N, false>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj,
+                                           metrics, ref, mse, s);
 }
 
 bool fv_run_fused(int nx) { return (poisson_uses_fft(nx) && nx <= kFvRunMaxNx) || (nx >= 1 && nx <= kFvSmallMaxNx); }
 
 hipError_t launch_fv_run(const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *pc, int B,
                          int nx, int T, float c, float dt, float nu, float dx2, float *flux_traj, float *metrics,
-                         const float *ref, float *mse, hipStream_t s) {
+                         const float *ref, float *mse, int pm, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if ((ref == nullptr) != (mse == nullptr)) return hipErrorInvalidValue;
+  if ((ref == nullptr) != (mse == nullptr) || !poisson_mode_ok(pm, nx)) return hipErrorInvalidValue;
   if (nx <= kFvSmallMaxNx) {  // contiguous states; no scoring at these nx (the fused hybrid kernel has its twin)
     if (mse || ld_s0 != 3LL * nx || !state_final) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((B + kFvThreads / 64 - 1) / (kFvThreads / 64));
     hipLaunchKernelGGL(fv_run_small_kernel, dim3(grid), dim3(kFvThreads), 0, s, state0, state_final, traj, pc, nx, c,
-                       dt, nu, dx2, flux_traj, metrics, B, T);
+                       dt, nu, dx2, flux_traj, metrics, B, T, pm == HF_POISSON_TRIDIAG ? 1 : 0);
     return hipGetLastError();
   }
   switch (fv_run_fused(nx) ? nx : 0) {
-    case 256: return fv_run_fft_launch<256>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, s);
-    case 512: return fv_run_fft_launch<512>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, s);
-    case 1024: return fv_run_fft_launch<1024>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, s);
+    case 256: return fv_run_fft_launch_pm<256>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, pm, s);
+    case 512: return fv_run_fft_launch_pm<512>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, pm, s);
+    case 1024: return fv_run_fft_launch_pm<1024>(state0, ld_s0, state_final, traj, pc, B, T, c, dt, nu, dx2, flux_traj, metrics, ref, mse, pm, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -764,8 +860,14 @@ hipError_t poisson_fft_launch(const float *n, int ld_n, float *E, int ld_E, cons
 }
 
 hipError_t launch_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B,
-                          int nx, hipStream_t s) {
+                          int nx, int pm, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  if (!poisson_mode_ok(pm, nx)) return hipErrorInvalidValue;
+  if (pm == HF_POISSON_TRIDIAG) {
+    hipLaunchKernelGGL(poisson_tri_kernel, dim3((unsigned)B), dim3(kFvThreads), sizeof(double) * nx, s, n,
+                       (int64_t)ld_n, E, (int64_t)ld_E, pc, nx);
+    return hipGetLastError();
+  }
   switch (poisson_uses_fft(nx) ? nx : 0) {
     case 256: return poisson_fft_launch<256>(n, ld_n, E, ld_E, pc, B, s);
     case 512: return poisson_fft_launch<512>(n, ld_n, E, ld_E, pc, B, s);

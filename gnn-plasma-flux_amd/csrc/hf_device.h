@@ -111,6 +111,102 @@ __device__ __forceinline__ float poisson_cell_nx(const double *s_rho, const doub
   return (float)(a0 + a1);
 }
 
+// ------------------------------------------ tridiagonal Poisson (opt-in mode)
+// HF_POISSON_TRIDIAG (include/hybridflux.h) is NOT the reference's operator:
+// the reference solves spectrally (src/baseline_solver.py:59-68, the default
+// here and the only parity mode).  It is the north star's cyclic-reduction
+// tridiagonal solve of the same equation, dE/dx = -(rho - mean rho), in the
+// second-order potential form on the periodic grid:
+//   (phi[i-1] - 2 phi[i] + phi[i+1]) / dx^2 = rho[i] - mean(rho),
+//   E[i] = -(phi[i+1] - phi[i-1]) / (2 dx).
+// Its Fourier symbol E_k = i (dx/2) cot(k dx/2) rho_k tends to the spectral
+// i rho_k / k as k dx -> 0 (0.02 relative at the k = 5 modes of the ICs at
+// nx = 64, ~1e-3 absolute in E).  With the unit right-hand side
+// d = rho - mean and phi = dx^2 psi:  E[i] = h (psi[i-1] - psi[i+1]), h = dx/2
+// (the whole plan of this mode, hf_poisson_plan).  The periodic system is
+// singular (constants) and E does not depend on the gauge, so psi[0] = 0 and
+// equation 0 is dropped: a Dirichlet tridiagonal system for psi[1..n-1].
+//
+// Cyclic reduction by one wave on a wave-private LDS row (T = double, or
+// double2 for a pair of ICs solved together): while the survivors (stride s)
+// are even in number, eliminate every other one,
+//   d[i] <- d[i-s] + 2 d[i] + d[i+s]          (i = 0 mod 2s; the coefficients
+// of the reduced system stay (1, -2, 1) at stride 2s); the R = n/s survivors
+// left (R odd, 1 for power-of-two n) are solved by lane 0 with psi[0] = 0 by
+// the Thomas recurrence of (1, -2, 1), whose pivots are -(j+1)/j in closed
+// form; then back-substitution level by level,
+//   psi[i] = ((psi[i-s] + psi[i+s]) - d[i]) / 2   (i = s mod 2s).
+// Float64 throughout.  Only the wave's own s_waitcnt orders the LDS levels (a
+// wave's LDS operations complete in order): no workgroup barrier.
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ double tri_zero(double) { return 0.0; }
+__device__ __forceinline__ double2 tri_zero(double2) { return make_double2(0.0, 0.0); }
+__device__ __forceinline__ double tri_add(double a, double b) { return a + b; }
+__device__ __forceinline__ double2 tri_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double tri_sub(double a, double b) { return a - b; }
+__device__ __forceinline__ double2 tri_sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double tri_scale(double a, double k) { return a * k; }
+__device__ __forceinline__ double2 tri_scale(double2 a, double k) { return make_double2(a.x * k, a.y * k); }
+__device__ __forceinline__ double tri_wave_sum(double a) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o, 64);
+  return a;
+}
+__device__ __forceinline__ double2 tri_wave_sum(double2 a) { return make_double2(tri_wave_sum(a.x), tri_wave_sum(a.y)); }
+
+// On entry x[0..n) = rho (any offset: the mean is removed here); on exit
+// x = psi with psi[0] = 0.  All 64 lanes of the wave call it (wave-uniform n).
+template <class T>
+__device__ void tridiag_psi_wave(T *x, int n, int lane) {
+  T acc = tri_zero(T());
+  for (int i = lane; i < n; i += 64) acc = tri_add(acc, x[i]);
+  const T mean = tri_scale(tri_wave_sum(acc), 1.0 / (double)n);
+  for (int i = lane; i < n; i += 64) x[i] = tri_sub(x[i], mean);
+  wave_lds_fence();
+  int s = 1;
+  for (; n % (2 * s) == 0; s *= 2) {  // forward reduction: survivors i = 2 s k
+    for (int k = lane; k < n / (2 * s); k += 64) {
+      const int i = 2 * s * k;
+      const T l = x[i == 0 ? n - s : i - s], r = x[i + s];
+      x[i] = tri_add(tri_add(l, r), tri_scale(x[i], 2.0));
+    }
+    wave_lds_fence();
+  }
+  if (lane == 0) {  // the R = n / s (odd) survivors j s, psi[0] = psi[R s] = 0
+    const int R = n / s;
+    T dp = tri_zero(T());
+    for (int j = 1; j < R; ++j) {
+      dp = tri_scale(tri_sub(x[j * s], dp), -(double)j / (double)(j + 1));
+      x[j * s] = dp;
+    }
+    T p = tri_zero(T());
+    for (int j = R - 1; j >= 1; --j) {
+      p = tri_add(x[j * s], tri_scale(p, (double)j / (double)(j + 1)));
+      x[j * s] = p;
+    }
+    x[0] = tri_zero(T());
+  }
+  wave_lds_fence();
+  for (s /= 2; s >= 1; s /= 2) {  // back-substitution: i = s + 2 s k
+    for (int k = lane; k < n / (2 * s); k += 64) {
+      const int i = s + 2 * s * k;
+      const T l = x[i - s], r = x[i + s == n ? 0 : i + s];
+      x[i] = tri_scale(tri_sub(tri_add(l, r), x[i]), 0.5);
+    }
+    wave_lds_fence();
+  }
+}
+
+// E at cell i from psi (tridiag_psi_wave): h (psi[i-1] - psi[i+1]), h = dx/2
+__device__ __forceinline__ double tri_E(const double *psi, int i, int n, double h) {
+  return h * (psi[i == 0 ? n - 1 : i - 1] - psi[i == n - 1 ? 0 : i + 1]);
+}
+__device__ __forceinline__ double2 tri_E(const double2 *psi, int i, int n, double h) {
+  const double2 l = psi[i == 0 ? n - 1 : i - 1], r = psi[i == n - 1 ? 0 : i + 1];
+  return make_double2(h * (l.x - r.x), h * (l.y - r.y));
+}
+
 // ---------------------------------------------------------------- FFT Poisson
 // For power-of-two nx in [kFftMinNx, kFftMaxNx] the spectral operator is
 // applied as the reference writes it (src/baseline_solver.py:59-68),

@@ -45,6 +45,12 @@ __host__ __device__ inline bool poisson_uses_fft(int nx) {
   return nx >= kFftMinNx && nx <= kFftMaxNx && (nx & (nx - 1)) == 0;
 }
 __host__ __device__ inline int poisson_plan_len(int nx) { return poisson_uses_fft(nx) ? 3 * nx : nx; }
+// Poisson mode of every FV/Poisson launcher below (pm): HF_POISSON_SPECTRAL
+// (the reference's operator; its plan is hf_poisson_coeffs) or
+// HF_POISSON_TRIDIAG (opt-in, not the reference's; plan = {dx/2}; one wave's
+// cyclic reduction over an LDS row of nx doubles, so nx <= kTriMaxNx).
+constexpr int kTriMaxNx = 16384;  // 128 KiB of LDS
+bool poisson_mode_ok(int pm, int nx);
 
 __host__ __device__ inline int chain_chunks(int layers, int prec) {
   return prec == kPrecF32 ? 16 * layers + 2 * kNT : 8 * layers + kNT;
@@ -101,6 +107,8 @@ hipError_t launch_pure_gnn_run(const float *params, int H, int L, const float *s
 int64_t pinn_ws_bytes(int D, int H, int64_t B);
 // scratch the rollouts actually use: the packed weights on their one-launch paths (baselines.hip)
 int64_t pure_gnn_run_ws_bytes(int H, int B, int nx, int T);
+// the one-launch PureGNN rollout also runs with no workspace (on nn.Linear's rows, unpacked)
+bool pure_gnn_run_ws_optional(int H, int nx, int T);
 int64_t pinn_run_ws_bytes(int D, int H, int64_t B);
 hipError_t launch_pinn_forward(const float *params, int D, int H, int L, const float *state, float *out, int64_t B,
                                void *ws, hipStream_t s);
@@ -125,6 +133,7 @@ struct RolloutExtras {
   float nu = 0.f, dx2 = 1.f;        // classical viscosity and f32(dx*dx)
   float *mse = nullptr;             // [B][T+1][3]; non-null enables the twin
   float *metrics_cl = nullptr;      // [B][T+1][HF_NUM_METRICS]
+  int poisson = HF_POISSON_SPECTRAL;  // Poisson mode (pm) of the hybrid step and the twin
 };
 hipError_t launch_chain_rollout_f32(const ChainW &, const float *, float *, const float *, const double *, int, int,
                                     int, float, float, float *, float *, float *, const RolloutExtras &,
@@ -132,7 +141,7 @@ hipError_t launch_chain_rollout_f32(const ChainW &, const float *, float *, cons
 // Cell-split rollout for small batches (chain_f32.hip; f32, nx in {32,48,64}, no classical twin).
 bool chain_rollout_prefers_cells(const ChainW &, int B, int nx);
 hipError_t launch_chain_rollout_cells(const ChainW &, const float *, float *, const float *, const double *, int,
-                                      int, int, float, float, float *, float *, float *, hipStream_t);
+                                      int, int, float, float, float *, float *, float *, int pm, hipStream_t);
 hipError_t launch_chain_rollout_k32(const ChainW &, const float *, float *, const float *, const double *, int, int,
                                     int, float, float, float *, float *, float *, const RolloutExtras &,
                                     hipStream_t);
@@ -180,7 +189,7 @@ hipError_t launch_rollout_summary(const float *met, const float *mse, const floa
 hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld_out,
                           const float *face_flux, const double *pc, int B, int nx, float c,
                           float dt, float nu, float dx2, float *flux_out, int64_t ld_flux,
-                          float *metrics, int64_t ld_metrics, hipStream_t s);
+                          float *metrics, int64_t ld_metrics, int pm, hipStream_t s);
 
 // The whole classical rollout (T steps of launch_fv_step's classical update)
 // in one launch, states held in registers: FFT nx up to 1024 (fv_run_fused).
@@ -192,14 +201,14 @@ hipError_t launch_fv_step(const float *in, int64_t ld_in, float *out, int64_t ld
 bool fv_run_fused(int nx);
 hipError_t launch_fv_run(const float *state0, int64_t ld_s0, float *state_final, float *traj, const double *pc, int B,
                          int nx, int T, float c, float dt, float nu, float dx2, float *flux_traj, float *metrics,
-                         const float *ref, float *mse, hipStream_t s);
+                         const float *ref, float *mse, int pm, hipStream_t s);
 
 // Metrics of a state batch (used for t=0 of non-fused rollouts).
 hipError_t launch_state_metrics(const float *st, int64_t ld, int B, int nx, float *metrics,
                                 int64_t ld_metrics, hipStream_t s);
 
 hipError_t launch_poisson(const float *n, int ld_n, float *E, int ld_E, const double *pc, int B,
-                          int nx, hipStream_t s);
+                          int nx, int pm, hipStream_t s);
 
 int64_t graph_workspace_bytes(const GraphW &w, int64_t N, int64_t E);
 // Training forward (activation tape) and backward, graph_train section of graph.hip.

@@ -557,7 +557,7 @@ hipError_t launch_ablation_loss(const float *fe, const float *st, const float *f
   float *En = reinterpret_cast<float *>(p + al256(sizeof(float) * (size_t)B * nx));
   float *part = reinterpret_cast<float *>(p + 2 * al256(sizeof(float) * (size_t)B * nx));
   hipLaunchKernelGGL(loss_update_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, nx, c, nn);
-  hipError_t e = launch_poisson(nn, nx, En, nx, pc, B, nx, s);  // detached E' (:138-145)
+  hipError_t e = launch_poisson(nn, nx, En, nx, pc, B, nx, HF_POISSON_SPECTRAL, s);  // detached E' (:138-145)
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(loss_terms_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, ft, sn, nn, En, B, nx, c, lam[0],
                      part, dfe);

@@ -27,6 +27,8 @@ HF_OP_RUN = 1
 HF_OP_COMPARE = 2
 HF_WS_TRAJ = 1
 HF_WS_FLUX_FACE = 2
+HF_POISSON_SPECTRAL = 0
+HF_POISSON_TRIDIAG = 1
 
 # name -> (restype, argtypes); mirrors include/hybridflux.h exactly.
 SIGNATURES = {
@@ -61,10 +63,21 @@ SIGNATURES = {
     "hf_poisson_plan_len": (c_int, [c_int]),
     "hf_poisson_coeffs": (c_int, [c_int, c_double, c_void_p]),
     "hf_poisson": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "hf_poisson_plan_size": (c_int, [c_int, c_int]),
+    "hf_poisson_plan": (c_int, [c_int, c_int, c_double, c_void_p]),
+    "hf_poisson_ex": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     "hf_run_workspace_bytes": (c_int64, [c_int, c_int, c_int, c_int]),
     "hf_workspace_need": (c_int64, [c_void_p, c_int, c_int, c_int, c_int, c_int]),
     "hf_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                         c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "hf_step_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                           c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "hf_run_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                          c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                          c_void_p]),
+    "hf_run_compare_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                  c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_int64, c_void_p]),
     "hf_run": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                        c_float, c_float, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                        c_void_p]),

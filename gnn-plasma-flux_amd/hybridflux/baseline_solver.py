@@ -5,7 +5,10 @@ classical step, rollout and Poisson solve run on the MI355X.
     dn/dt + d(nu)/dx = 0
     du/dt + d(u^2/2)/dx = E + nu d^2u/dx^2
     E from the spectral solve of the reference (src/baseline_solver.py:59-68),
-    which satisfies dE/dx = -(n - 1 - mean(n - 1)).
+    which satisfies dE/dx = -(n - 1 - mean(n - 1)); poisson="tridiagonal"
+    selects the opt-in cyclic-reduction solve of the same equation's
+    second-order potential form instead (NOT the reference's operator; see
+    engine.Grid).
 
 Single-IC methods keep the reference's numpy-in / numpy-out shape; the
 `*_batch` methods take [B,3,nx] torch tensors already on the device (or numpy,
@@ -20,7 +23,7 @@ from . import engine
 
 
 class BaselineSolver:
-    def __init__(self, nx=64, length=2 * math.pi, dt=5e-3, t_end=1.0, nu=1e-3, device="cuda"):
+    def __init__(self, nx=64, length=2 * math.pi, dt=5e-3, t_end=1.0, nu=1e-3, device="cuda", poisson="spectral"):
         self.nx = nx
         self.length = length
         self.dx = length / nx
@@ -29,7 +32,8 @@ class BaselineSolver:
         self.n0 = 1.0
         self.nu = nu
         self.device = torch.device(device)
-        self.grid = engine.Grid(nx, length, dt, nu)
+        self.grid = engine.Grid(nx, length, dt, nu, poisson=poisson)
+        self.poisson = poisson
         self.x = self.grid.x
         self.k = 2.0 * np.pi * np.fft.fftfreq(nx, d=self.dx)
         if self.dt / self.dx > 0.5:  # src/baseline_solver.py:23-24

@@ -119,12 +119,25 @@ class DeviceModel:
             pass
 
 
+POISSON_MODES = {"spectral": _lib.HF_POISSON_SPECTRAL, "tridiagonal": _lib.HF_POISSON_TRIDIAG}
+
+
 class Grid:
     """Geometry + time-step constants (src/baseline_solver.py:7-27) and their
-    device copies: cell centres x (float32) and the circulant Poisson column."""
+    device copies: cell centres x (float32) and the Poisson plan.
 
-    def __init__(self, nx=64, length=2 * math.pi, dt=5e-3, nu=1e-3):
+    poisson selects the operator every step / rollout / solve of this grid
+    applies: "spectral" (default) is the reference's (src/baseline_solver.py:
+    59-68, the parity mode); "tridiagonal" is the OPT-IN cyclic-reduction solve
+    of the second-order potential form of the same equation, which is NOT the
+    reference's operator (~1e-3 from it at nx = 64; include/hybridflux.h
+    HF_POISSON_TRIDIAG).  The training loss always uses the spectral plan."""
+
+    def __init__(self, nx=64, length=2 * math.pi, dt=5e-3, nu=1e-3, poisson="spectral"):
+        if poisson not in POISSON_MODES:
+            raise ValueError(f"poisson must be one of {sorted(POISSON_MODES)}, got {poisson!r}")
         self.nx, self.length, self.dt, self.nu = int(nx), float(length), float(dt), float(nu)
+        self.poisson, self.pmode = poisson, POISSON_MODES[poisson]
         self.dx = self.length / self.nx
         self.x = np.linspace(0.5 * self.dx, self.length - 0.5 * self.dx, self.nx)
         self.c32 = float(np.float32(self.dt / self.dx))
@@ -133,16 +146,34 @@ class Grid:
         self.dx2_32 = float(np.float32(self.dx ** 2))
         pc = np.empty(lib().hf_poisson_plan_len(self.nx), dtype=np.float64)
         check(lib().hf_poisson_coeffs(self.nx, self.length, pc.ctypes.data_as(c_void_p)))
-        self.poisson_c = pc
+        self.poisson_c = pc  # the spectral plan (also the training loss's)
+        if self.pmode == _lib.HF_POISSON_SPECTRAL:
+            self.plan = pc
+        else:
+            self.plan = np.empty(lib().hf_poisson_plan_size(self.pmode, self.nx), dtype=np.float64)
+            if self.plan.size < 1:
+                raise ValueError(f"{poisson} Poisson does not support nx = {self.nx}")
+            check(lib().hf_poisson_plan(self.pmode, self.nx, self.length, self.plan.ctypes.data_as(c_void_p)))
         self._dev = {}
 
-    def on(self, device):
+    def _consts(self, device):
         device = torch.device(device)
         key = str(device)
         if key not in self._dev:
-            self._dev[key] = (torch.as_tensor(self.x.astype(np.float32), device=device),
-                              torch.as_tensor(self.poisson_c, device=device))
+            x = torch.as_tensor(self.x.astype(np.float32), device=device)
+            pc = torch.as_tensor(self.poisson_c, device=device)
+            plan = pc if self.plan is self.poisson_c else torch.as_tensor(self.plan, device=device)
+            self._dev[key] = (x, plan, pc)
         return self._dev[key]
+
+    def on(self, device):
+        """(x, Poisson plan of this grid's mode) on device."""
+        x, plan, _ = self._consts(device)
+        return x, plan
+
+    def spectral_plan(self, device):
+        """The spectral plan on device (hf_ablation_loss: the reference trainer's solve)."""
+        return self._consts(device)[2]
 
 
 def _state(t, nx):
@@ -186,8 +217,8 @@ def step(model, grid, state, flux_face=False, metrics=False, ws=None):
     x, pc = grid.on(dev)
     w, wb = workspace(HF_OP_STEP, B, grid.nx, 1, dev, ws, model=model, flux_face=flux_face)
     with torch.cuda.device(dev):
-        check(lib().hf_step(model.handle if model else None, ptr(state), ptr(out), ptr(x), ptr(pc), B,
-                            grid.nx, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(F), ptr(M), ptr(w), wb,
+        check(lib().hf_step_ex(model.handle if model else None, ptr(state), ptr(out), ptr(x), ptr(pc),
+                               grid.pmode, B, grid.nx, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(F), ptr(M), ptr(w), wb,
                             stream_of(dev)))
     return out, F, M
 
@@ -216,8 +247,8 @@ def run(model, grid, state0, T, traj=True, flux=False, metrics=False, out=None, 
     x, pc = grid.on(dev)
     w, wb = workspace(HF_OP_RUN, B, grid.nx, T, dev, ws, model=model, traj=tr)
     with torch.cuda.device(dev):
-        check(lib().hf_run(model.handle if model else None, ptr(state0), ptr(final), ptr(x), ptr(pc), B,
-                           grid.nx, T, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(tr), ptr(fl),
+        check(lib().hf_run_ex(model.handle if model else None, ptr(state0), ptr(final), ptr(x), ptr(pc),
+                              grid.pmode, B, grid.nx, T, grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(tr), ptr(fl),
                            ptr(me), ptr(w), wb, stream_of(dev)))
     return {"final": final, "traj": tr, "flux": fl, "metrics": me}
 
@@ -236,7 +267,8 @@ def run_compare(model, grid, state0, T, metrics=True, out=None, ws=None):
     x, pc = grid.on(dev)
     w, wb = workspace(HF_OP_COMPARE, B, grid.nx, T, dev, ws, model=model)
     with torch.cuda.device(dev):
-        check(lib().hf_run_compare(model.handle, ptr(state0), ptr(final), ptr(x), ptr(pc), B, grid.nx, T,
+        check(lib().hf_run_compare_ex(model.handle, ptr(state0), ptr(final), ptr(x), ptr(pc), grid.pmode, B,
+                                      grid.nx, T,
                                    grid.c32, grid.dt32, grid.nu32, grid.dx2_32, ptr(mse), ptr(me), ptr(mc),
                                    ptr(w), wb, stream_of(dev)))
     return {"final": final, "mse": mse, "metrics": me, "metrics_classical": mc}
@@ -328,14 +360,15 @@ def graph_backward(params, dims, nf, ei, chain_nx, tape, grad_flux, want_nf_grad
 
 
 def poisson(grid, n):
-    """Spectral Poisson E for densities n [B,nx] (src/baseline_solver.py:59-68)."""
+    """Poisson E for densities n [B,nx]: the grid's mode (spectral: src/baseline_solver.py:59-68)."""
     require_device(n, "n")
     n = n.to(torch.float32).contiguous()
     B = n.shape[0]
     E = torch.empty_like(n)
     _, pc = grid.on(n.device)
     with torch.cuda.device(n.device):
-        check(lib().hf_poisson(ptr(n), grid.nx, ptr(E), grid.nx, ptr(pc), B, grid.nx, stream_of(n.device)))
+        check(lib().hf_poisson_ex(ptr(n), grid.nx, ptr(E), grid.nx, ptr(pc), grid.pmode, B, grid.nx,
+                                  stream_of(n.device)))
     return E
 
 
@@ -412,7 +445,7 @@ def ablation_loss_terms(grid, flux_edge, st, ft, sn, lam):
     dfe = torch.empty(B, 2 * nx, device=dev)
     ws = torch.empty(int(lib().hf_ablation_loss_workspace_bytes(B, nx)), dtype=torch.uint8, device=dev)
     lam_h = np.asarray(lam, dtype=np.float32)
-    _, pc = grid.on(dev)
+    pc = grid.spectral_plan(dev)
     with torch.cuda.device(dev):
         check(lib().hf_ablation_loss(ptr(fe), ptr(st), ptr(ft), ptr(sn), B, nx, grid.c32, float(np.float32(grid.dx)),
                                      ptr(lam_h), ptr(pc), ptr(loss), ptr(fl), ptr(dfe), ptr(ws),

@@ -41,12 +41,16 @@ def load_state_dict(model_path):
 
 class HybridSolver:
     def __init__(self, model_path, radius, nx=64, length=2 * math.pi, dt=5e-3, t_end=1.0, device="cuda",
-                 precision="f32"):
+                 precision="f32", poisson="spectral"):
         """precision: chain-kernel arithmetic, "f32" (default, exact float32
         MFMA), "f16x3" (float32-accurate split-fp16 MFMA, ~5x the matrix rate)
-        or "bf16" (bf16 weights/activations, BASELINE config 4)."""
+        or "bf16" (bf16 weights/activations, BASELINE config 4).
+        poisson: "spectral" (default, the reference's operator) or
+        "tridiagonal" (opt-in, NOT the reference's: the north star's
+        cyclic-reduction solve fused into the same step kernels; engine.Grid)."""
         self.device = torch.device(device)
-        self.baseline = BaselineSolver(nx=nx, length=length, dt=dt, t_end=t_end, device=self.device)
+        self.baseline = BaselineSolver(nx=nx, length=length, dt=dt, t_end=t_end, device=self.device,
+                                       poisson=poisson)
         model = FluxGNN(input_dim=MODEL_CONFIG["input_dim"], hidden_dim=MODEL_CONFIG["hidden_dim"],
                         num_layers=MODEL_CONFIG["num_layers"], precision=precision)
         model.load_state_dict(load_state_dict(model_path))

@@ -95,9 +95,15 @@ def gather_ic_rows_packed(tensors, n_total, group=None):
     side into one [b_local, sum of row sizes] buffer, gathered, and split back
     into [n_total, ...] tensors.  One RCCL call instead of one per tensor (each
     call pays the collective's latency across the ranks)."""
+    tensors = list(tensors)
+    t0 = tensors[0]
+    for t in tensors[1:]:  # torch.cat would silently promote a mixed dtype for every part
+        if t.dtype != t0.dtype or t.device != t0.device or t.shape[0] != t0.shape[0]:
+            raise ValueError(f"gather_ic_rows_packed: tensors must share dtype, device and leading size; got "
+                             f"{t0.dtype}/{t0.device}/{t0.shape[0]} and {t.dtype}/{t.device}/{t.shape[0]}")
     if not dist.is_initialized():
-        return list(tensors)
-    b = tensors[0].shape[0]
+        return tensors
+    b = t0.shape[0]
     widths = [int(math.prod(t.shape[1:])) for t in tensors]
     packed = torch.cat([t.reshape(b, w) for t, w in zip(tensors, widths)], dim=1)
     flat = gather_ic_rows(packed, n_total, group)

@@ -198,8 +198,8 @@ int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const
  * rollout is ONE launch for all T steps for nx in {16, 32, 48, 64} with H in
  * {64, 128} (one IC per workgroup, activations in LDS); its workspace holds a
  * packed copy of the message/output weights made at the start of the call (the
- * copy for up to 8 layers; with more layers the launch reads nn.Linear's rows
- * in place).  Otherwise, on chains whose nx divides 128 with H a multiple of 64,
+ * copy for up to 8 layers; with more layers, or with dev_workspace == NULL, the
+ * launch reads nn.Linear's rows in place, slower).  Otherwise, on chains whose nx divides 128 with H a multiple of 64,
  * each message layer is one f32 MFMA GEMM that forms the messages and the
  * residual in its epilogue (csrc/tgemm.h EpiMsg); other shapes run the generic
  * linear + gather kernels.
@@ -213,7 +213,10 @@ int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const
  * whose workspace holds a packed copy of the weights made at the start of the
  * call (hf_pinn_workspace_bytes: the copy for the largest layer count, 8);
  * other shapes run per-layer GEMMs through the workspace.  B = 0 or T = 0
- * needs none.
+ * needs none.  ABI note (round 4): hf_pinn_run / hf_pinn_forward require the
+ * workspace whenever hf_pinn_workspace_bytes > 0 (a NULL workspace is
+ * HF_EINVAL; it used to be accepted); hf_pure_gnn_run accepts NULL on its
+ * one-launch shapes.
  */
 int64_t hf_pure_gnn_param_count(int in_dim, int hidden, int layers);
 int64_t hf_pure_gnn_workspace_bytes(int hidden, int64_t N, int64_t E);
@@ -250,6 +253,37 @@ int hf_poisson_coeffs(int nx, double length, double *host_c);
  * dev_c: device copy of hf_poisson_coeffs. */
 int hf_poisson(const float *dev_n, int ld_n, float *dev_E, int ld_E,
                const double *dev_c, int B, int nx, void *stream);
+
+/*
+ * Poisson modes.  Every entry point without a mode argument, and every *_ex
+ * call given HF_POISSON_SPECTRAL, applies the reference's spectral operator
+ * (src/baseline_solver.py:59-68) with the plan of hf_poisson_coeffs: the
+ * parity mode and the default.
+ *
+ * HF_POISSON_TRIDIAG is an OPT-IN mode that is NOT the reference's operator
+ * (no parity with the reference is claimed for it): the cyclic-reduction
+ * tridiagonal solve the north star names, of the same equation dE/dx =
+ * -(rho - mean rho), rho = n - 1, in second-order potential form on the
+ * periodic grid:
+ *   (phi[i-1] - 2 phi[i] + phi[i+1]) / dx^2 = rho[i] - mean(rho),
+ *   E[i] = -(phi[i+1] - phi[i-1]) / (2 dx),
+ * solved in float64 by one wave per IC (or IC pair) with phi[0] = 0 (E does not
+ * depend on the gauge) and rounded to float32 once.  It differs from the
+ * spectral E by ~1e-3 at nx = 64 (the symbol (dx/2) cot(k dx/2) vs 1/k).
+ * Fused into the same kernels as the spectral solve (the persistent rollouts
+ * at nx <= 64, the FV kernels at every other nx); nx <= 16384.  The training
+ * loss (hf_ablation_loss) always uses the spectral operator.
+ */
+#define HF_POISSON_SPECTRAL 0
+#define HF_POISSON_TRIDIAG 1
+/* Length in doubles of the plan of `mode` for nx cells (-1: unsupported):
+ * hf_poisson_plan_len(nx) for SPECTRAL, 1 for TRIDIAG (plan[0] = dx/2). */
+int hf_poisson_plan_size(int mode, int nx);
+/* Host helper (no device work): the plan of `mode` (SPECTRAL: hf_poisson_coeffs). */
+int hf_poisson_plan(int mode, int nx, double length, double *host_plan);
+/* hf_poisson with a Poisson mode; dev_plan is a device copy of hf_poisson_plan(mode, ...). */
+int hf_poisson_ex(const float *dev_n, int ld_n, float *dev_E, int ld_E, const double *dev_plan,
+                  int poisson_mode, int B, int nx, void *stream);
 
 /*
  * Scratch of the generic (non-fused) sequencing.  hf_step, hf_run and
@@ -295,6 +329,13 @@ int hf_step(hf_model_t model, const float *dev_state_in, float *dev_state_out,
             float c, float dt, float nu, float dx2,
             float *dev_flux_face, float *dev_metrics,
             void *dev_workspace, int64_t workspace_bytes, void *stream);
+/* hf_step with a Poisson mode (dev_plan: hf_poisson_plan(poisson_mode, ...));
+ * hf_step == hf_step_ex(..., dev_c, HF_POISSON_SPECTRAL, ...). */
+int hf_step_ex(hf_model_t model, const float *dev_state_in, float *dev_state_out,
+               const float *dev_x, const double *dev_plan, int poisson_mode, int B, int nx,
+               float c, float dt, float nu, float dx2,
+               float *dev_flux_face, float *dev_metrics,
+               void *dev_workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * T-step rollout (HybridSolver.run src/hybrid_solver.py:66-73 when model !=
@@ -323,6 +364,12 @@ int hf_run(hf_model_t model, const float *dev_state0, float *dev_state_final,
            float c, float dt, float nu, float dx2,
            float *dev_traj, float *dev_flux_traj, float *dev_metrics,
            void *dev_workspace, int64_t workspace_bytes, void *stream);
+/* hf_run with a Poisson mode; same paths, workspace and aliasing rules. */
+int hf_run_ex(hf_model_t model, const float *dev_state0, float *dev_state_final,
+              const float *dev_x, const double *dev_plan, int poisson_mode, int B, int nx, int T,
+              float c, float dt, float nu, float dx2,
+              float *dev_traj, float *dev_flux_traj, float *dev_metrics,
+              void *dev_workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * Hybrid rollout scored against the classical solver from the same ICs, in
@@ -350,6 +397,13 @@ int hf_run_compare(hf_model_t model, const float *dev_state0, float *dev_state_f
                    float c, float dt, float nu, float dx2, float *dev_mse,
                    float *dev_metrics, float *dev_metrics_classical,
                    void *dev_workspace, int64_t workspace_bytes, void *stream);
+/* hf_run_compare with a Poisson mode: the hybrid rollout AND its classical
+ * twin both use it. */
+int hf_run_compare_ex(hf_model_t model, const float *dev_state0, float *dev_state_final,
+                      const float *dev_x, const double *dev_plan, int poisson_mode, int B, int nx, int T,
+                      float c, float dt, float nu, float dx2, float *dev_mse,
+                      float *dev_metrics, float *dev_metrics_classical,
+                      void *dev_workspace, int64_t workspace_bytes, void *stream);
 
 /*
  * Metric series of recorded trajectories (the host-side scoring of

@@ -241,10 +241,12 @@ def test_baseline_rollout_workspace_queries():
     assert L.hf_pinn_workspace_bytes(192, 256, 0) == 0
     assert L.hf_pinn_workspace_bytes(96, 128, 7) > 0
     assert L.hf_pinn_workspace_bytes(0, 128, 7) == -1
-    # the one-launch rollouts need their workspace (the packed weights): a NULL
-    # one is refused before any device call
+    # PureGNN's per-step path and the one-launch PINN rollout need their
+    # workspace: a NULL one is refused before any device call (the one-launch
+    # PureGNN rollout accepts NULL and reads nn.Linear's rows: not called here,
+    # it would launch on the dummy pointers)
     dummy = ctypes.c_void_p(1)
-    assert L.hf_pure_gnn_run(dummy, 128, 4, dummy, dummy, dummy, 4096, 64, 50, None, None, None) == _lib.HF_EINVAL
+    assert L.hf_pure_gnn_run(dummy, 128, 4, dummy, dummy, dummy, 7, 100, 5, None, None, None) == _lib.HF_EINVAL
     assert b"NULL workspace" in L.hf_last_error()
     assert L.hf_pinn_run(dummy, 192, 256, 4, dummy, dummy, 4096, 50, None, None, None) == _lib.HF_EINVAL
     assert b"NULL workspace" in L.hf_last_error()

@@ -131,3 +131,39 @@ def test_packed_gather_one_collective(world):
     gathered in ONE collective, split back in global IC order (world 8: three
     empty shards)."""
     mp.spawn(_packed_worker, args=(world, _free_port()), nprocs=world, join=True)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_sets_ipc_mode_torchrun_style():
+    """A bench.py process started by a launcher (WORLD_SIZE already set, as
+    torchrun / the driver's 8-GPU run do) has HSA_ENABLE_IPC_MODE_LEGACY=0 in
+    its environment before anything can touch the GPU (RCCL needs dmabuf IPC on
+    this host driver), not only when bench.py launches its own ranks."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k != "HSA_ENABLE_IPC_MODE_LEGACY"}
+    env.update(WORLD_SIZE="2", RANK="1", LOCAL_RANK="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    code = ("import os, sys; sys.argv = ['bench.py']; import bench; "
+            "print('IPC=' + str(os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY')))")
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "IPC=0" in p.stdout.splitlines()
+
+
+def test_bench_group_setup_times_out_without_peer():
+    """Rank 0 of 2 whose peer never starts: bench.init_group must give up
+    within HF_DIST_TIMEOUT_S instead of the 10-minute default (run in its own
+    interpreter, as a rank is)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="2",
+               HF_DIST_TIMEOUT_S="5")
+    code = ("import sys, time, torch; sys.argv = ['bench.py']; import bench; t0 = time.perf_counter()\n"
+            "try:\n    bench.init_group('gloo', 2, torch.device('cpu')); print('RESULT joined')\n"
+            "except Exception as e:\n    print('RESULT', type(e).__name__, round(time.perf_counter() - t0, 1))\n")
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    res = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT")]
+    assert res and "joined" not in res[0], (p.stdout[-1000:], p.stderr[-2000:])
+    assert float(res[0].split()[-1]) < 60, res

@@ -148,3 +148,25 @@ def test_cfg5_full_size_eight_ranks_equal_one_rank_bitwise(tmp_path):
         assert x.shape == y.shape and x.shape[0] == 32768, (key, x.shape, y.shape)
         assert np.array_equal(x.view(np.uint32), y.view(np.uint32)), key
     assert np.isfinite(a["cfg5_32768_f32/final"]).all()
+
+
+@pytest.mark.timeout(300)
+def test_rank_exiting_early_fails_the_job_within_timeout():
+    """8-GPU readiness: a 2-rank torchrun-style bench.py
+    job (gloo on this box's one GPU) in which rank 1 vanishes before the group
+    forms (HF_BENCH_EXIT_RANK=1, exit code 0, so the launcher keeps waiting on
+    rank 0) must end non-zero within the group timeout (HF_DIST_TIMEOUT_S)
+    instead of hanging for the 10-minute default."""
+    import time
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--ics-per-gpu", "64",
+           "--no-cpu-baseline", "--no-other-configs", "--also", ""]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, env=_env(HF_BENCH_EXIT_RANK="1", HF_DIST_TIMEOUT_S="20"), capture_output=True,
+                       text=True, timeout=240, cwd=ROOT)
+    secs = time.perf_counter() - t0
+    assert p.returncode != 0, p.stdout[-2000:]
+    assert secs < 200, secs
+    assert "exiting early" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]  # no bench line from a broken job

@@ -122,19 +122,43 @@ def test_f16x3_range(hf):
 # values compared: the oracle itself, accumulating in float32 instead of
 # float64, differs from its own float64 form by up to 1.3e-3 on the
 # random-weight cases (max over 5 ICs; mean 7e-6).  Random-weight cases are
-# therefore held to a flip-sized maximum plus a MEAN error bound, which a
-# systematic error (wrong neighbour, wrong weight, wrong rounding mode) breaks.
+# therefore held to a FLIP COUNT instead of a maximum (round 5; the 4e-3
+# maximum let one flip reach 1.77e-3 unremarked): every edge flux either
+# agrees with EMUL to the no-flip f32-accumulation gate below, or it is
+# downstream of a bf16 rounding flip; the edges outside the no-flip gate are
+# counted (recorded) and held to a small fraction of all edges, and the MEAN
+# error stays bounded.  A systematic error (wrong neighbour, wrong weight,
+# wrong rounding mode) moves most edges off the no-flip gate and fails both.
 BF16_FLUX_EMUL = 1.1e-3    # edge flux vs EMUL, one evaluation
 BF16_STATE_EMUL = 1e-3     # 30-step state vs EMUL
 BF16_FLUX_WBF16 = 7.5e-3   # edge flux vs WBF16
 BF16_STATE_WBF16 = 1e-2    # 30-step state vs WBF16
-BF16_FLUX_EMUL_RAND = 4e-3    # edge flux vs EMUL, random weights: max (a few flips)
+BF16_FLUX_EMUL_RAND_FLIP_FRAC = 0.1  # edges off the no-flip gate (flip-affected), random weights, L >= 2
 BF16_FLUX_EMUL_RAND_MEAN = 5e-5  # ... and mean |error|
 # With at most one update layer the only bf16 roundings of accumulated values
 # are h0 and h1, and these cases show no flip (max 4.2e-7 = a few f32 ulps of
 # the readout sum, identical in every recorded pass since round 2): they are
 # held to an f32-accumulation-order gate instead of the flip-sized one.
 BF16_FLUX_EMUL_RAND_NOFLIP = 1e-5
+
+
+def bf16_random_weight_gate(fe, want, layers, record, key):
+    """The random-weight bf16 gate (comment above): at most one update layer,
+    every edge within the no-flip gate; otherwise the edges off it (downstream
+    of a bf16 rounding flip) counted, recorded and held to a fraction of all
+    edges, and the mean |error| bounded."""
+    err = np.abs(np.asarray(fe, np.float64) - want)
+    off = int((err > BF16_FLUX_EMUL_RAND_NOFLIP).sum())
+    record(key, "max_abs_vs_emul", err.max())
+    record(key, "mean_abs_vs_emul", err.mean())
+    record(key, "flip_affected_edges", off)
+    record(key, "edges", err.size)
+    assert np.isfinite(fe).all()
+    if layers <= 1:
+        close(fe, want, BF16_FLUX_EMUL_RAND_NOFLIP)
+    else:
+        assert off <= BF16_FLUX_EMUL_RAND_FLIP_FRAC * err.size, (off, err.size)
+    assert err.mean() <= BF16_FLUX_EMUL_RAND_MEAN, err.mean()
 
 
 def _bf16_solver(hf, nx, dt):
@@ -319,7 +343,4 @@ def test_bf16_flux_layers_and_nx(hf, record, layers, nx):
     nf, ei = hf.build_chain_graph_batch(ics, G.x, DEV)
     with torch.no_grad():
         fe = m(nf, ei).cpu().numpy().reshape(5, 2 * nx)
-    record(f"bf16_flux_L{layers}_nx{nx}", "max_abs_vs_emul", np.abs(fe - want).max())
-    record(f"bf16_flux_L{layers}_nx{nx}", "mean_abs_vs_emul", np.abs(fe - want).mean())
-    close(fe, want, BF16_FLUX_EMUL_RAND_NOFLIP if layers <= 1 else BF16_FLUX_EMUL_RAND)
-    assert np.abs(fe - want).mean() <= BF16_FLUX_EMUL_RAND_MEAN
+    bf16_random_weight_gate(fe, want, layers, record, f"bf16_flux_L{layers}_nx{nx}")
