@@ -42,6 +42,7 @@ STATE_BYTES_PER_CELL_STEP = 24     # read (n,u,E) + write (n,u,E) float32
 PEAK_F32_MFMA_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 PEAK_F16_MFMA_TFLOPS = 2500.0      # MI355X_MICROARCH.md: dense FP16/BF16 matrix peak (no sparsity)
 PEAK_HBM_GBS = 8000.0
+PEAK_L2_GBS = 34500.0              # MI355X_MICROARCH.md: L2 aggregate ~34.5 TB/s
 METRIC = "hybrid rollout timesteps/sec (batched ICs) at 1/2/4/8 MI355X"
 
 
@@ -173,6 +174,13 @@ def other_models(dev, B, K, warm_s=0.3):
     flop = {"pure_gnn": nx * 2 * (4 * H + L * 2 * H * H + H * H + 3 * H),       # tools/bench_models.py
             "pinn": 2 * (3 * nx * 256 + 2 * 256 * 256 + 256 * 3 * nx)}
     fns = {"pure_gnn": lambda: pg.rollout(ics, K, solver.x), "pinn": lambda: pn.rollout(ics, K)}
+    # L2 -> CU weight bytes per step of the one-launch rollouts (csrc/baselines.hip): PureGNN one IC
+    # per workgroup, each reading the message layers' [W_a ; W_b] and output_mlp.0 (the packed copy);
+    # PINN 16 ICs per workgroup, each reading every layer's weights
+    pg_w = 4 * (L * 2 * H * H + H * H)
+    pn_w = 4 * sum(int(v.numel()) for k, v in pn.state_dict().items() if k.endswith("weight"))
+    l2_bytes = {"pure_gnn": B * pg_w, "pinn": -(-B // 16) * pn_w}
+    l2_model = {"pure_gnn": f"{B} workgroups x {pg_w} B per step", "pinn": f"{-(-B // 16)} workgroups x {pn_w} B per step"}
     out = {}
     stream = torch.cuda.current_stream(dev)
     for name, fn in fns.items():
@@ -188,9 +196,15 @@ def other_models(dev, B, K, warm_s=0.3):
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
         kms = e0.elapsed_time(e1)
+        l2 = l2_bytes[name] * K
         out[name] = {"value": round(B * K / wall, 1), "unit": "IC-steps/s", "ics": B, "nx": nx, "steps": K,
                      "kernel_ms": round(kms, 3), "flop_per_ic_step": flop[name],
-                     "mfma_frac": round(flop[name] * B * K / (kms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)}
+                     "mfma_frac": round(flop[name] * B * K / (kms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4),
+                     # the other roof of these weight-streaming kernels: every workgroup reads
+                     # the whole weight set from L2 each step (algorithmic L2 -> CU bytes)
+                     "l2_weight_bytes": l2, "l2_GBs": round(l2 / (kms * 1e-3) / 1e9, 1),
+                     "l2_frac": round(l2 / (kms * 1e-3) / (PEAK_L2_GBS * 1e9), 4),
+                     "l2_model": l2_model[name]}
     return out
 
 

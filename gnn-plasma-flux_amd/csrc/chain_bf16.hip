@@ -222,8 +222,13 @@ struct CoreBF16 {
       if constexpr (U == UPC - 1) F.slot = R.next();
       load_unit(F, (U + 1) % UPC, R.lane);
     } else {
+#ifdef HF_DIAG_NODS  // timing diagnostic only: results are wrong (no fragment ds_reads: lane-made fragments)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = u4{(unsigned)R.lane, (unsigned)(4 * U + i), 0x3f803f80u, (unsigned)R.lane};
+#else
 #pragma unroll
       for (int i = 0; i < 4; ++i) w[i] = __builtin_bit_cast(u4, ldf4(F.slot + ((4 * U + i) * 64 + R.lane) * 4));
+#endif
       if constexpr (U == kDmaUnit) R.issue_pending();
       if constexpr (U == UPC - 1) F.slot = R.next();
     }

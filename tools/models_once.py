@@ -1,0 +1,44 @@
+"""The PureGNN and PINN one-launch rollouts of bench.py's other_models
+(4096 ICs x 64 cells, 30 steps, trajectory recorded), warmed, then one
+rollout each: a short program for rocprofv3 counter passes
+(tools/gpu_models_l2.sh).  Prints each rollout's HIP-event time."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gnn-plasma-flux_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    from hybridflux import BaselineSolver
+    from hybridflux.baselines import PINN, PureGNN
+    dev = torch.device("cuda", 0)
+    B, K = 4096, 30
+    b = np.load(os.path.join(ROOT, "tests", "golden", "baselines.npz"))
+    solver = BaselineSolver(64, device=dev)
+    ics = solver.initial_conditions(range(1000, 1000 + B), as_tensor=True)
+    pg = PureGNN(4, 128, 4)
+    pg.load_state_dict({k[9:]: torch.from_numpy(b[k]) for k in b.files if k.startswith("pure_gnn.")})
+    pn = PINN(3 * 64, 256, 4)
+    pn.load_state_dict({k[5:]: torch.from_numpy(b[k]) for k in b.files if k.startswith("pinn.")})
+    pg, pn = pg.to(dev), pn.to(dev)
+    for name, fn in (("pure_gnn", lambda: pg.rollout(ics, K, solver.x)), ("pinn", lambda: pn.rollout(ics, K))):
+        t_end = time.perf_counter() + 0.3
+        while time.perf_counter() < t_end:
+            fn()
+            torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"{name} {e0.elapsed_time(e1):.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
