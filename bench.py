@@ -66,6 +66,20 @@ def cpu_baseline(weights, nx, T, n_ics, threads):
     return alpha, beta
 
 
+def cpu_batched(weights, nx, T, n_ics, threads):
+    """The batched torch-CPU form of the port alone, on `threads` threads (the
+    (beta) context figure at the process's full CPU affinity set)."""
+    from oracle import hybrid_oracle as O
+    torch.set_num_threads(threads)
+    p = O.params_from(weights)
+    G = O.Grid(nx)
+    ics = np.stack([O.initial_condition(G, 1000 + i) for i in range(n_ics)])
+    O.hybrid_run(p, G, ics[:8], 2)
+    t0 = time.perf_counter()
+    O.hybrid_run(p, G, ics, T)
+    return n_ics * T / (time.perf_counter() - t0)
+
+
 def pinned(n):
     """The first n CPUs this process may run on (taskset -c equivalent), as a set."""
     avail = sorted(os.sched_getaffinity(0))
@@ -621,11 +635,14 @@ def main():
                 alpha, beta = cpu_baseline(weights, nx, 30, args.cpu_sample_ics, len(cores))
             finally:
                 os.sched_setaffinity(0, keep)
+            beta_all = cpu_batched(weights, nx, 30, args.cpu_sample_ics, len(keep))
             cpu = {"value": round(alpha, 1), "unit": "IC-steps/s", "cores": len(cores), "kind": "port",
                    "sample": f"{args.cpu_sample_ics} ICs x 30 steps, one IC at a time (reference-faithful "
                              f"HybridSolver loop: torch-CPU FluxGNN + numpy FV/FFT), nx={nx}",
                    "pinned_cpus": f"{min(cores)}-{max(cores)} ({len(cores)} of host nproc {os.cpu_count()})",
-                   "batched_torch_cpu_value": round(beta, 1)}
+                   "batched_torch_cpu_value": round(beta, 1),
+                   "batched_torch_cpu_all_cores": {"value": round(beta_all, 1), "threads": len(keep),
+                                                   "note": "the batched form at the process's full CPU affinity set"}}
         line = {
             "metric": METRIC,
             "value": round(value, 1),

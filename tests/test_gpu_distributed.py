@@ -151,7 +151,7 @@ def test_cfg5_full_size_eight_ranks_equal_one_rank_bitwise(tmp_path):
 
 
 @pytest.mark.timeout(300)
-def test_rank_exiting_early_fails_the_job_within_timeout():
+def test_rank_exiting_early_fails_the_job_within_timeout(record):
     """8-GPU readiness: a 2-rank torchrun-style bench.py
     job (gloo on this box's one GPU) in which rank 1 vanishes before the group
     forms (HF_BENCH_EXIT_RANK=1, exit code 0, so the launcher keeps waiting on
@@ -166,6 +166,7 @@ def test_rank_exiting_early_fails_the_job_within_timeout():
     p = subprocess.run(cmd, env=_env(HF_BENCH_EXIT_RANK="1", HF_DIST_TIMEOUT_S="20"), capture_output=True,
                        text=True, timeout=240, cwd=ROOT)
     secs = time.perf_counter() - t0
+    record("rank_exit_early", "job_seconds", secs)
     assert p.returncode != 0, p.stdout[-2000:]
     assert secs < 200, secs
     assert "exiting early" in p.stderr

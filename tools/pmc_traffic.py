@@ -3,7 +3,7 @@ per-launch HBM traffic that bench.py reports as roofline.traffic.
 
     python tools/pmc_traffic.py TAG_A STEPS_A TAG_B STEPS_B ICS NX TRAJ(0|1) > profiles/pmc_traffic.json
 
-Two passes at different step counts (tools/gpu_pmc.sh TAG_A STEPS_A, then TAG_B
+Two passes at different step counts (tools/gpu_pmc_traffic.sh runs both: TAG_A STEPS_A, then TAG_B
 STEPS_B) separate a fixed part (state, weight stream, launch) from a per-step
 part (trajectory and metric writes), so bench.py can state the traffic of a
 launch of any --steps: traffic(K) = fixed_bytes + per_step_bytes * K.
