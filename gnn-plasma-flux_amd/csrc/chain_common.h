@@ -164,6 +164,61 @@ struct CellHalo {
   }
 };
 
+// Activation tape of the fused training forward (chain_train_fwd_kernel): the
+// core stores h[l] after every layer and the readout's P (+ b_e) / Q, in the
+// row-major layout the backward GEMMs read (train_chain.hip ChainTape:
+// h[l][row][feature], pq[row][P | Q]).  A lane holds features 16nt + 4g ..+3
+// of one cell per tile: one float4 store each.
+struct NoTape {
+  static constexpr bool kOn = false;
+};
+struct TrainTape {
+  static constexpr bool kOn = true;
+  float *h0;        // h[0]; h[l] = h0 + l * hstride
+  int64_t hstride;  // floats between the layers' arrays
+  float *pq;        // [N][2H]
+  int64_t row0;     // row of cell 0 of the wave's IC (b * nx)
+  bool live;        // idle waves (mirroring a real IC) store nothing
+  // ReLU'(h[l]) = h[l] > 0 of layers l < L as bits in the lanes' own layout
+  // (chain_train_bwd_kernel reads them back): word [l][b][mt][lane], bit 4nt + r
+  unsigned *mbits;
+  int64_t mstride;  // words per layer (B * MT * 64)
+  int64_t mrow;     // b * MT * 64
+  int layers;
+  template <int MT>
+  __device__ __forceinline__ void put_h(int l, const f4 (&h)[MT][kNT], int lane) const {
+    if (!live) return;
+    float *p = h0 + l * hstride + row0 * kH + 4 * (lane >> 4);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < kNT; ++nt)
+        *reinterpret_cast<f4 *>(p + (int64_t)cell_of<MT>(mt, lane & 15) * kH + 16 * nt) = h[mt][nt];
+    if (l < layers) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        unsigned m = 0;
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) m |= (h[mt][nt][r] > 0.f ? 1u : 0u) << (4 * nt + r);
+        mbits[l * mstride + mrow + mt * 64 + lane] = m;
+      }
+    }
+  }
+  template <int MT>
+  __device__ __forceinline__ void put_pq(int ot, const f4 (&P)[MT], const f4 (&Q)[MT], int lane) const {
+    if (!live) return;
+    float *p = pq + row0 * 2 * kH + 16 * ot + 4 * (lane >> 4);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float *r = p + (int64_t)cell_of<MT>(mt, lane & 15) * 2 * kH;
+      *reinterpret_cast<f4 *>(r) = P[mt];
+      *reinterpret_cast<f4 *>(r + kH) = Q[mt];
+    }
+  }
+};
+
 // v[i-1] + v[i+1] for a cell-split wave: row shifts, with the lane that falls
 // off the row taking the halo value.  The same single fp32 add as nb_sum.
 __device__ __forceinline__ float nb_sum_halo(float v, float hl, float hr) {
@@ -557,6 +612,144 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_flux_ker
         if (fe && g == 0) fe[b * 2 * nx + face] = f_fwd[mt];
         if (fe && g == 1) fe[b * 2 * nx + nx + face] = f_bwd[mt];
         if (ff && g == 2) ff[b * nx + face] = face_flux(f_fwd[mt], f_bwd[mt]);
+      }
+    }
+  }
+  R.drain();
+}
+
+// ---------------------------------------------------------------------------
+// Fused training forward (FluxGNN.forward under autograd on tagged chains of
+// nx = 16*MT cells, train_chain.hip launch_chain_forward_train): the flux
+// kernel's IC-per-wave pass plus the activation tape (TrainTape) the backward
+// GEMMs read.  W comes from pack_chain_f32_kernel (the parameters change every
+// optimizer step); b2 is read from the device (*b2p).
+template <class Core, int MT>
+__global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_fwd_kernel(
+    ChainW W, const float *__restrict__ b2p, const float *__restrict__ nf, int64_t items, float *__restrict__ fe,
+    float *h0, int64_t hstride, float *pq, unsigned *mbits) {
+  constexpr int nx = 16 * MT;
+  constexpr int kRingFloats = Core::kSlots * Core::kChunkFloats;
+  __shared__ f4 lds4[lds_floats<Core, false>() / 4];
+  float *lds = reinterpret_cast<float *>(lds4);
+  W.b2 = *b2p;
+  const Small S = stage_small(W, lds + kRingFloats);
+  auto R = make_ring<Core>(W, lds);
+  const int lane = R.lane, j = lane & 15, g = lane >> 4;
+  __syncthreads();
+  R.prime();
+  typename Core::Feed F;
+  Core::begin(R, F);
+  const int64_t groups = (items + Core::kNW - 1) / Core::kNW;
+  auto load_feat = [&](int64_t grp, float (&feat)[MT]) {
+    const int64_t item_raw = grp * Core::kNW + R.wave;
+    const int64_t b = item_raw < items ? item_raw : items - 1;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) feat[mt] = nf[(b * nx + cell_of<MT>(mt, j)) * kIn + g];
+  };
+  float pre[MT];
+  if (blockIdx.x < groups) load_feat(blockIdx.x, pre);
+  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    float feat[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) feat[mt] = pre[mt];
+    if (grp + gridDim.x < groups) load_feat(grp + gridDim.x, pre);
+    const int64_t item_raw = grp * Core::kNW + R.wave;
+    const bool live = item_raw < items;
+    const int64_t b = live ? item_raw : items - 1;
+    const TrainTape T{h0, hstride, pq, b * nx, live, mbits, items * MT * 64, b * MT * 64, W.layers};
+    float f_fwd[MT], f_bwd[MT];
+    Core::template gnn_tape<MT>(W, S, R, F, feat, f_fwd, f_bwd, T);
+    if (live) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int face = cell_of<MT>(mt, j);
+        if (g == 0) fe[b * 2 * nx + face] = f_fwd[mt];
+        if (g == 1) fe[b * 2 * nx + nx + face] = f_bwd[mt];
+      }
+    }
+  }
+  R.drain();
+}
+
+// Fused data gradient of the update layers (train_chain.hip
+// launch_chain_backward): from g[L] = ReLU'(h[L]) * dh[L] (the readout's
+// gradient, global) to g[l] = ReLU'(h[l]) * (W_a^T g[l+1] + W_b^T agg g[l+1])
+// for l = L-1 .. 0 (the aggregation is self-adjoint on the periodic chain),
+// one IC per wave through the flux kernel's layer pass: the same [x ; agg x]
+// B operand from registers, the transposed weights streamed through the ring
+// (pack_chain_bwd_f32_kernel), the ReLU' bits the forward stored
+// (TrainTape::mbits).  g[l] = g0 + l * gstride, [N][H] each.
+template <class Core, int MT>
+__global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bwd_kernel(
+    ChainW W, int64_t items, float *g0, int64_t gstride, const unsigned *__restrict__ mbits) {
+  constexpr int nx = 16 * MT;
+  __shared__ f4 lds4[Core::kSlots * Core::kChunkFloats / 4];
+  float *lds = reinterpret_cast<float *>(lds4);
+  const int L = W.layers;
+  auto R = make_ring<Core>(W, lds);
+  R.chunks = 16 * L;  // update layers only
+  R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0, R.chunks * Core::kChunkFloats * 4,
+                                             0x00020000);
+  const int lane = R.lane, j = lane & 15, g4 = 4 * (lane >> 4);
+  __syncthreads();
+  R.prime();
+  typename Core::Feed F;
+  Core::begin(R, F);
+  const int64_t groups = (items + Core::kNW - 1) / Core::kNW, mstride = items * MT * 64;
+  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    const int64_t item_raw = grp * Core::kNW + R.wave;
+    const bool live = item_raw < items;
+    const int64_t b = live ? item_raw : items - 1;
+    f4 g[MT][kNT];
+    {
+      const float *src = g0 + L * gstride + b * nx * kH + g4;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) g[mt][nt] = ldf4(src + (int64_t)cell_of<MT>(mt, j) * kH + 16 * nt);
+    }
+    for (int l = L - 1; l >= 0; --l) {
+      unsigned mb[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) mb[mt] = mbits[l * mstride + b * MT * 64 + mt * 64 + lane];
+      f4 acc[MT][kNT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+      NoHalo X;
+      float bop[MT];
+      Core::template b_operand<MT, 0>(g, bop, X);
+      Core::template layer_chunk<MT, 0>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 4>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 8>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 12>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 16>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 20>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 24>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 28>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 32>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 36>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 40>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 44>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 48>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 52>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 56>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 60>(R, F, g, bop, acc, X);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g[mt][nt][r] = (mb[mt] >> (4 * nt + r)) & 1u ? acc[mt][nt][r] : 0.f;
+      if (live) {
+        float *dst = g0 + l * gstride + b * nx * kH + g4;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < kNT; ++nt)
+            *reinterpret_cast<f4 *>(dst + (int64_t)cell_of<MT>(mt, j) * kH + 16 * nt) = g[mt][nt];
       }
     }
   }

@@ -238,24 +238,33 @@ struct CoreF32T {
   static __device__ __forceinline__ void gnn(const ChainW &W, const Small &S, R_t &R, Feed &F, float * /*park*/,
                                              const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT]) {
     NoHalo X;
-    gnn_impl<MT, NoHalo>(W, S, R, F, feat, ffwd, fbwd, X);
+    gnn_impl<MT, NoHalo>(W, S, R, F, feat, ffwd, fbwd, X, NoTape{});
+  }
+  // The same pass storing the activation tape (chain_train_fwd_kernel).
+  template <int MT>
+  static __device__ __forceinline__ void gnn_tape(const ChainW &W, const Small &S, R_t &R, Feed &F,
+                                                  const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT],
+                                                  const TrainTape &T) {
+    NoHalo X;
+    gnn_impl<MT, NoHalo>(W, S, R, F, feat, ffwd, fbwd, X, T);
   }
   // A cell-split wave: 16 consecutive cells of an IC spread over several
   // waves (chain_rollout_cells_kernel below), boundary columns exchanged through X.
   static __device__ __forceinline__ void gnn_cells(const ChainW &W, const Small &S, R_t &R, Feed &F,
                                                    const float (&feat)[1], float (&ffwd)[1], float (&fbwd)[1],
                                                    CellHalo &X) {
-    gnn_impl<1, CellHalo>(W, S, R, F, feat, ffwd, fbwd, X);
+    gnn_impl<1, CellHalo>(W, S, R, F, feat, ffwd, fbwd, X, NoTape{});
   }
 
-  template <int MT, class H>
+  template <int MT, class H, class TP>
   static __device__ __forceinline__ void gnn_impl(const ChainW &W, const Small &S, R_t &R, Feed &F,
                                                   const float (&feat)[MT], float (&ffwd)[MT], float (&fbwd)[MT],
-                                                  H &X) {
+                                                  H &X, const TP &T) {
     const int lane = R.lane;
     const int g4 = 4 * (lane >> 4);
     f4 h[MT][kNT];
     input_layer<MT>(S, lane, feat, h);
+    if constexpr (TP::kOn) T.template put_h<MT>(0, h, lane);
     // cell-split waves: the boundary columns are published here and read
     // after the ring barrier that ends the next layer's first chunk
     // (layer_step<4>), long before the first neighbour-sum k-step (32)
@@ -294,6 +303,7 @@ struct CoreF32T {
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) h[mt][nt] = relu4(acc[mt][nt]);
+      if constexpr (TP::kOn) T.template put_h<MT>(l + 1, h, lane);
       if constexpr (H::kOn) {
         if (l + 1 < W.layers) X.publish(h);
       }
@@ -327,6 +337,7 @@ struct CoreF32T {
         }
         readout_chunk<MT, 0>(R, F, h, P, Q);
         readout_chunk<MT, 1>(R, F, h, P, Q);
+        if constexpr (TP::kOn) T.template put_pq<MT>(ot, P, Q, lane);
         readout_epilogue<MT, true>(P, Q, be, ldf4(S.w2 + 16 * ot + g4), pf, pb);
       }
       float ff[MT], fb[MT];
@@ -401,6 +412,150 @@ hipError_t launch_chain_flux_f32(const ChainW &w, const float *nf, const float *
     }
   }
   return chain::launch_flux_core<CoreF32>(w, nf, state, ld_state, x, B, nx, fe, ff, s);
+}
+
+// ---------------------------------------------------------------------------
+// Fused training forward (train_chain.hip launch_chain_forward_train at
+// nx in {16, 32, 48, 64}, FluxGNN(4, 128, L <= 8)).
+namespace {
+__device__ __forceinline__ int kperm_dev(int s, int lane) { return 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3); }
+
+// The f32 chain stream and small arrays of capi.cpp pack_chain (kPrecF32),
+// built on the device from state-dict-ordered parameters (GraphW view): the
+// optimizer changes them every step, so the host pack is no option.  One
+// thread per packed float: the stream's nstream floats, then the small arrays
+// (win [2][64][4], b_in, b_l[L], b_e, w2).
+__global__ void pack_chain_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream, float *__restrict__ small) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int L = w.layers;
+  if (idx < nstream) {
+    const int c = (int)(idx >> 11), rem = (int)(idx & 2047), j = rem >> 8, lane = (rem >> 2) & 63, cc = rem & 3;
+    float v;
+    if (c < 16 * L) {  // update layer l, chunk gi: k-step s, output tile nt
+      const int l = c >> 4, s = 4 * (c & 15) + (j >> 1), nt = 4 * (j & 1) + cc;
+      const int k = (s < kKS ? 0 : kH) + kperm_dev(s % kKS, lane);
+      v = w.w_l[l * w.lsw + (int64_t)(16 * nt + (lane & 15)) * 2 * kH + k];
+      if (s >= kKS) v *= 0.5f;  // the mean's 1/deg folded into W_b (exact)
+    } else {  // readout tile ot, half hh: P (cc even) / Q (odd) of k-step s
+      const int r = c - 16 * L, ot = r >> 1, s = 16 * (r & 1) + 2 * j + (cc >> 1);
+      v = w.w_e[(int64_t)(16 * ot + (lane & 15)) * 2 * kH + (cc & 1) * kH + kperm_dev(s, lane)];
+    }
+    stream[idx] = v;
+    return;
+  }
+  const int i = (int)(idx - nstream);
+  if (i >= 512 + kH * (3 + L)) return;
+  float v;
+  if (i < 512) {
+    const int lane = (i >> 2) & 63, nt = 4 * (i >> 8) + (i & 3);
+    v = w.w_in[(16 * nt + (lane & 15)) * kIn + (lane >> 4)];
+  } else if (i < 512 + kH) {
+    v = w.b_in[i - 512];
+  } else if (i < 512 + kH * (1 + L)) {
+    const int o = i - 512 - kH;
+    v = w.b_l[(o / kH) * w.lsb + o % kH];
+  } else if (i < 512 + kH * (2 + L)) {
+    v = w.b_e[i - 512 - kH * (1 + L)];
+  } else {
+    v = w.w_2[i - 512 - kH * (2 + L)];
+  }
+  small[i] = v;
+}
+
+// The update layers' transposed weights for chain_train_bwd_kernel, in the
+// f32 stream format, layers L-1 .. 0: A(n, k) = W_l[k][n] (k < H: W_a^T) or
+// W_l[k - H][H + n] / 2 (W_b^T with the mean's 1/deg).
+__global__ void pack_chain_bwd_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nstream) return;
+  const int c = (int)(idx >> 11), rem = (int)(idx & 2047), j = rem >> 8, lane = (rem >> 2) & 63, cc = rem & 3;
+  const int l = w.layers - 1 - (c >> 4), s = 4 * (c & 15) + (j >> 1), n = 16 * (4 * (j & 1) + cc) + (lane & 15);
+  const int k = kperm_dev(s % kKS, lane);
+  const float *W = w.w_l + l * w.lsw;
+  stream[idx] = s < kKS ? W[(int64_t)k * 2 * kH + n] : 0.5f * W[(int64_t)k * 2 * kH + kH + n];
+}
+
+template <int MT>
+int64_t train_blocks(int64_t B) {
+  const int64_t groups = (B + CoreF32::kNW - 1) / CoreF32::kNW;
+  const int64_t res = (int64_t)resident_groups() * CoreF32::kWGPerCU;
+  return groups < res ? groups : res;
+}
+template <int MT>
+hipError_t train_fwd_launch(const ChainW &cw, const float *b2p, const float *nf, int64_t B, float *fe, float *h0,
+                            int64_t hstride, float *pq, unsigned *mbits, hipStream_t s) {
+  hipLaunchKernelGGL((chain_train_fwd_kernel<CoreF32, MT>), dim3((unsigned)train_blocks<MT>(B)),
+                     dim3(64 * CoreF32::kNW), 0, s, cw, b2p, nf, B, fe, h0, hstride, pq, mbits);
+  return hipGetLastError();
+}
+template <int MT>
+hipError_t train_bwd_launch(const ChainW &cw, int64_t B, float *g0, int64_t gstride, const unsigned *mbits,
+                            hipStream_t s) {
+  hipLaunchKernelGGL((chain_train_bwd_kernel<CoreF32, MT>), dim3((unsigned)train_blocks<MT>(B)),
+                     dim3(64 * CoreF32::kNW), 0, s, cw, B, g0, gstride, mbits);
+  return hipGetLastError();
+}
+}  // namespace
+
+int64_t chain_train_pack_bytes(int layers) {
+  return (int64_t)chain_chunks(layers, kPrecF32) * chain_chunk_bytes(kPrecF32) +
+         (int64_t)sizeof(float) * (512 + kH * (3 + layers));
+}
+int64_t chain_train_mask_bytes(int layers, int64_t N) { return (int64_t)layers * N * 16; }
+int64_t chain_train_bwd_pack_bytes(int layers) { return (int64_t)16 * layers * chain_chunk_bytes(kPrecF32); }
+
+hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, float *g0, int64_t gstride,
+                                        const unsigned *mbits, void *pack, hipStream_t s) {
+  const int L = w.layers;
+  if (B <= 0 || L == 0) return hipSuccess;
+  float *stream = static_cast<float *>(pack);
+  const int64_t nstream = (int64_t)16 * L * 2048;
+  hipLaunchKernelGGL(pack_chain_bwd_f32_kernel, dim3((unsigned)(nstream / 256)), dim3(256), 0, s, w, stream, nstream);
+  ChainW cw{};
+  cw.stream = stream;
+  cw.layers = L;
+  cw.prec = kPrecF32;
+  switch (nx) {
+    case 16: return train_bwd_launch<1>(cw, B, g0, gstride, mbits, s);
+    case 32: return train_bwd_launch<2>(cw, B, g0, gstride, mbits, s);
+    case 48: return train_bwd_launch<3>(cw, B, g0, gstride, mbits, s);
+    case 64: return train_bwd_launch<4>(cw, B, g0, gstride, mbits, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+bool chain_train_fused_ok(const GraphW &w, int nx) {
+  return w.in_dim == kIn && w.hidden == kH && w.layers >= 0 && w.layers <= kMaxChainLayers &&
+         (nx == 16 || nx == 32 || nx == 48 || nx == 64);
+}
+
+hipError_t launch_chain_train_fwd_fused(const GraphW &w, const float *nf, int64_t B, int nx, float *fe, float *h0,
+                                        int64_t hstride, float *pq, unsigned *mbits, void *pack, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  const int L = w.layers;
+  float *stream = static_cast<float *>(pack);
+  const int64_t nstream = (int64_t)chain_chunks(L, kPrecF32) * chain_chunk_bytes(kPrecF32) / 4;
+  float *small = stream + nstream;
+  const int64_t total = nstream + 512 + kH * (3 + L);
+  hipLaunchKernelGGL(pack_chain_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, w, stream, nstream,
+                     small);
+  ChainW cw{};
+  cw.stream = stream;
+  cw.win = small;
+  cw.bin = small + 512;
+  cw.bl = small + 512 + kH;
+  cw.be = small + 512 + kH * (1 + L);
+  cw.w2 = small + 512 + kH * (2 + L);
+  cw.b2 = 0.f;  // read from w.b_2 on the device
+  cw.layers = L;
+  cw.prec = kPrecF32;
+  switch (nx) {
+    case 16: return train_fwd_launch<1>(cw, w.b_2, nf, B, fe, h0, hstride, pq, mbits, s);
+    case 32: return train_fwd_launch<2>(cw, w.b_2, nf, B, fe, h0, hstride, pq, mbits, s);
+    case 48: return train_fwd_launch<3>(cw, w.b_2, nf, B, fe, h0, hstride, pq, mbits, s);
+    case 64: return train_fwd_launch<4>(cw, w.b_2, nf, B, fe, h0, hstride, pq, mbits, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_chain_rollout_f32(const ChainW &w, const float *state0, float *state_final, const float *x,

@@ -415,9 +415,29 @@ bool chain_train_ok(const GraphW &w, int chain_nx, int64_t N) {
          w.in_dim <= 8 && N > 0 && N * 2 * H + 2 * H < (int64_t(1) << 31);
 }
 
+#ifndef HF_TRAIN_FUSED
+#define HF_TRAIN_FUSED 1  // 0: the GEMM forward at every nx (A/B builds)
+#endif
+
+// h[0..L] | pq | (FluxGNN(4, 128, L <= 8): the fused forward's packed weights
+// and ReLU' bits; the chain length is unknown here, so the space is kept for
+// every chain)
+bool fused_width(const GraphW &w) { return HF_TRAIN_FUSED && chain_train_fused_ok(w, 64); }
 int64_t chain_tape_bytes(const GraphW &w, int64_t N) {
-  return (int64_t)((w.layers + 1) * al256(sizeof(float) * N * w.hidden) + al256(sizeof(float) * N * 2 * w.hidden));
+  return (int64_t)((w.layers + 1) * al256(sizeof(float) * N * w.hidden) + al256(sizeof(float) * N * 2 * w.hidden) +
+                   (fused_width(w) ? al256((size_t)chain_train_pack_bytes(w.layers)) +
+                                         al256((size_t)chain_train_mask_bytes(w.layers, N))
+                                   : 0));
 }
+struct FusedTape {
+  void *pack;
+  unsigned *mbits;
+};
+FusedTape fused_tape(const GraphW &w, int64_t N, const ChainTape &t) {
+  char *p = reinterpret_cast<char *>(t.pq) + al256(sizeof(float) * N * 2 * w.hidden);
+  return FusedTape{p, reinterpret_cast<unsigned *>(p + al256((size_t)chain_train_pack_bytes(w.layers)))};
+}
+bool fused_chain(const GraphW &w, int nx, int64_t N) { return HF_TRAIN_FUSED && chain_train_fused_ok(w, nx) && N % nx == 0; }
 
 int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   const int64_t H = w.hidden;
@@ -428,6 +448,8 @@ int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   b += al256(sizeof(float) * S * 2 * H);        // bias partials
   b += al256(sizeof(float) * kEdgeBlocks * (H + 1));
   b += al256(sizeof(float) * kInputSplits * H * (w.in_dim + 1));
+  if (fused_width(w))  // fused backward: g[0..L] side by side + the transposed weights
+    b += (w.layers + 1) * al256(sizeof(float) * N * H) + al256((size_t)chain_train_bwd_pack_bytes(w.layers));
   return (int64_t)b;
 }
 
@@ -435,6 +457,11 @@ hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t 
                                       hipStream_t s) {
   const int H = w.hidden, L = w.layers, hsh = __builtin_ctz(H);
   const ChainTape t = carve_chain_tape(w, N, tape);
+  if (fused_chain(w, nx, N)) {  // (N = B * nx on a tagged chain)
+    const FusedTape f = fused_tape(w, N, t);
+    return launch_chain_train_fwd_fused(w, nf, N / nx, nx, flux, t.h[0], (int64_t)(al256(sizeof(float) * N * H) / 4),
+                                        t.pq, f.mbits, f.pack, s);
+  }
 #define HF_IN_FWD(FF)                                                                                      \
   hipLaunchKernelGGL(input_forward_kernel<FF>, dim3((unsigned)((N * (H / 4) + 255) / 256)), dim3(256), 0, s, nf, \
                      w.w_in, w.b_in, H, N, t.h[0])
@@ -477,6 +504,11 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   float *bpart = take(sizeof(float) * S * 2 * H);
   float *epart = take(sizeof(float) * kEdgeBlocks * (H + 1));
   float *ipart = take(sizeof(float) * kInputSplits * H * (F + 1));
+  // fused (FluxGNN(4, 128) on nx <= 64): g[l] = G + l * gstride for every layer
+  const bool fused = fused_chain(w, nx, N);
+  const int64_t gstride = (int64_t)(al256(sizeof(float) * N * H) / 4);
+  float *G = fused ? take((L + 1) * al256(sizeof(float) * N * H)) : nullptr;
+  void *bpack = fused ? static_cast<void *>(take((size_t)chain_train_bwd_pack_bytes(L))) : nullptr;
   hipError_t e;
   auto reduce = [&](int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff, int64_t nbias,
                     float *bias) {
@@ -503,12 +535,16 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   {
     const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
     const VPlain B{w.w_e, 2LL * H, 2LL * H, hsh, H, H};  // B(r = c, j = k) = [W_a ; W_b][c][k]
-    if ((e = tgemm<VPlain, false, VPlain, true>(A, B, EpiMask{dl[cur], H, t.h[L], H}, N, H, 2 * H, 1, s))) return e;
+    float *gL = fused ? G + L * gstride : dl[cur];
+    if ((e = tgemm<VPlain, false, VPlain, true>(A, B, EpiMask{gL, H, t.h[L], H}, N, H, 2 * H, 1, s))) return e;
   }
+  // fused: every layer's data gradient in one IC-per-wave pass (chain_train_bwd_kernel)
+  if (fused && (e = launch_chain_train_bwd_fused(w, N / nx, nx, G, gstride, fused_tape(w, N, t).mbits, bpack, s)))
+    return e;
   for (int l = L - 1; l >= 0; --l) {  // update layers, last to first                      (:53-60)
     // dW_l[o][k] = sum_m delta[m][o] [h[l] ; agg h[l]][m][k], db_l = column sums of delta
     {
-      const VPlain A{dl[cur], H, N, kNoSplit, 0, H};
+      const VPlain A{fused ? G + (l + 1) * gstride : dl[cur], H, N, kNoSplit, 0, H};
       const VStencil B{t.h[l], N, H, nx};
       if ((e = tgemm<VPlain, true, VStencil, true, EpiPart, true>(A, B, EpiPart{part, H, 2LL * H}, H, 2 * H, N,
                                                                   kWgradSplits, s, bpart)))
@@ -519,7 +555,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
     }
     // dh[l] = W_a^T delta + W_b^T agg(delta) (the aggregation's adjoint is itself on the
     // chain), masked by ReLU'(h[l]): B(r, j) = W_l[r % H][(r / H) H + j]
-    {
+    if (!fused) {
       const VStencil A{dl[cur], N, H, nx};
       const VPlain B{w.w_l + l * w.lsw, 2LL * H, 2LL * H, hsh, H, H};
       if ((e = tgemm<VStencil, false, VPlain, true>(A, B, EpiMask{dl[cur ^ 1], H, t.h[l], H}, N, H, 2 * H, 1, s)))
@@ -528,7 +564,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
     }
   }
   // input MLP                                                                        (:49)
-  const float *d0 = dl[cur];
+  const float *d0 = fused ? G : dl[cur];
   const int64_t rows = (N + kInputSplits - 1) / kInputSplits;
   const int nsp = (int)((N + rows - 1) / rows);
   float *ipb = ipart + (int64_t)kInputSplits * H * F;

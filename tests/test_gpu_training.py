@@ -104,7 +104,9 @@ def test_backward_deterministic_and_chain_batch_vs_oracle(hf):
                                                           (2, 4, 1, 64, False), (7, 6, 0, 32, False),
                                                           (100, 3, 3, 128, False), (64, 300, 4, 128, True),
                                                           (64, 4, 3, 16, False), (16, 3, 2, 8, False),
-                                                          (8, 2, 1, 4, False), (64, 3, 2, 256, False)])
+                                                          (8, 2, 1, 4, False), (64, 3, 2, 256, False),
+                                                          (16, 5, 2, 128, False), (32, 9, 0, 128, False),
+                                                          (48, 7, 8, 128, False)])
 def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden, kinkfree):
     """The chain training path (train_chain.hip: stencil-loader GEMMs, P/Q
     readout, split-K weight gradients) on tagged chains of any nx, layer count
@@ -120,7 +122,10 @@ def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden, kinkfree):
     products below 3), so its ReLU derivatives are unambiguous and the gate
     stays the gradient gate; the small cases exercise the masks.  Widths 4, 8
     and 16 are below the GEMM's 32-wide reduction chunk: tagged chains of those
-    widths take the generic CSR path and must give the same answers."""
+    widths take the generic CSR path and must give the same answers.
+    FluxGNN(4, 128, L <= 8) on nx in {16, 32, 48, 64} runs the fused forward
+    (chain_train_fwd_kernel: the flux kernel's pass storing the tape); nx = 1
+    and 100 at width 128 run the GEMM forward."""
     rng = np.random.default_rng(nx * 100 + layers)
     if kinkfree:
         u = lambda a, shape: rng.uniform(-a, a, shape)  # noqa: E731
@@ -156,6 +161,26 @@ def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden, kinkfree):
     grads_close(nf.grad, nf_o.grad.numpy())
     for k, q in m.named_parameters():
         grads_close(q.grad, p[k].grad.numpy())
+
+
+@pytest.mark.parametrize("nx,B", [(64, 1), (64, 9), (64, 2000), (16, 13), (48, 6)])
+def test_fused_training_forward_equals_inference(hf, nx, B):
+    """FluxGNN(4, 128, 4) under autograd on a tagged chain of nx in {16, 32, 48,
+    64} runs chain_train_fwd_kernel (device-packed weights, tape stores) —
+    the inference flux kernel's own pass, so its flux equals the no-grad
+    forward (chain_flux_kernel) bit for bit; B = 2000 is the training bench's
+    batch (several IC groups per workgroup)."""
+    w = golden("weights_W1_r2.npz")
+    m = load(hf, {k: w[k] for k in w.files}, (4, 128, 4))
+    G = O.Grid(nx, dt=5e-3)
+    states = np.stack([O.initial_condition(G, s) for s in range(7, 7 + min(B, 64))])
+    states = np.concatenate([states] * ((B + len(states) - 1) // len(states)))[:B]
+    nf, ei = hf.build_chain_graph_batch(states, G.x, DEV)
+    with torch.no_grad():
+        want = m(nf, ei).cpu().numpy()
+    got = m(nf, ei)
+    assert got.requires_grad
+    assert np.array_equal(got.detach().cpu().numpy(), want)
 
 
 def test_backward_edge_cases(hf):
