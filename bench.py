@@ -228,8 +228,10 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
     the cfg_name ablation loss, loss.backward(), Adam) on `batch` samples of
     the reference dataset recipe (DATASET_CONFIG: 50 ICs x 40 steps, nx = 64,
     generated on the GPU by hybridflux.datagen), FluxGNN(4,128,4) random-init
-    (torch.manual_seed(0)).  Eager, and replaying the captured step
-    (hybridflux.training.GraphedStep); each warmed for warm_s, then `steps`
+    (torch.manual_seed(0)).  Eager with torch's default (multi-tensor) Adam,
+    eager with its single-kernel fused=True Adam (the same update), and
+    replaying the captured step (hybridflux.training.GraphedStep, fused
+    capturable Adam); each warmed for warm_s, then `steps`
     steps timed with HIP events + the wall clock.  FLOPs per sample: FluxGNN
     forward + backward (tools/bench_train.py flop_per_sample); the loss terms,
     FV updates and Adam are inside the timed step but not counted."""
@@ -248,11 +250,14 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
            "batch": batch, "steps": steps, "flop_per_sample": fps,
            "dataset": "DATASET_CONFIG recipe: 50 ICs x 40 steps, nx=64 (GPU classical rollout)"}
     best = None
-    for mode in ("eager", "graphed"):
+    for mode in ("eager", "eager_fused_adam", "graphed"):
         graphed = mode == "graphed"
         torch.manual_seed(0)
         m = FluxGNN(4, 128, 4).to(dev)
-        opt = torch.optim.Adam(m.parameters(), lr=1e-3, capturable=graphed)
+        # graphed: the fused Adam kernel in its capturable form (the multi-tensor
+        # capturable Adam costs ~60 us more per step inside the graph)
+        opt = (torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=graphed) if mode != "eager" else
+               torch.optim.Adam(m.parameters(), lr=1e-3))
         gs = GraphedStep(m, opt, data, batch, x_dev, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
         gen = torch.Generator().manual_seed(1)
         order = torch.randint(0, len(data), (steps * batch,), generator=gen).to(dev)

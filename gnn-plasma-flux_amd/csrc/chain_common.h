@@ -165,20 +165,49 @@ struct CellHalo {
 };
 
 // Activation tape of the fused training forward (chain_train_fwd_kernel): the
-// core stores h[l] after every layer and the readout's P (+ b_e) / Q, in the
-// row-major layout the backward GEMMs read (train_chain.hip ChainTape:
-// h[l][row][feature], pq[row][P | Q]).  A lane holds features 16nt + 4g ..+3
-// of one cell per tile: one float4 store each.
+// core stores h[l] and the readout's P (+ b_e) / Q in the row-major layout the
+// backward GEMMs read (train_chain.hip ChainTape: h[l][row][feature],
+// pq[row][P | Q]).  A lane holds features 16nt + 4g ..+3 of one cell per tile:
+// one float4 store each.  h[l] is stored while it is the B operand of the
+// next pass, one tile every other k-step (put_tile), not as a burst after the
+// ReLU: every wave reaches the end of a layer at about the same time, and 32
+// stores per lane at once stall the matrix pipe on the memory queue.
 struct NoTape {
   static constexpr bool kOn = false;
 };
-struct TrainTape {
+// Row-major [N][kH] arrays, one per layer (h[l], or the backward's g[l]),
+// written tile by tile from the lane layout.
+struct TileStore {
+  float *base;     // array 0; array l = base + l * stride
+  int64_t stride;  // floats between the arrays
+  int64_t row0;    // row of cell 0 of the wave's IC (b * nx)
+  bool live;       // idle waves (mirroring a real IC) store nothing
+  template <int MT>
+  __device__ __forceinline__ void put(int l, const f4 &v, int mt, int nt, int lane) const {
+    if (!live) return;
+    // one lane base per array; tile (mt, nt) at a constant offset (cell_of(mt, j) = MT j + mt),
+    // so the stores carry immediate offsets instead of 32 live addresses
+    float *p = base + l * stride + (row0 + MT * (lane & 15)) * kH + 4 * (lane >> 4);
+    *reinterpret_cast<f4 *>(p + mt * kH + 16 * nt) = v;
+  }
+  template <int MT, int IDX>
+  __device__ __forceinline__ void put_tile(int l, const f4 (&h)[MT][kNT], int lane) const {
+    put<MT>(l, h[IDX / kNT][IDX % kNT], IDX / kNT, IDX % kNT, lane);
+  }
+  template <int MT, int NT>
+  __device__ __forceinline__ void put_col(int l, const f4 (&h)[MT][kNT], int lane) const {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) put<MT>(l, h[mt][NT], mt, NT, lane);
+  }
+  template <int MT>
+  __device__ __forceinline__ void put_all(int l, const f4 (&h)[MT][kNT], int lane) const {
+    put_col<MT, 0>(l, h, lane), put_col<MT, 1>(l, h, lane), put_col<MT, 2>(l, h, lane), put_col<MT, 3>(l, h, lane);
+    put_col<MT, 4>(l, h, lane), put_col<MT, 5>(l, h, lane), put_col<MT, 6>(l, h, lane), put_col<MT, 7>(l, h, lane);
+  }
+};
+struct TrainTape : TileStore {
   static constexpr bool kOn = true;
-  float *h0;        // h[0]; h[l] = h0 + l * hstride
-  int64_t hstride;  // floats between the layers' arrays
-  float *pq;        // [N][2H]
-  int64_t row0;     // row of cell 0 of the wave's IC (b * nx)
-  bool live;        // idle waves (mirroring a real IC) store nothing
+  float *pq;  // [N][2H]
   // ReLU'(h[l]) = h[l] > 0 of layers l < L as bits in the lanes' own layout
   // (chain_train_bwd_kernel reads them back): word [l][b][mt][lane], bit 4nt + r
   unsigned *mbits;
@@ -186,24 +215,16 @@ struct TrainTape {
   int64_t mrow;     // b * MT * 64
   int layers;
   template <int MT>
-  __device__ __forceinline__ void put_h(int l, const f4 (&h)[MT][kNT], int lane) const {
-    if (!live) return;
-    float *p = h0 + l * hstride + row0 * kH + 4 * (lane >> 4);
+  __device__ __forceinline__ void put_mask(int l, const f4 (&h)[MT][kNT], int lane) const {
+    if (!live || l >= layers) return;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int mt = 0; mt < MT; ++mt) {
+      unsigned m = 0;
 #pragma unroll
       for (int nt = 0; nt < kNT; ++nt)
-        *reinterpret_cast<f4 *>(p + (int64_t)cell_of<MT>(mt, lane & 15) * kH + 16 * nt) = h[mt][nt];
-    if (l < layers) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        unsigned m = 0;
-#pragma unroll
-        for (int nt = 0; nt < kNT; ++nt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) m |= (h[mt][nt][r] > 0.f ? 1u : 0u) << (4 * nt + r);
-        mbits[l * mstride + mrow + mt * 64 + lane] = m;
-      }
+        for (int r = 0; r < 4; ++r) m |= (h[mt][nt][r] > 0.f ? 1u : 0u) << (4 * nt + r);
+      mbits[l * mstride + mrow + mt * 64 + lane] = m;
     }
   }
   template <int MT>
@@ -217,6 +238,11 @@ struct TrainTape {
       *reinterpret_cast<f4 *>(r + kH) = Q[mt];
     }
   }
+};
+// The backward pass's tile stores of g[l+1] while it feeds layer l (g[L] is
+// the pass's input, already in memory: not stored again).
+struct GradTape : TileStore {
+  static constexpr bool kOn = true;
 };
 
 // v[i-1] + v[i+1] for a cell-split wave: row shifts, with the lane that falls
@@ -657,7 +683,9 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_fw
     const int64_t item_raw = grp * Core::kNW + R.wave;
     const bool live = item_raw < items;
     const int64_t b = live ? item_raw : items - 1;
-    const TrainTape T{h0, hstride, pq, b * nx, live, mbits, items * MT * 64, b * MT * 64, W.layers};
+    TrainTape T;
+    T.base = h0, T.stride = hstride, T.row0 = b * nx, T.live = live;
+    T.pq = pq, T.mbits = mbits, T.mstride = items * MT * 64, T.mrow = b * MT * 64, T.layers = W.layers;
     float f_fwd[MT], f_bwd[MT];
     Core::template gnn_tape<MT>(W, S, R, F, feat, f_fwd, f_bwd, T);
     if (live) {
@@ -701,6 +729,8 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bw
     const int64_t item_raw = grp * Core::kNW + R.wave;
     const bool live = item_raw < items;
     const int64_t b = live ? item_raw : items - 1;
+    GradTape GT;
+    GT.base = g0, GT.stride = gstride, GT.row0 = b * nx, GT.live = live;
     f4 g[MT][kNT];
     {
       const float *src = g0 + L * gstride + b * nx * kH + g4;
@@ -719,39 +749,33 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bw
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
       NoHalo X;
+      const int tl = l + 1 < L ? l + 1 : -1;  // g[l+1] (the B operand) to memory, spread over the pass
       float bop[MT];
       Core::template b_operand<MT, 0>(g, bop, X);
-      Core::template layer_chunk<MT, 0>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 4>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 8>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 12>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 16>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 20>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 24>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 28>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 32>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 36>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 40>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 44>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 48>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 52>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 56>(R, F, g, bop, acc, X);
-      Core::template layer_chunk<MT, 60>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 0>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 4>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 8>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 12>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 16>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 20>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 24>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 28>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 32>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 36>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 40>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 44>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 48>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 52>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 56>(R, F, g, bop, acc, X, GT, tl);
+      Core::template layer_chunk<MT, 60>(R, F, g, bop, acc, X, GT, tl);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) g[mt][nt][r] = (mb[mt] >> (4 * nt + r)) & 1u ? acc[mt][nt][r] : 0.f;
-      if (live) {
-        float *dst = g0 + l * gstride + b * nx * kH + g4;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < kNT; ++nt)
-            *reinterpret_cast<f4 *>(dst + (int64_t)cell_of<MT>(mt, j) * kH + 16 * nt) = g[mt][nt];
-      }
     }
+    GT.template put_all<MT>(0, g, lane);  // g[0]: no pass follows
   }
   R.drain();
 }

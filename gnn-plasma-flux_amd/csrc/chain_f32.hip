@@ -108,9 +108,11 @@ struct CoreF32T {
   // B operand on entry and the next k-step's on exit: the next operand's lane
   // shifts are interleaved with this k-step's MFMAs instead of stalling the
   // matrix pipe between m-tiles.
-  template <int MT, int KS, class H>
+  // TP (a TileStore): tile KS/2 of h goes to array tl (tl >= 0) after k-step KS
+  // (odd KS), so a pass stores its B operand spread over its first 2*MT*kNT k-steps.
+  template <int MT, int KS, class H, class TP = NoTape>
   static __device__ __forceinline__ void layer_step(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
-                                                    f4 (&acc)[MT][kNT], H &X) {
+                                                    f4 (&acc)[MT][kNT], H &X, const TP &T = TP{}, int tl = -1) {
     f4 a[2];
     take<KS % kUPC>(R, F, a);
     if constexpr (H::kOn && KS == kUPC) X.read();  // the ring barrier of take<kUPC-1> follows every publish
@@ -136,14 +138,17 @@ struct CoreF32T {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) b[mt] = bn[mt];
     }
+    if constexpr (TP::kOn && KS % 2 == 1 && KS / 2 < MT * kNT) {
+      if (tl >= 0) T.template put_tile<MT, KS / 2>(tl, h, R.lane);
+    }
   }
-  template <int MT, int KS0, class H>
+  template <int MT, int KS0, class H, class TP = NoTape>
   static __device__ __forceinline__ void layer_chunk(R_t &R, Feed &F, const f4 (&h)[MT][kNT], float (&b)[MT],
-                                                     f4 (&acc)[MT][kNT], H &X) {
-    layer_step<MT, KS0 + 0>(R, F, h, b, acc, X);
-    layer_step<MT, KS0 + 1>(R, F, h, b, acc, X);
-    layer_step<MT, KS0 + 2>(R, F, h, b, acc, X);
-    layer_step<MT, KS0 + 3>(R, F, h, b, acc, X);
+                                                     f4 (&acc)[MT][kNT], H &X, const TP &T = TP{}, int tl = -1) {
+    layer_step<MT, KS0 + 0>(R, F, h, b, acc, X, T, tl);
+    layer_step<MT, KS0 + 1>(R, F, h, b, acc, X, T, tl);
+    layer_step<MT, KS0 + 2>(R, F, h, b, acc, X, T, tl);
+    layer_step<MT, KS0 + 3>(R, F, h, b, acc, X, T, tl);
   }
 
   // One readout unit: k-steps s = 16*HH + 4*U + i for P (W_e[:, :H]) and Q (W_e[:, H:]).
@@ -264,7 +269,7 @@ struct CoreF32T {
     const int g4 = 4 * (lane >> 4);
     f4 h[MT][kNT];
     input_layer<MT>(S, lane, feat, h);
-    if constexpr (TP::kOn) T.template put_h<MT>(0, h, lane);
+    if constexpr (TP::kOn) T.template put_mask<MT>(0, h, lane);
     // cell-split waves: the boundary columns are published here and read
     // after the ring barrier that ends the next layer's first chunk
     // (layer_step<4>), long before the first neighbour-sum k-step (32)
@@ -283,27 +288,27 @@ struct CoreF32T {
       }
       float b[MT];
       b_operand<MT, 0>(h, b, X);
-      layer_chunk<MT, 0>(R, F, h, b, acc, X);
-      layer_chunk<MT, 4>(R, F, h, b, acc, X);
-      layer_chunk<MT, 8>(R, F, h, b, acc, X);
-      layer_chunk<MT, 12>(R, F, h, b, acc, X);
-      layer_chunk<MT, 16>(R, F, h, b, acc, X);
-      layer_chunk<MT, 20>(R, F, h, b, acc, X);
-      layer_chunk<MT, 24>(R, F, h, b, acc, X);
-      layer_chunk<MT, 28>(R, F, h, b, acc, X);
-      layer_chunk<MT, 32>(R, F, h, b, acc, X);
-      layer_chunk<MT, 36>(R, F, h, b, acc, X);
-      layer_chunk<MT, 40>(R, F, h, b, acc, X);
-      layer_chunk<MT, 44>(R, F, h, b, acc, X);
-      layer_chunk<MT, 48>(R, F, h, b, acc, X);
-      layer_chunk<MT, 52>(R, F, h, b, acc, X);
-      layer_chunk<MT, 56>(R, F, h, b, acc, X);
-      layer_chunk<MT, 60>(R, F, h, b, acc, X);
+      layer_chunk<MT, 0>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 4>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 8>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 12>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 16>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 20>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 24>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 28>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 32>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 36>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 40>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 44>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 48>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 52>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 56>(R, F, h, b, acc, X, T, l);
+      layer_chunk<MT, 60>(R, F, h, b, acc, X, T, l);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) h[mt][nt] = relu4(acc[mt][nt]);
-      if constexpr (TP::kOn) T.template put_h<MT>(l + 1, h, lane);
+      if constexpr (TP::kOn) T.template put_mask<MT>(l + 1, h, lane);
       if constexpr (H::kOn) {
         if (l + 1 < W.layers) X.publish(h);
       }
@@ -313,6 +318,7 @@ struct CoreF32T {
       return;
     }
 
+    if constexpr (TP::kOn) T.template put_all<MT>(W.layers, h, lane);  // h[L] (one burst)
     // edge readout, P/Q split (src/flux_gnn.py:62-66).  The 128-feature dot
     // w2 . ReLU(z) is summed as four partial dots over tile pairs (2w, 2w+1),
     // then added in w order; readout_cells keeps the same order, so both

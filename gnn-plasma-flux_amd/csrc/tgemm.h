@@ -145,10 +145,11 @@ struct EpiMask {
 struct EpiPart {
   float *part;
   int64_t I, J;
+  int64_t z = 0;  // the split (set by tgemm_kernel)
   __device__ float bias_of(int64_t) const { return 0.f; }
   static constexpr bool kPre = false, kBlock = false;
   __device__ float pre(int64_t, int64_t) const { return 0.f; }
-  __device__ void operator()(int64_t i, int64_t j, float v, float, float) const { part[(blockIdx.z * I + i) * J + j] = v; }
+  __device__ void operator()(int64_t i, int64_t j, float v, float, float) const { part[(z * I + i) * J + j] = v; }
 };
 // out[i][j] = tanh(v + bias[j]) (PureGNN's output_mlp.0, train_pure_gnn.py:74-75)
 struct EpiTanh {
@@ -250,8 +251,26 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
   __shared__ float sA[2][kBufF];
   __shared__ float sB[2][kBufF];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wi = wave >> 1, wj = wave & 1, h = lane >> 5;
-  const int64_t i0 = (int64_t)blockIdx.x * kBM, j0 = (int64_t)blockIdx.y * kBN;
-  const int64_t rb = (int64_t)blockIdx.z * rsplit;
+#ifndef HF_TG_XCD
+#define HF_TG_XCD 1
+#endif
+  // HF_TG_XCD (measured +0.8 % on the training step, profiles/r05_train_tgemm_xcd_prio_ab.txt):
+  // pairs of consecutive tiles (x fastest) on one XCD.  Blocks b and
+  // b + 8 share an XCD (MI355X_MICROARCH.md, workgroup dispatch); consecutive
+  // tiles of a weight-gradient split read the same rows (the two column tiles
+  // of [h ; agg h], or the P and Q halves against h[L]).
+  unsigned bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (HF_TG_XCD) {
+    const unsigned gx = gridDim.x, gy = gridDim.y, T = gx * gy * gridDim.z;
+    unsigned L = bx + gx * (by + gy * bz);
+    if (L < T - T % 16) L = 2 * (8 * (L >> 4) + (L & 7)) + ((L >> 3) & 1);
+    bx = L % gx;
+    by = (L / gx) % gy;
+    bz = L / (gx * gy);
+  }
+  const int64_t i0 = (int64_t)bx * kBM, j0 = (int64_t)by * kBN;
+  const int64_t rb = (int64_t)bz * rsplit;
+  if constexpr (std::is_same<Epi, EpiPart>::value) epi.z = bz;
   const int64_t re = rb + rsplit < R ? rb + rsplit : R;
   f16 acc[2][2];
 #pragma unroll
@@ -417,7 +436,7 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
         }
     }
   }
-  if (COLSUM && blockIdx.y == 0) {
+  if (COLSUM && by == 0) {
     // thread t summed the rows t>>5 (+8q) of columns 4(t&31)..+3: fold the 8 row groups in order
     __shared__ f4 s_cs[256];
     s_cs[t] = csum;
@@ -429,7 +448,7 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int64_t i = i0 + 4 * t + e;
-        if (i < I) bias_part[(int64_t)blockIdx.z * I + i] = v[e];
+        if (i < I) bias_part[(int64_t)bz * I + i] = v[e];
       }
     }
   }

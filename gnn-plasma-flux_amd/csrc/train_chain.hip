@@ -181,6 +181,92 @@ __global__ __launch_bounds__(256) void edge_backward_kernel(const float *__restr
     partial[(int64_t)blockIdx.x * (H + 1) + H] = __fadd_rn(__fadd_rn(s_b2[0], s_b2[1]), __fadd_rn(s_b2[2], s_b2[3]));
 }
 
+// The same for H = 128 with each PQ row read once: a wave owns kEbCells
+// consecutive cells of one IC and loads rows i0-1 .. i0+kEbCells (one float4
+// per lane: lanes 0-31 hold P, lanes 32-63 Q of channels 4(l&31)..+3); the
+// other half's value of a row comes from a lane swap.  A P lane forms dP_i
+// from z_f(i) = P_i + Q_{i+1} and z_b(i-1) = P_i + Q_{i-1}, a Q lane dQ_i from
+// z_b(i) = Q_i + P_{i+1} and z_f(i-1) = Q_i + P_{i-1}: the same sums and
+// products as edge_backward_kernel, bit for bit.  dw2 is accumulated per lane
+// half (P lanes the g_f terms, Q lanes the g_b terms) and joined at the end,
+// in a fixed order.
+constexpr int kEbCells = 16;
+__device__ __forceinline__ float other_half(float v) {  // v of lane l ^ 32
+  const unsigned u = __float_as_uint(v);
+  const auto s = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float((threadIdx.x & 32) ? s[0] : s[1]);
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__global__ __launch_bounds__(256) void edge_backward_h128_kernel(const float *__restrict__ PQ, int64_t B, int nx,
+                                                                 const float *__restrict__ w2,
+                                                                 const float *__restrict__ g, float *__restrict__ dPQ,
+                                                                 float *__restrict__ partial) {
+  constexpr int H = 128, RW = 2 * H;
+  __shared__ f4 s_acc[4][32];
+  __shared__ float s_b2[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool qs = lane >= 32;
+  const f4 w = *reinterpret_cast<const f4 *>(w2 + 4 * (lane & 31));
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;
+  const int segs = (nx + kEbCells - 1) / kEbCells;
+  const int64_t units = B * segs;
+  for (int64_t u = (int64_t)blockIdx.x * 4 + wv; u < units; u += (int64_t)gridDim.x * 4) {
+    const int64_t b = u / segs;
+    const int i0 = (int)(u - b * segs) * kEbCells, nc = nx - i0 < kEbCells ? nx - i0 : kEbCells;
+    const float *G = g + b * 2 * nx;
+    const float *R = PQ + b * nx * RW + 4 * lane;
+    float *D = dPQ + b * nx * RW + 4 * lane;
+    // lane t <= kEbCells: g_f, g_b of cell i0 - 1 + t (periodic)
+    // cells i0 - 1 .. i0 + kEbCells, periodic (one wrap when nx > kEbCells)
+    auto wrap = [&](int i) { return nx > kEbCells ? (i < 0 ? i + nx : (i >= nx ? i - nx : i)) : ((i % nx) + nx) % nx; };
+    const int ct = wrap(i0 - 1 + (lane <= kEbCells ? lane : 0));
+    const float gfv = G[ct], gbv = G[nx + ct];
+    f4 row[kEbCells + 2];
+#pragma unroll
+    for (int r = 0; r < kEbCells + 2; ++r) row[r] = *reinterpret_cast<const f4 *>(R + (int64_t)wrap(i0 - 1 + r) * RW);
+#pragma unroll
+    for (int k = 0; k < kEbCells; ++k) {
+      if (k >= nc) continue;  // (wave-uniform)
+      const float gfm = lane_f(gfv, k + 1), gbm = lane_f(gbv, k + 1);
+      const float gfp = lane_f(gfv, k), gbp = lane_f(gbv, k);
+      const float a = qs ? gbm : gfm, c = qs ? gfp : gbp;
+      f4 d;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float own = row[k + 1][e];
+        // (the other half's values by a lane swap per use: swapping each row once
+        // holds ~270 VGPRs, one wave per SIMD, for a memory-bound kernel)
+        const float z1 = __fadd_rn(own, other_half(row[k + 2][e])), z2 = __fadd_rn(own, other_half(row[k][e]));
+        d[e] = __fadd_rn(z1 > 0.f ? __fmul_rn(a, w[e]) : 0.f, z2 > 0.f ? __fmul_rn(c, w[e]) : 0.f);
+        acc[e] = fmaf(a, z1 > 0.f ? z1 : 0.f, acc[e]);
+      }
+      *reinterpret_cast<f4 *>(D + (int64_t)(i0 + k) * RW) = d;
+      accb = __fadd_rn(accb, __fadd_rn(gfm, gbm));
+    }
+  }
+  f4 tot;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float o = other_half(acc[e]);  // every lane takes part in the swap
+    tot[e] = qs ? __fadd_rn(o, acc[e]) : __fadd_rn(acc[e], o);
+  }
+  if (lane < 32) s_acc[wv][lane] = tot;
+  if (lane == 0) s_b2[wv] = accb;
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < H) {
+    const float *sa = reinterpret_cast<const float *>(s_acc);
+    partial[(int64_t)blockIdx.x * (H + 1) + t] =
+        __fadd_rn(__fadd_rn(sa[t], sa[128 + t]), __fadd_rn(sa[256 + t], sa[384 + t]));
+  } else if (t == H) {
+    partial[(int64_t)blockIdx.x * (H + 1) + H] =
+        __fadd_rn(__fadd_rn(s_b2[0], s_b2[1]), __fadd_rn(s_b2[2], s_b2[3]));
+  }
+}
+
 // gw2[c] = sum_b partial[b][c] (c < H), gb2 = sum_b partial[b][H]: block c,
 // thread k sums blocks k, k + 256, ... in order, then a fixed-order LDS tree.
 __global__ __launch_bounds__(256) void edge_partial_reduce_kernel(const float *__restrict__ partial, int nb, int H,
@@ -517,8 +603,12 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
     return hipGetLastError();
   };
   // readout: dPQ, dw2, db2                                                          (:62-66)
-  hipLaunchKernelGGL(edge_backward_kernel, dim3(kEdgeBlocks), dim3(256), 0, s, t.pq, H, N, nx, w.w_2, grad_flux, dPQ,
-                     epart);
+  if (H == 128)
+    hipLaunchKernelGGL(edge_backward_h128_kernel, dim3(kEdgeBlocks), dim3(256), 0, s, t.pq, N / nx, nx, w.w_2,
+                       grad_flux, dPQ, epart);
+  else
+    hipLaunchKernelGGL(edge_backward_kernel, dim3(kEdgeBlocks), dim3(256), 0, s, t.pq, H, N, nx, w.w_2, grad_flux, dPQ,
+                       epart);
   hipLaunchKernelGGL(edge_partial_reduce_kernel, dim3((unsigned)(H + 1)), dim3(256), 0, s, epart,
                      kEdgeBlocks, H, const_cast<float *>(g.w_2), const_cast<float *>(g.b_2));
   // dW_e[c % H][(c / H) H + k] = sum_m dPQ[m][c] h[L][m][k]; db_e = column sums of dP

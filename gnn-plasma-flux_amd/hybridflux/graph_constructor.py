@@ -14,10 +14,31 @@ import torch
 CHAIN_TAG = "_hf_chain"
 
 
+_EI_CACHE = {}  # (nx, batch, device) -> (edge_index, its _version when cached)
+_EI_CACHE_MAX = 4
+
+
 def chain_edge_index(nx, batch=1, device=None):
     """Edge list of `batch` disjoint periodic chains of nx cells.  Per IC b the
     2*nx edges are (i -> i+1) for i < nx, then (i+1 -> i) — the order of
-    src/graph_constructor.py:34-38 — offset by b*nx nodes."""
+    src/graph_constructor.py:34-38 — offset by b*nx nodes.
+
+    The training loop builds the same graph every step (train_ablation.py:115
+    calls build_chain_graph per sample), so the tensor of a (nx, batch, device)
+    is built once and handed out again while it is unmodified (its autograd
+    _version unchanged): eight small device launches less per step."""
+    key = (int(nx), int(batch), str(torch.device(device) if device is not None else torch.device("cpu")))
+    hit = _EI_CACHE.get(key)
+    if hit is not None and hit[0]._version == hit[1]:
+        return hit[0]
+    ei = _chain_edge_index(nx, batch, device)
+    if len(_EI_CACHE) >= _EI_CACHE_MAX:
+        _EI_CACHE.pop(next(iter(_EI_CACHE)))
+    _EI_CACHE[key] = (ei, ei._version)
+    return ei
+
+
+def _chain_edge_index(nx, batch, device):
     src = torch.arange(nx, dtype=torch.long, device=device)
     dst = (src + 1) % nx
     row = torch.cat([src, dst])

@@ -44,13 +44,15 @@ def flop_per_sample(cfg_name, nx=64, H=128, L=4, F=4):
 
 def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False, fused_adam=False, warm_s=0.3):
     """samples/s of `steps` optimizer steps at `batch` samples each (eager, or
-    replaying the captured step: hybridflux.training.GraphedStep; fused_adam:
-    torch's single-kernel Adam instead of the default multi-tensor one)."""
+    replaying the captured step: hybridflux.training.GraphedStep, with torch's
+    fused capturable Adam; fused_adam: eager with torch's single-kernel Adam
+    instead of the default multi-tensor one)."""
     from hybridflux.training import GraphedStep, train_steps
     torch.manual_seed(0)
     m = hf.FluxGNN(4, 128, 4).to("cuda")
     opt = (torch.optim.Adam(m.parameters(), lr=1e-3, fused=True) if fused_adam else
-           torch.optim.Adam(m.parameters(), lr=1e-3, capturable=graphed))
+           torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True, fused=True) if graphed else
+           torch.optim.Adam(m.parameters(), lr=1e-3))
     cfg = hf.ABLATION_CONFIGS[cfg_name]
     gen = torch.Generator().manual_seed(1)
     gs = GraphedStep(m, opt, data, batch, x, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
