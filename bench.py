@@ -80,6 +80,26 @@ def cpu_batched(weights, nx, T, n_ics, threads):
     return n_ics * T / (time.perf_counter() - t0)
 
 
+def cgroup_cpus():
+    """CPUs this process's cgroup may use (cpu.max quota / period), or None when
+    unlimited or unreadable.  On the GPU box the affinity set is the whole host
+    (256 CPUs) while the share is 16: torch threads beyond the quota only queue."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        return None
+
+
+_T_START = time.perf_counter()
+
+
+def progress(msg):
+    """A phase marker on stderr (the GPU box's runner kills a run silent for 180 s)."""
+    print(f"bench.py [{time.perf_counter() - _T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def pinned(n):
     """The first n CPUs this process may run on (taskset -c equivalent), as a set."""
     avail = sorted(os.sched_getaffinity(0))
@@ -251,6 +271,7 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
            "dataset": "DATASET_CONFIG recipe: 50 ICs x 40 steps, nx=64 (GPU classical rollout)"}
     best = None
     for mode in ("eager", "eager_fused_adam", "graphed"):
+        progress(f"training line: {mode}")
         graphed = mode == "graphed"
         torch.manual_seed(0)
         m = FluxGNN(4, 128, 4).to(dev)
@@ -491,6 +512,7 @@ def main():
 
     # warmup: one rollout of W steps (compiles nothing; faults the code objects
     # in) and its metric exchange
+    progress(f"headline warmup ({B} ICs x {nx} cells, {Wr} steps)")
     warm = solver.run_batch(ics, Wr, traj=warm_traj if warm_traj is not None else False, metrics=warm_met,
                             out=warm_final, ws=ws)
     gather_rollout(warm, n_total)
@@ -531,6 +553,7 @@ def main():
     kernel_ms_again = ev2.elapsed_time(ev3)
 
     # other precisions, same ICs / K / warmup, timed the same way (reported, not the headline)
+    progress("headline timed; alternates")
     alt = {}
     for prec in [p for p in args.also.split(",") if p and p != args.precision]:
         s2 = HybridSolver(weights, radius=3, nx=nx, dt=dt, device=dev, precision=prec)
@@ -597,6 +620,7 @@ def main():
 
     others = None
     if world == 1 and not args.no_other_configs:
+        progress("cfg2 / cfg4")
         # cfg4's first ICs (seeds 1000..1003) against committed vectors: the bf16
         # kernels' emulation and the f32 forward on bf16 weights (tests/golden/
         # make_oracle_vectors.py), and the reference's own f32 rollout
@@ -614,7 +638,11 @@ def main():
                   other_config(w_r2, dev, "cfg4: 1024-cell chain, 4096-IC batch, r=2, bf16 MLP weights, dt=3.125e-4",
                                4096, 1024, "bf16", 30, 30, 2, fixture=fx, tridiag=True)]
 
+    if world == 1 and not args.no_other_configs:
+        progress("PureGNN / PINN")
     models = other_models(dev, 4096, 30) if world == 1 and not args.no_other_configs else None
+    if world == 1 and not args.no_other_configs and not args.no_train:
+        progress("training line")
     train = train_line(dev) if world == 1 and not args.no_other_configs and not args.no_train else None
 
     wall_max = max_over_ranks(wall)
@@ -637,17 +665,24 @@ def main():
             keep = os.sched_getaffinity(0)
             os.sched_setaffinity(0, cores)
             try:
+                progress(f"cpu baseline on {len(cores)} pinned cores")
                 alpha, beta = cpu_baseline(weights, nx, 30, args.cpu_sample_ics, len(cores))
             finally:
                 os.sched_setaffinity(0, keep)
-            beta_all = cpu_batched(weights, nx, 30, args.cpu_sample_ics, len(keep))
+            quota = cgroup_cpus()
+            n_all = min(len(keep), quota) if quota else len(keep)
+            progress(f"cpu baseline: batched form on {n_all} threads (affinity {len(keep)}, cgroup {quota})")
+            beta_all = cpu_batched(weights, nx, 30, args.cpu_sample_ics, n_all)
             cpu = {"value": round(alpha, 1), "unit": "IC-steps/s", "cores": len(cores), "kind": "port",
                    "sample": f"{args.cpu_sample_ics} ICs x 30 steps, one IC at a time (reference-faithful "
                              f"HybridSolver loop: torch-CPU FluxGNN + numpy FV/FFT), nx={nx}",
                    "pinned_cpus": f"{min(cores)}-{max(cores)} ({len(cores)} of host nproc {os.cpu_count()})",
                    "batched_torch_cpu_value": round(beta, 1),
-                   "batched_torch_cpu_all_cores": {"value": round(beta_all, 1), "threads": len(keep),
-                                                   "note": "the batched form at the process's full CPU affinity set"}}
+                   "batched_torch_cpu_all_cores": {
+                       "value": round(beta_all, 1), "threads": n_all, "affinity_cpus": len(keep),
+                       "cgroup_cpus": quota,
+                       "note": "the batched form on every CPU the process may use: its affinity set, capped at "
+                               "its cgroup CPU quota (threads beyond the quota only queue)"}}
         line = {
             "metric": METRIC,
             "value": round(value, 1),
