@@ -515,8 +515,11 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
   constexpr int NX = 16 * NC, NTH = 64 * (H / 16);
   __shared__ float s_st[3 * NX];
   __shared__ float s_x[NX];
-  __shared__ f4v s_act4[H * NX / 4];
-  float *act = reinterpret_cast<float *>(s_act4);
+  // two activation buffers: a layer reads h from one and writes h' to the
+  // other, so no barrier has to separate every wave's reads of h from the
+  // in-place rewrite (one barrier per layer instead of two)
+  __shared__ f4v s_act4[2][H * NX / 4];
+  float *act = reinterpret_cast<float *>(s_act4[0]), *act2 = reinterpret_cast<float *>(s_act4[1]);
   const int tid = threadIdx.x, u = tid >> 6, lane = tid & 63, q4 = 4 * (lane >> 4);
   const int64_t b = blockIdx.x;
   const int64_t ldt = (int64_t)(T + 1) * 3 * NX;
@@ -546,14 +549,13 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
         pure_tiles_packed<H, NC, 2>(w.w_lp + ((int64_t)l * (H / 16) + u) * 2 * (H / 16) * 256, act, lane, acc);
       else
         pure_tiles<H, NC, 2>([&](int j, int m) { return W + (int64_t)(16 * u + m) * 2 * H + j * H; }, act, lane, acc);
-      __syncthreads();  // every wave's reads of h are done: h is rewritten in place below
       f4v bq;
 #pragma unroll
       for (int i = 0; i < 4; ++i) bq[i] = bl[16 * u + q4 + i];
 #pragma unroll
       for (int g = 0; g < NC; ++g) {
-        float *hp = act + ((u * NC + g) * 64 + lane) * 4;
-        f4v h = *reinterpret_cast<const f4v *>(hp);
+        const int o = ((u * NC + g) * 64 + lane) * 4;
+        f4v h = *reinterpret_cast<const f4v *>(act + o);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           // cell NC c + g: left (g - 1, c) or, at g = 0, (NC - 1, c - 1); right (g + 1, c) or (0, c + 1)
@@ -564,9 +566,12 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
           m = __fadd_rn(m, tanh_fast(__fadd_rn(__fadd_rn(pr, qv), bq[i])));
           h[i] = __fadd_rn(h[i], m);
         }
-        *reinterpret_cast<f4v *>(hp) = h;
+        *reinterpret_cast<f4v *>(act2 + o) = h;
       }
       __syncthreads();
+      float *tmp = act;
+      act = act2;
+      act2 = tmp;
     }
     // output_mlp.0: o = tanh(W_o1 h + b_o1), written over h once every wave has read it
     {
@@ -578,16 +583,20 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
       f4v bo;
 #pragma unroll
       for (int i = 0; i < 4; ++i) bo[i] = w.b_o1[16 * u + q4 + i];
-      __syncthreads();
 #pragma unroll
       for (int g = 0; g < NC; ++g) {
         f4v o;
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = tanh_fast(__fadd_rn(acc[0][g][i], bo[i]));
-        *reinterpret_cast<f4v *>(act + ((u * NC + g) * 64 + lane) * 4) = o;
+        *reinterpret_cast<f4v *>(act2 + ((u * NC + g) * 64 + lane) * 4) = o;
       }
     }
     __syncthreads();
+    {
+      float *tmp = act;
+      act = act2;
+      act2 = tmp;
+    }
     // output_mlp.2 and the update: state += W_o2 o + b_o2
     if (tid < 3 * NX) {
       const int ch = tid / NX, c = tid - ch * NX;
