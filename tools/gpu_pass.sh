@@ -13,7 +13,7 @@ echo "pytest rc=$prc"; tail -1 gpurun_out/pytest_gpu_$TAG.log; grep -E "^FAILED|
 case $prc in 124|134|137|139) exit 3;; esac
 grep -qE "Fatal|core dumped|Aborted|Segmentation|Memory access fault" gpurun_out/pytest_gpu_$TAG.log && exit 3
 timeout -k 10 150 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 && cat gpurun_out/smoke_$TAG.log || exit 4
-timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 5
+timeout -k 10 500 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 5
 cut -c1-600 gpurun_out/bench_$TAG.json
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver_$TAG.json 2> gpurun_out/bench_driver_$TAG.err || exit 6
 cut -c1-300 gpurun_out/bench_driver_$TAG.json
