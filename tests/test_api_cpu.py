@@ -59,6 +59,21 @@ def test_build_chain_graph_matches_reference_layout():
     assert torch.equal(nfb, O.node_features(G, states))
 
 
+def test_chain_edge_index_cache_is_safe():
+    """chain_edge_index hands out the tensor of a (nx, batch, device) again only
+    while it is unmodified: an in-place edit drops the tag and the next call
+    builds a fresh, correct edge index."""
+    from hybridflux.graph_constructor import chain_edge_index, chain_tag
+    a = chain_edge_index(7, 3)
+    assert chain_edge_index(7, 3) is a and chain_tag(a) == (3, 7)
+    assert torch.equal(a, O.chain_edges(7, 3))
+    a[0, 0] = 5  # a caller edits its copy in place
+    assert chain_tag(a) is None
+    b = chain_edge_index(7, 3)
+    assert b is not a and chain_tag(b) == (3, 7) and torch.equal(b, O.chain_edges(7, 3))
+    assert chain_edge_index(7, 4) is not b  # another batch size, another tensor
+
+
 def test_cpu_inputs_raise_no_fallback():
     """Host tensors are staged to a HIP device; with none visible (this
     container) every drop-in entry point raises instead of computing on the CPU."""
