@@ -1,0 +1,12 @@
+#!/bin/bash
+# Training tests on the shipped build, its training-step kernel trace, then
+# the A/B against the split-K GEMM weight gradients (HF_WGRAD_DIRECT=0).
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+TAG=${1:-r05_wg}
+timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout 300 --timeout-method thread > gpurun_out/tr_pytest_$TAG.log 2>&1
+rc=$?; tail -3 gpurun_out/tr_pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+bash tools/gpu_train_prof.sh $TAG > gpurun_out/prof_$TAG.out 2>&1 || exit $?
+head -14 gpurun_out/train_kernel_stats_$TAG.md | cut -c1-160
+bash tools/gpu_train_ab.sh wg gnn-plasma-flux_amd/hybridflux/_lib/libhybridflux.so build/ab/lib_gemmwg.so
