@@ -48,8 +48,10 @@ def bench_build(tag):
 
 
 def traffic(tag):
-    f = last_value(glob(f"gpurun_out/pmc_fetch_{tag}/*.db")[0], "FETCH_SIZE")
-    w = last_value(glob(f"gpurun_out/pmc_write_{tag}/*.db")[0], "WRITE_SIZE")
+    # databases under /tmp on the box (tools/gpu_pmc_traffic.sh), or gpurun_out/ (older passes)
+    db = lambda kind: (glob(f"/tmp/pmc_{kind}_{tag}/*.db") + glob(f"gpurun_out/pmc_{kind}_{tag}/*.db"))[0]  # noqa: E731
+    f = last_value(db("fetch"), "FETCH_SIZE")
+    w = last_value(db("write"), "WRITE_SIZE")
     return 2 * f[1] * 1024, w[1] * 1024, f[2] / 1e3
 
 
