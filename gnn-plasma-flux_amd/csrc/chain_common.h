@@ -126,10 +126,18 @@ constexpr int kRingSlots = 4;
 // off a wave's 16 lanes come from the adjacent waves' boundary columns,
 // exchanged through LDS once per layer (chain_rollout_cells_kernel, chain_f32.hip).
 struct NoHalo {
-  static constexpr bool kOn = false;
+  static constexpr bool kOn = false, kSecond = false;
+};
+// The readout's data gradient as a layer pass (chain_train_bwd_kernel): the
+// B operand's second half (k-steps 32..63) is dQ itself, not a neighbour sum
+// of the first half's array (which holds dP).
+template <int MT>
+struct SecondHalf {
+  static constexpr bool kOn = false, kSecond = true;
+  f4 q[MT][kNT];
 };
 struct CellHalo {
-  static constexpr bool kOn = true;
+  static constexpr bool kOn = true, kSecond = false;
   f4 l[kNT], r[kNT];  // the lane's 32 features at cell 16*pos - 1 (lanes j=0) / 16*pos + 16 (lanes j=15)
   f4 *xh;             // [parity 2][wave 4][side 2][g 4][nt 8]: boundary columns of h
   f4 *xq;             // [wave 4][ot 8][P|Q 2][g 4]: column j=0 of the readout accumulators
@@ -208,7 +216,7 @@ struct TileStore {
 struct TrainTape : TileStore {
   static constexpr bool kOn = true;
   float *pq;  // [N][2H]
-  // ReLU'(h[l]) = h[l] > 0 of layers l < L as bits in the lanes' own layout
+  // ReLU'(h[l]) = h[l] > 0 of layers l <= L as bits in the lanes' own layout
   // (chain_train_bwd_kernel reads them back): word [l][b][mt][lane], bit 4nt + r
   unsigned *mbits;
   int64_t mstride;  // words per layer (B * MT * 64)
@@ -216,7 +224,7 @@ struct TrainTape : TileStore {
   int layers;
   template <int MT>
   __device__ __forceinline__ void put_mask(int l, const f4 (&h)[MT][kNT], int lane) const {
-    if (!live || l >= layers) return;
+    if (!live || l > layers) return;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       unsigned m = 0;
@@ -710,13 +718,14 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_fw
 // (TrainTape::mbits).  g[l] = g0 + l * gstride, [N][H] each.
 template <class Core, int MT>
 __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bwd_kernel(
-    ChainW W, int64_t items, float *g0, int64_t gstride, const unsigned *__restrict__ mbits) {
+    ChainW W, int64_t items, float *g0, int64_t gstride, const unsigned *__restrict__ mbits,
+    const float *__restrict__ dPQ) {
   constexpr int nx = 16 * MT;
   __shared__ f4 lds4[Core::kSlots * Core::kChunkFloats / 4];
   float *lds = reinterpret_cast<float *>(lds4);
   const int L = W.layers;
   auto R = make_ring<Core>(W, lds);
-  R.chunks = 16 * L;  // update layers only
+  R.chunks = 16 * (L + (dPQ ? 1 : 0));  // (the readout's pass,) the update layers
   R.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(W.stream), 0, R.chunks * Core::kChunkFloats * 4,
                                              0x00020000);
   const int lane = R.lane, j = lane & 15, g4 = 4 * (lane >> 4);
@@ -732,7 +741,50 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bw
     GradTape GT;
     GT.base = g0, GT.stride = gstride, GT.row0 = b * nx, GT.live = live;
     f4 g[MT][kNT];
-    {
+    if (dPQ) {
+      // g[L] = ReLU'(h[L]) * (W_a^T dP + W_b^T dQ): a layer pass with B = [dP ; dQ]
+      SecondHalf<MT> X;
+      const float *src = dPQ + b * nx * 2 * kH + g4;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) {
+          g[mt][nt] = ldf4(src + (int64_t)cell_of<MT>(mt, j) * 2 * kH + 16 * nt);
+          X.q[mt][nt] = ldf4(src + (int64_t)cell_of<MT>(mt, j) * 2 * kH + kH + 16 * nt);
+        }
+      unsigned mb[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) mb[mt] = mbits[L * mstride + b * MT * 64 + mt * 64 + lane];
+      f4 acc[MT][kNT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
+      float bop[MT];
+      Core::template b_operand<MT, 0>(g, bop, X);
+      Core::template layer_chunk<MT, 0>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 4>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 8>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 12>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 16>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 20>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 24>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 28>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 32>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 36>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 40>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 44>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 48>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 52>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 56>(R, F, g, bop, acc, X);
+      Core::template layer_chunk<MT, 60>(R, F, g, bop, acc, X);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g[mt][nt][r] = (mb[mt] >> (4 * nt + r)) & 1u ? acc[mt][nt][r] : 0.f;
+    } else {
       const float *src = g0 + L * gstride + b * nx * kH + g4;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -749,7 +801,8 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bw
 #pragma unroll
         for (int nt = 0; nt < kNT; ++nt) acc[mt][nt] = f4{0.f, 0.f, 0.f, 0.f};
       NoHalo X;
-      const int tl = l + 1 < L ? l + 1 : -1;  // g[l+1] (the B operand) to memory, spread over the pass
+      // g[l+1] (the B operand) to memory, spread over the pass (g[L] only when made here)
+      const int tl = l + 1 < L || dPQ ? l + 1 : -1;
       float bop[MT];
       Core::template b_operand<MT, 0>(g, bop, X);
       Core::template layer_chunk<MT, 0>(R, F, g, bop, acc, X, GT, tl);

@@ -92,7 +92,10 @@ struct CoreF32T {
 #else
     if constexpr (KS >= kKS) {
 #endif
-      if constexpr (H::kOn) {
+      if constexpr (H::kSecond) {  // the readout's backward: [dP ; dQ], no neighbour sum
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) b[mt] = X.q[mt][s >> 2][s & 3];
+      } else if constexpr (H::kOn) {
         static_assert(MT == 1, "cell-split waves hold 16 cells");
         b[0] = nb_sum_halo(b[0], X.l[s >> 2][s & 3], X.r[s >> 2][s & 3]);
       } else {
@@ -471,14 +474,17 @@ __global__ void pack_chain_f32_kernel(GraphW w, float *__restrict__ stream, int6
 // The update layers' transposed weights for chain_train_bwd_kernel, in the
 // f32 stream format, layers L-1 .. 0: A(n, k) = W_l[k][n] (k < H: W_a^T) or
 // W_l[k - H][H + n] / 2 (W_b^T with the mean's 1/deg).
-__global__ void pack_chain_bwd_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream) {
+// ro: the readout's [W_a^T | W_b^T] of edge_mlp.0 first (16 chunks, no 1/deg).
+__global__ void pack_chain_bwd_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream, int ro) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= nstream) return;
   const int c = (int)(idx >> 11), rem = (int)(idx & 2047), j = rem >> 8, lane = (rem >> 2) & 63, cc = rem & 3;
-  const int l = w.layers - 1 - (c >> 4), s = 4 * (c & 15) + (j >> 1), n = 16 * (4 * (j & 1) + cc) + (lane & 15);
-  const int k = kperm_dev(s % kKS, lane);
-  const float *W = w.w_l + l * w.lsw;
-  stream[idx] = s < kKS ? W[(int64_t)k * 2 * kH + n] : 0.5f * W[(int64_t)k * 2 * kH + kH + n];
+  const bool readout = ro && c < 16;
+  const int l = w.layers - 1 - ((c - (ro ? 16 : 0)) >> 4), s = 4 * (c & 15) + (j >> 1);
+  const int n = 16 * (4 * (j & 1) + cc) + (lane & 15), k = kperm_dev(s % kKS, lane);
+  const float *W = readout ? w.w_e : w.w_l + l * w.lsw;
+  const float half = readout ? 1.f : 0.5f;
+  stream[idx] = s < kKS ? W[(int64_t)k * 2 * kH + n] : half * W[(int64_t)k * 2 * kH + kH + n];
 }
 
 template <int MT>
@@ -496,9 +502,9 @@ hipError_t train_fwd_launch(const ChainW &cw, const float *b2p, const float *nf,
 }
 template <int MT>
 hipError_t train_bwd_launch(const ChainW &cw, int64_t B, float *g0, int64_t gstride, const unsigned *mbits,
-                            hipStream_t s) {
+                            const float *dPQ, hipStream_t s) {
   hipLaunchKernelGGL((chain_train_bwd_kernel<CoreF32, MT>), dim3((unsigned)train_blocks<MT>(B)),
-                     dim3(64 * CoreF32::kNW), 0, s, cw, B, g0, gstride, mbits);
+                     dim3(64 * CoreF32::kNW), 0, s, cw, B, g0, gstride, mbits, dPQ);
   return hipGetLastError();
 }
 }  // namespace
@@ -507,25 +513,26 @@ int64_t chain_train_pack_bytes(int layers) {
   return (int64_t)chain_chunks(layers, kPrecF32) * chain_chunk_bytes(kPrecF32) +
          (int64_t)sizeof(float) * (512 + kH * (3 + layers));
 }
-int64_t chain_train_mask_bytes(int layers, int64_t N) { return (int64_t)layers * N * 16; }
-int64_t chain_train_bwd_pack_bytes(int layers) { return (int64_t)16 * layers * chain_chunk_bytes(kPrecF32); }
+int64_t chain_train_mask_bytes(int layers, int64_t N) { return (int64_t)(layers + 1) * N * 16; }
+int64_t chain_train_bwd_pack_bytes(int layers) { return (int64_t)16 * (layers + 1) * chain_chunk_bytes(kPrecF32); }
 
 hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, float *g0, int64_t gstride,
-                                        const unsigned *mbits, void *pack, hipStream_t s) {
+                                        const unsigned *mbits, void *pack, const float *dPQ, hipStream_t s) {
   const int L = w.layers;
-  if (B <= 0 || L == 0) return hipSuccess;
+  if (B <= 0 || (L == 0 && !dPQ)) return hipSuccess;
   float *stream = static_cast<float *>(pack);
-  const int64_t nstream = (int64_t)16 * L * 2048;
-  hipLaunchKernelGGL(pack_chain_bwd_f32_kernel, dim3((unsigned)(nstream / 256)), dim3(256), 0, s, w, stream, nstream);
+  const int64_t nstream = (int64_t)16 * (L + (dPQ ? 1 : 0)) * 2048;
+  hipLaunchKernelGGL(pack_chain_bwd_f32_kernel, dim3((unsigned)(nstream / 256)), dim3(256), 0, s, w, stream, nstream,
+                     dPQ ? 1 : 0);
   ChainW cw{};
   cw.stream = stream;
   cw.layers = L;
   cw.prec = kPrecF32;
   switch (nx) {
-    case 16: return train_bwd_launch<1>(cw, B, g0, gstride, mbits, s);
-    case 32: return train_bwd_launch<2>(cw, B, g0, gstride, mbits, s);
-    case 48: return train_bwd_launch<3>(cw, B, g0, gstride, mbits, s);
-    case 64: return train_bwd_launch<4>(cw, B, g0, gstride, mbits, s);
+    case 16: return train_bwd_launch<1>(cw, B, g0, gstride, mbits, dPQ, s);
+    case 32: return train_bwd_launch<2>(cw, B, g0, gstride, mbits, dPQ, s);
+    case 48: return train_bwd_launch<3>(cw, B, g0, gstride, mbits, dPQ, s);
+    case 64: return train_bwd_launch<4>(cw, B, g0, gstride, mbits, dPQ, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -235,8 +235,9 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
 // storing the tape (h[l] at h0 + l * hstride, pq) and the ReLU' bits of
 // h[0..L-1] (chain_train_mask_bytes); `pack` holds chain_train_pack_bytes(L)
 // of device-packed weights.  Backward: the update layers' data gradients
-// g[L-1..0] from g[L] (g[l] at g0 + l * gstride), `pack` holding
-// chain_train_bwd_pack_bytes(L) of transposed weights.
+// g[L-1..0] from g[L] (g[l] at g0 + l * gstride), or (dPQ non-NULL) from the
+// readout's dP / dQ, g[L] included; `pack` holds chain_train_bwd_pack_bytes(L)
+// of transposed weights.
 bool chain_train_fused_ok(const GraphW &w, int nx);
 int64_t chain_train_pack_bytes(int layers);
 int64_t chain_train_mask_bytes(int layers, int64_t N);
@@ -244,7 +245,7 @@ int64_t chain_train_bwd_pack_bytes(int layers);
 hipError_t launch_chain_train_fwd_fused(const GraphW &w, const float *nf, int64_t B, int nx, float *fe, float *h0,
                                         int64_t hstride, float *pq, unsigned *mbits, void *pack, hipStream_t s);
 hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, float *g0, int64_t gstride,
-                                        const unsigned *mbits, void *pack, hipStream_t s);
+                                        const unsigned *mbits, void *pack, const float *dPQ, hipStream_t s);
 // The ablation loss's single-step terms and d loss / d flux_edge (train_chain.hip).
 int64_t ablation_loss_ws_bytes(int B, int nx);
 hipError_t launch_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx,

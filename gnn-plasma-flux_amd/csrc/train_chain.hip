@@ -75,6 +75,68 @@ inline unsigned part_reduce_blocks(int64_t I, int64_t J, int64_t nbias) {
   return (unsigned)((I * J + 63) / 64 + (nbias + 63) / 64);
 }
 
+// The same reduction with float4 loads (J % 4 == 0, nbias % 4 == 0, I % 4 ==
+// 0): a block is 32 float4 columns (128 outputs) x 8 split slices; slice q sums
+// splits [qS/8, (q+1)S/8) in order, then the 8 slice sums are added in a fixed
+// tree (deterministic).  1 KiB per wave load instead of 256 B.
+__global__ __launch_bounds__(256) void part_reduce4_kernel(const float *__restrict__ part, int S, int64_t I, int64_t J,
+                                                           float *out, int ish, int64_t ld, int64_t hoff,
+                                                           const float *__restrict__ bias_part, int64_t nbias,
+                                                           float *bias) {
+  __shared__ f4 s_q[8][32];
+  const int c = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int64_t n4 = I * J / 4, wblocks = (n4 + 31) / 32;
+  const bool wb = blockIdx.x < wblocks;
+  const int64_t t = (wb ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - wblocks) * 32 + c;  // float4 index
+  const bool ok = t < (wb ? n4 : (bias ? nbias / 4 : 0));
+  const f4 *src = reinterpret_cast<const f4 *>(wb ? part : bias_part);
+  const int64_t per = wb ? n4 : I / 4;  // float4s per split
+  const int s0 = (int)((int64_t)S * q / 8), s1 = (int)((int64_t)S * (q + 1) / 8);
+  f4 v = f4{0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+#pragma unroll 4
+    for (int sp = s0; sp < s1; ++sp) {
+      const f4 x = src[(int64_t)sp * per + t];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = __fadd_rn(v[e], x[e]);
+    }
+  }
+  s_q[q][c] = v;
+  __syncthreads();
+  if (q == 0 && ok) {
+    f4 r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      r[e] = __fadd_rn(__fadd_rn(__fadd_rn(s_q[0][c][e], s_q[1][c][e]), __fadd_rn(s_q[2][c][e], s_q[3][c][e])),
+                       __fadd_rn(__fadd_rn(s_q[4][c][e], s_q[5][c][e]), __fadd_rn(s_q[6][c][e], s_q[7][c][e])));
+    if (wb) {
+      const int64_t i = 4 * t / J, j = 4 * t - i * J;
+      float *o = out + (i & ((int64_t(1) << ish) - 1)) * ld + (i >> ish) * hoff + j;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = r[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias[4 * t + e] = r[e];
+    }
+  }
+}
+inline unsigned part_reduce4_blocks(int64_t I, int64_t J, int64_t nbias) {
+  return (unsigned)((I * J / 4 + 31) / 32 + (nbias / 4 + 31) / 32);
+}
+// the float4 form where the shapes allow it
+#ifndef HF_PART_REDUCE4
+#define HF_PART_REDUCE4 1
+#endif
+inline void launch_part_reduce(const float *part, int S, int64_t I, int64_t J, float *out, int ish, int64_t ld,
+                               int64_t hoff, const float *bias_part, int64_t nbias, float *bias, hipStream_t s) {
+  if (HF_PART_REDUCE4 && J % 4 == 0 && I % 4 == 0 && nbias % 4 == 0)
+    hipLaunchKernelGGL(part_reduce4_kernel, dim3(part_reduce4_blocks(I, J, nbias)), dim3(256), 0, s, part, S, I, J,
+                       out, ish, ld, hoff, bias_part, nbias, bias);
+  else
+    hipLaunchKernelGGL(part_reduce_kernel, dim3(part_reduce_blocks(I, J, nbias)), dim3(256), 0, s, part, S, I, J, out,
+                       ish, ld, hoff, bias_part, nbias, bias);
+}
+
 // h0[m][o] = ReLU(b_in[o] + sum_c W_in[o][c] nf[m][c])           (src/flux_gnn.py:49)
 // Thread = one row m and 4 consecutive o (H % 4 == 0); F is a template
 // argument so the row and the weights stay in registers.
@@ -598,8 +660,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   hipError_t e;
   auto reduce = [&](int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff, int64_t nbias,
                     float *bias) {
-    hipLaunchKernelGGL(part_reduce_kernel, dim3(part_reduce_blocks(I, J, nbias)), dim3(256), 0, s, part, (int)S, I, J,
-                       out, ish, ld, hoff, bpart, nbias, bias);
+    launch_part_reduce(part, (int)S, I, J, out, ish, ld, hoff, bpart, nbias, bias, s);
     return hipGetLastError();
   };
   // readout: dPQ, dw2, db2                                                          (:62-66)
@@ -620,16 +681,21 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
       return e;
     if ((e = reduce(2 * H, H, const_cast<float *>(g.w_e), hsh, 2LL * H, H, H, const_cast<float *>(g.b_e)))) return e;
   }
-  // dh[L] = [W_a ; W_b]^T dPQ, masked by ReLU'(h[L])
+  // dh[L] = [W_a ; W_b]^T dPQ, masked by ReLU'(h[L]) (fused: the first pass of chain_train_bwd_kernel)
   int cur = 0;
-  {
+#ifndef HF_TRAIN_RO_FOLD
+#define HF_TRAIN_RO_FOLD 1
+#endif
+  const bool fold = fused && HF_TRAIN_RO_FOLD;
+  if (!fold) {
     const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
     const VPlain B{w.w_e, 2LL * H, 2LL * H, hsh, H, H};  // B(r = c, j = k) = [W_a ; W_b][c][k]
     float *gL = fused ? G + L * gstride : dl[cur];
     if ((e = tgemm<VPlain, false, VPlain, true>(A, B, EpiMask{gL, H, t.h[L], H}, N, H, 2 * H, 1, s))) return e;
   }
   // fused: every layer's data gradient in one IC-per-wave pass (chain_train_bwd_kernel)
-  if (fused && (e = launch_chain_train_bwd_fused(w, N / nx, nx, G, gstride, fused_tape(w, N, t).mbits, bpack, s)))
+  if (fused && (e = launch_chain_train_bwd_fused(w, N / nx, nx, G, gstride, fused_tape(w, N, t).mbits, bpack,
+                                                 fold ? dPQ : nullptr, s)))
     return e;
   for (int l = L - 1; l >= 0; --l) {  // update layers, last to first                      (:53-60)
     // dW_l[o][k] = sum_m delta[m][o] [h[l] ; agg h[l]][m][k], db_l = column sums of delta
@@ -662,9 +728,8 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   hipLaunchKernelGGL(input_wgrad_kernel<FF>, dim3((unsigned)nsp), dim3(256), 0, s, d0, nf, H, N, rows, ipart, ipb)
   HF_INPUT_DISPATCH(F, HF_IN_WG)
 #undef HF_IN_WG
-  hipLaunchKernelGGL(part_reduce_kernel, dim3(part_reduce_blocks(H, F, H)), dim3(256), 0, s, ipart, nsp, (int64_t)H,
-                     (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F, (int64_t)0, ipb, (int64_t)H,
-                     const_cast<float *>(g.b_in));
+  launch_part_reduce(ipart, nsp, (int64_t)H, (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F, (int64_t)0,
+                     ipb, (int64_t)H, const_cast<float *>(g.b_in), s);
   if (grad_nf)
     hipLaunchKernelGGL(input_dgrad_kernel, dim3((unsigned)((N * F + 255) / 256)), dim3(256), 0, s, d0, w.w_in, F, H, N,
                        grad_nf);

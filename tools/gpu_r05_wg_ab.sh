@@ -1,6 +1,6 @@
 #!/bin/bash
 # Training tests on the shipped build, its training-step kernel trace, then
-# the A/B against the split-K GEMM weight gradients (HF_WGRAD_DIRECT=0).
+# the A/B against every build/ab/lib_*.so (AB_TAG names the outputs).
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -9,4 +9,4 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py -x -q --timeout
 rc=$?; tail -3 gpurun_out/tr_pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
 bash tools/gpu_train_prof.sh $TAG > gpurun_out/prof_$TAG.out 2>&1 || exit $?
 head -14 gpurun_out/train_kernel_stats_$TAG.md | cut -c1-160
-bash tools/gpu_train_ab.sh wg gnn-plasma-flux_amd/hybridflux/_lib/libhybridflux.so build/ab/lib_gemmwg.so
+bash tools/gpu_train_ab.sh ${AB_TAG:-ab} gnn-plasma-flux_amd/hybridflux/_lib/libhybridflux.so build/ab/lib_*.so
