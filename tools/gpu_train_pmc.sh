@@ -1,8 +1,8 @@
 #!/bin/bash
 # PMC passes over the training bench at B = 2000 (tools/bench_train.py), one
 # counter set per pass: shader clock + MFMA busy; instruction mix / waits; LDS
-# bank conflicts + HBM fetch; HBM write + L2 requests.  Summaries per tgemm
-# variant (forward stencil, data-gradient stencil, weight-gradient split).
+# bank conflicts + HBM fetch; HBM write + L2 requests.  Summaries for the
+# fused forward / backward passes and the weight-gradient GEMM.
 set -o pipefail
 cd "$(dirname "$0")/.."
 TAG=${1:-r05}
@@ -15,12 +15,11 @@ for P in "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES
          "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE FETCH_SIZE" \
          "WRITE_SIZE TCP_TCC_READ_REQ_sum"; do
   i=$((i + 1))
-  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-trace -d gpurun_out/pmc_tr${i}_$TAG -o p -- $B \
+  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-trace -d /tmp/pmc_tr${i}_$TAG -o p -- $B \
     > gpurun_out/pmc_tr${i}_$TAG.log 2>&1 || exit $?
 done
-for K in "VStencil, false, hf::tg::VPlain, false" "VStencil, false, hf::tg::VPlain, true" \
-         "VPlain, true, hf::tg::VStencil, true" "tgemm_kernel"; do
+for K in "chain_train_fwd" "chain_train_bwd" "VPlain, true, hf::tg::VStencil, true" "tgemm_kernel"; do
   echo "== $K"
-  python3 tools/pmc_summary.py "$K" gpurun_out/pmc_tr[1-4]_$TAG/*.db | grep -v dispatch=
+  python3 tools/pmc_summary.py "$K" /tmp/pmc_tr[1-4]_$TAG/*.db | grep -v dispatch=
 done > gpurun_out/pmc_train_$TAG.txt 2>&1
 cat gpurun_out/pmc_train_$TAG.txt
