@@ -252,7 +252,10 @@ __global__ __launch_bounds__(256) void edge_backward_kernel(const float *__restr
 // products as edge_backward_kernel, bit for bit.  dw2 is accumulated per lane
 // half (P lanes the g_f terms, Q lanes the g_b terms) and joined at the end,
 // in a fixed order.
-constexpr int kEbCells = 16;
+#ifndef HF_EB_CELLS
+#define HF_EB_CELLS 8
+#endif
+constexpr int kEbCells = HF_EB_CELLS;  // cells per wave: 8 (47.5 us at B = 2000; 16: 51.0, 32: 51.3; r05_train_small_kernels_ab.txt)
 __device__ __forceinline__ float other_half(float v) {  // v of lane l ^ 32
   const unsigned u = __float_as_uint(v);
   const auto s = __builtin_amdgcn_permlane32_swap(u, u, false, false);
@@ -386,6 +389,50 @@ __global__ __launch_bounds__(256) void input_wgrad_kernel(const float *__restric
       if (c < F) part[((int64_t)blockIdx.x * H + o) * F + c] = v;
       else bpart[(int64_t)blockIdx.x * H + o] = v;
     }
+  }
+}
+
+// The same at H = 128, F = 4 with float4 loads: thread (row lane k = t >> 5,
+// feature quad o4 = t & 31) sums rows m0 + k, m0 + k + 8, ... for features
+// 4 o4 .. +3 (one float4 of d, one of nf per row), then the 8 row lanes are
+// added in order through LDS.
+__global__ __launch_bounds__(256) void input_wgrad_h128f4_kernel(const float *__restrict__ d,
+                                                                 const float *__restrict__ nf, int64_t N,
+                                                                 int64_t rows, float *__restrict__ part,
+                                                                 float *__restrict__ bpart) {
+  constexpr int H = 128, F = 4;
+  __shared__ float s_w[8][H][F + 1];
+  const int k = threadIdx.x >> 5, o4 = threadIdx.x & 31;
+  const int64_t m0 = (int64_t)blockIdx.x * rows;
+  const int64_t m1 = m0 + rows < N ? m0 + rows : N;
+  f4 w[F], bs = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < F; ++c) w[c] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int64_t m = m0 + k; m < m1; m += 8) {
+    const f4 dv = *reinterpret_cast<const f4 *>(d + m * H + 4 * o4);
+    const f4 x = *reinterpret_cast<const f4 *>(nf + m * F);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bs[e] = __fadd_rn(bs[e], dv[e]);
+#pragma unroll
+      for (int c = 0; c < F; ++c) w[c][e] = fmaf(dv[e], x[c], w[c][e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+#pragma unroll
+    for (int c = 0; c < F; ++c) s_w[k][4 * o4 + e][c] = w[c][e];
+    s_w[k][4 * o4 + e][F] = bs[e];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < H * (F + 1); i += 256) {
+    const int o = i / (F + 1), c = i - o * (F + 1);
+    float v = s_w[0][o][c];
+#pragma unroll
+    for (int kk = 1; kk < 8; ++kk) v = __fadd_rn(v, s_w[kk][o][c]);
+    if (c < F) part[((int64_t)blockIdx.x * H + o) * F + c] = v;
+    else bpart[(int64_t)blockIdx.x * H + o] = v;
   }
 }
 
@@ -726,7 +773,13 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   float *ipb = ipart + (int64_t)kInputSplits * H * F;
 #define HF_IN_WG(FF) \
   hipLaunchKernelGGL(input_wgrad_kernel<FF>, dim3((unsigned)nsp), dim3(256), 0, s, d0, nf, H, N, rows, ipart, ipb)
-  HF_INPUT_DISPATCH(F, HF_IN_WG)
+#ifndef HF_INPUT_WGRAD4
+#define HF_INPUT_WGRAD4 1
+#endif
+  if (HF_INPUT_WGRAD4 && H == 128 && F == 4)
+    hipLaunchKernelGGL(input_wgrad_h128f4_kernel, dim3((unsigned)nsp), dim3(256), 0, s, d0, nf, N, rows, ipart, ipb);
+  else
+    HF_INPUT_DISPATCH(F, HF_IN_WG)
 #undef HF_IN_WG
   launch_part_reduce(ipart, nsp, (int64_t)H, (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F, (int64_t)0,
                      ipb, (int64_t)H, const_cast<float *>(g.b_in), s);
