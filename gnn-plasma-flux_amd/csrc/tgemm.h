@@ -25,6 +25,28 @@ typedef float f16 __attribute__((ext_vector_type(16)));
 #ifndef HF_TG_WG
 #define HF_TG_WG 2
 #endif
+// timing diagnostics (CXXFLAGS_EXTRA=-DHF_DIAG_TG_*; results wrong): no stage
+// loads (NOGL), LDS stores (NOLS), stage barriers (NOBAR), partial-tile stores (NOEPI)
+#ifdef HF_DIAG_TG_NOGL
+constexpr bool kDiagNoGl = true;
+#else
+constexpr bool kDiagNoGl = false;
+#endif
+#ifdef HF_DIAG_TG_NOLS
+constexpr bool kDiagNoLs = true;
+#else
+constexpr bool kDiagNoLs = false;
+#endif
+#ifdef HF_DIAG_TG_NOBAR
+constexpr bool kDiagNoBar = true;
+#else
+constexpr bool kDiagNoBar = false;
+#endif
+#ifdef HF_DIAG_TG_NOEPI
+constexpr bool kDiagNoEpi = true;
+#else
+constexpr bool kDiagNoEpi = false;
+#endif
 constexpr int kBM = 128, kBN = 128, kKC = HF_TG_KC;  // reduction chunk per stage (32; 16: a build knob)
 constexpr int kNQ = kBM * kKC / 4 / 256;             // float4 per thread per operand per stage
 constexpr int kIMSh = kKC == 32 ? 3 : 2;             // log2(float4 per [i][r] row)
@@ -73,6 +95,12 @@ struct VPlain {
   __device__ void load2(const Row &w, int c, f4 &a, f4 &) const { a = load4(w, c); }
   __device__ f4 combine(int, const f4 &a, const f4 &) const { return a; }
   bool fits32() const { return rows * ld + cols + (rows >> hshift) * hoff < (int64_t(1) << 31); }
+  // exact GEMMs (tgemm_kernel EX): the row kKC further on, unsplit views only
+  __device__ void adv(Row &w) const { w.off += kKC * (int)ld; }
+  __device__ void load2x(const Row &w, int c, f4 &a, f4 &) const {
+    a = *reinterpret_cast<const f4 *>(p + (unsigned)(w.off + c));
+  }
+  bool exact_ok(int64_t R) const { return hshift >= 62 && R <= rows; }
 };
 constexpr int kNoSplit = 62;
 // [X ; agg X] of X [rows][C] on chains of nx rows: cols [0, C) are X, [C, 2C)
@@ -85,13 +113,29 @@ struct VStencil {
   int C, nx;
   struct Row {
     int self, nxt, prv;  // float offsets of the rows (nxt, prv less C)
+    int i;               // the row's cell on its chain
   };
   __device__ Row row(int64_t r) const {
     r = r < rows ? r : rows - 1;
     const int i = (int)((unsigned)r % (unsigned)nx);
     const int64_t nr = r + (i == nx - 1 ? 1 - nx : 1), pr = r + (i == 0 ? nx - 1 : -1);
-    return Row{(int)(r * C), (int)(nr * C - C), (int)(pr * C - C)};
+    return Row{(int)(r * C), (int)(nr * C - C), (int)(pr * C - C), i};
   }
+  // exact GEMMs: the row kKC further on, its cell stepped instead of divided out
+  __device__ void adv(Row &w) const {
+    const int d = kKC % nx;
+    w.self += kKC * C;
+    w.i += d;
+    w.i -= w.i >= nx ? nx : 0;
+    w.nxt = w.self + (w.i == nx - 1 ? -nx * C : 0);
+    w.prv = w.self + (w.i == 0 ? (nx - 2) * C : -2 * C);
+  }
+  __device__ void load2x(const Row &w, int c, f4 &a, f4 &b) const {
+    const bool self = c < C;
+    a = *reinterpret_cast<const f4 *>(X + (unsigned)((self ? w.self : w.nxt) + c));
+    b = *reinterpret_cast<const f4 *>(X + (unsigned)((self ? w.self : w.prv) + c));
+  }
+  bool exact_ok(int64_t R) const { return R <= rows; }
   // Two-phase: load2 issues two loads (the two neighbour rows, or the row
   // itself twice for c < C: branch-free, the second is an L1 hit), combine forms
   // (a + b) * 0.5 later, when the stage is written to LDS.  The one-call form
@@ -149,7 +193,9 @@ struct EpiPart {
   __device__ float bias_of(int64_t) const { return 0.f; }
   static constexpr bool kPre = false, kBlock = false;
   __device__ float pre(int64_t, int64_t) const { return 0.f; }
-  __device__ void operator()(int64_t i, int64_t j, float v, float, float) const { part[(z * I + i) * J + j] = v; }
+  __device__ void operator()(int64_t i, int64_t j, float v, float, float) const {
+    if (!kDiagNoEpi || v == 1.2345e-30f) part[(z * I + i) * J + j] = v;
+  }
 };
 // out[i][j] = tanh(v + bias[j]) (PureGNN's output_mlp.0, train_pure_gnn.py:74-75)
 struct EpiTanh {
@@ -243,9 +289,14 @@ struct EpiMsg {
 // r = 8g + 4h + s), an [r][i] tile one ds_read_b32 per MFMA at the same r.
 // COLSUM (ARM A only): the split's column sums of GA over its rows (the bias
 // gradient), written to bias_part[split][i] by the blocks of column tile 0.
-template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM>
+// EX (both operands RM; host-checked: whole tiles, R % kKC == 0, R within both
+// views, unsplit views): no clamps or zeroed rows, and each thread's row
+// handles are stepped by kKC per stage instead of recomputed (the stencil's
+// cell index without a division).
+template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM, bool EX = false>
 __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi epi, int64_t I, int64_t J, int64_t R,
                                                        int64_t rsplit, float *bias_part) {
+  static_assert(!EX || (ARM && BRM), "exact form: both operands run along the reduction");
   // (a block epilogue parks a 128 x 65 tile in each operand's two buffers)
   constexpr int kBufF = (Epi::kBlock && 2 * kTileF < kBM * 65) ? (kBM * 65 + 1) / 2 : kTileF;
   __shared__ float sA[2][kBufF];
@@ -302,6 +353,13 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) rowb[q] = gb.row(j0 + ((t + 256 * q) >> kIMSh));
   }
+  if (EX) {  // the first stage's rows; gload steps them
+#pragma unroll
+    for (int q = 0; q < kNQ; ++q) {
+      rowa[q] = ga.row(rb + ((t + 256 * q) >> 5));
+      rowb[q] = gb.row(rb + ((t + 256 * q) >> 5));
+    }
+  }
   // Branch-free loads: addresses clamped by the views; only reduction rows
   // past the split's end (RM operands) are zeroed, by select.  [i][r]
   // operands need R % kKC == 0 (host-checked), so their r never runs past re.
@@ -320,8 +378,15 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
 #pragma unroll
     for (int q = 0; q < kNQ; ++q) {
       const int idx = t + 256 * q;
-      ga.load2(ARM ? ga.row(r0 + (idx >> 5)) : rowa[q], col_a(q, r0), ra[set][q], ra2[LA::kTwo ? set : 0][q]);
-      gb.load2(BRM ? gb.row(r0 + (idx >> 5)) : rowb[q], col_b(q, r0), rbv[set][q], rb2[LB::kTwo ? set : 0][q]);
+      if constexpr (EX) {
+        ga.load2x(rowa[q], col_a(q, r0), ra[set][q], ra2[LA::kTwo ? set : 0][q]);
+        gb.load2x(rowb[q], col_b(q, r0), rbv[set][q], rb2[LB::kTwo ? set : 0][q]);
+        ga.adv(rowa[q]);
+        gb.adv(rowb[q]);
+      } else {
+        ga.load2(ARM ? ga.row(r0 + (idx >> 5)) : rowa[q], col_a(q, r0), ra[set][q], ra2[LA::kTwo ? set : 0][q]);
+        gb.load2(BRM ? gb.row(r0 + (idx >> 5)) : rowb[q], col_b(q, r0), rbv[set][q], rb2[LB::kTwo ? set : 0][q]);
+      }
     }
   };
   auto lstore = [&](int buf, int set, int64_t r0) {
@@ -330,7 +395,7 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
       const int idx = t + 256 * q, im = (1 << kIMSh) - 1;
       f4 va = ga.combine(col_a(q, r0), ra[set][q], ra2[LA::kTwo ? set : 0][q]);
       f4 vb = gb.combine(col_b(q, r0), rbv[set][q], rb2[LB::kTwo ? set : 0][q]);
-      const bool in = r0 + (idx >> 5) < re;
+      const bool in = EX || r0 + (idx >> 5) < re;
       if (ARM) va = f4{in ? va[0] : 0.f, in ? va[1] : 0.f, in ? va[2] : 0.f, in ? va[3] : 0.f};
       if (BRM) vb = f4{in ? vb[0] : 0.f, in ? vb[1] : 0.f, in ? vb[2] : 0.f, in ? vb[3] : 0.f};
       float *pa = ARM ? &sA[buf][(idx >> 5) * kStrRM + 4 * (idx & 31)] : &sA[buf][(idx >> kIMSh) * kStrIM + 4 * (idx & im)];
@@ -350,7 +415,8 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
   auto stage = [&](auto parity, int64_t r0) {
     constexpr int cur = decltype(parity)::value;
     // LDS[cur] holds stage r0; depth 2: register set cur^1 holds (in flight) stage r0 + kKC
-    if (kDepth == 2) {
+    if (kDiagNoGl) {
+    } else if (kDepth == 2) {
       if (r0 + 2 * kKC < re) gload(cur % kDepth, r0 + 2 * kKC);
     } else if (r0 + kKC < re) {
       gload(0, r0 + kKC);
@@ -386,8 +452,8 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
 #pragma unroll
           for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][s], bv[b][s], acc[a][b], 0, 0, 0);
     }
-    if (r0 + kKC < re) lstore(cur ^ 1, (cur ^ 1) % kDepth, r0 + kKC);
-    __syncthreads();
+    if (!kDiagNoLs && r0 + kKC < re) lstore(cur ^ 1, (cur ^ 1) % kDepth, r0 + kKC);
+    if (!kDiagNoBar) __syncthreads();
   };
   for (int64_t r0 = rb; r0 < re;) {
     stage(std::integral_constant<int, 0>{}, r0);
@@ -454,7 +520,11 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
   }
 }
 
-template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM = false>
+#ifndef HF_TG_EXACT
+#define HF_TG_EXACT 1
+#endif
+// EXOK (both operands RM): the exact kernel where the shapes allow it
+template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM = false, bool EXOK = false>
 hipError_t tgemm(const LA &ga, const LB &gb, const Epi &epi, int64_t I, int64_t J, int64_t R, int splits,
                  hipStream_t s, float *bias_part = nullptr) {
   if (I <= 0 || J <= 0) return hipSuccess;
@@ -464,6 +534,13 @@ hipError_t tgemm(const LA &ga, const LB &gb, const Epi &epi, int64_t I, int64_t 
   rsplit = (rsplit + kKC - 1) / kKC * kKC;
   const int64_t S = R > 0 ? (R + rsplit - 1) / rsplit : 1;
   dim3 grid((unsigned)((I + kBM - 1) / kBM), (unsigned)((J + kBN - 1) / kBN), (unsigned)S);
+  if constexpr (EXOK && ARM && BRM) {
+    if (HF_TG_EXACT && R > 0 && I % kBM == 0 && J % kBN == 0 && R % kKC == 0 && ga.exact_ok(R) && gb.exact_ok(R)) {
+      hipLaunchKernelGGL((tgemm_kernel<LA, ARM, LB, BRM, Epi, COLSUM, true>), grid, dim3(256), 0, s, ga, gb, epi, I, J,
+                         R, rsplit, bias_part);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((tgemm_kernel<LA, ARM, LB, BRM, Epi, COLSUM>), grid, dim3(256), 0, s, ga, gb, epi, I, J, R,
                      rsplit > 0 ? rsplit : kKC, bias_part);
   return hipGetLastError();

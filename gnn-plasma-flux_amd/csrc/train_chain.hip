@@ -723,7 +723,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   {
     const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
     const VPlain B{t.h[L], H, N, kNoSplit, 0, H};
-    if ((e = tgemm<VPlain, true, VPlain, true, EpiPart, true>(A, B, EpiPart{part, 2LL * H, H}, 2 * H, H, N,
+    if ((e = tgemm<VPlain, true, VPlain, true, EpiPart, true, true>(A, B, EpiPart{part, 2LL * H, H}, 2 * H, H, N,
                                                                kWgradSplits, s, bpart)))
       return e;
     if ((e = reduce(2 * H, H, const_cast<float *>(g.w_e), hsh, 2LL * H, H, H, const_cast<float *>(g.b_e)))) return e;
@@ -749,7 +749,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
     {
       const VPlain A{fused ? G + (l + 1) * gstride : dl[cur], H, N, kNoSplit, 0, H};
       const VStencil B{t.h[l], N, H, nx};
-      if ((e = tgemm<VPlain, true, VStencil, true, EpiPart, true>(A, B, EpiPart{part, H, 2LL * H}, H, 2 * H, N,
+      if ((e = tgemm<VPlain, true, VStencil, true, EpiPart, true, true>(A, B, EpiPart{part, H, 2LL * H}, H, 2 * H, N,
                                                                   kWgradSplits, s, bpart)))
         return e;
       if ((e = reduce(H, 2 * H, const_cast<float *>(g.w_l + l * g.lsw), kNoSplit, 2LL * H, 0, H,
