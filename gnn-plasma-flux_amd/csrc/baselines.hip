@@ -301,7 +301,10 @@ __device__ __forceinline__ void pinn_layer(const PinnRows<NT> &wrow, const float
     for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(acc[j][i], bq[i]);
     if (ACT == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = tanh_fast(v[i]);
+      for (int i = 0; i < 4; i += 2) {  // packed pairs (bit-identical to tanh_fast)
+        const hf_f2 t = tanh_fast2(hf_f2{v[i], v[i + 1]});
+        v[i] = t.x, v[i + 1] = t.y;
+      }
     } else {
       const f4v st = *reinterpret_cast<const f4v *>(o);
 #pragma unroll
@@ -562,9 +565,17 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
           const float pl = g > 0 ? acc[0][g - 1][i] : dpp_ror(acc[0][NC - 1][i], 0);
           const float pr = g < NC - 1 ? acc[0][g + 1][i] : dpp_ror(acc[0][0][i], 1);
           const float qv = acc[1][g][i];
-          float m = tanh_fast(__fadd_rn(__fadd_rn(pl, qv), bq[i]));
-          m = __fadd_rn(m, tanh_fast(__fadd_rn(__fadd_rn(pr, qv), bq[i])));
-          h[i] = __fadd_rn(h[i], m);
+#ifndef HF_PURE_TANH2
+#define HF_PURE_TANH2 1
+#endif
+          if (HF_PURE_TANH2) {  // the two messages' tanh as packed f32 (bit-identical)
+            const hf_f2 t = tanh_fast2((hf_f2{pl, pr} + qv) + bq[i]);
+            h[i] = __fadd_rn(h[i], __fadd_rn(t.x, t.y));
+          } else {
+            float m = tanh_fast(__fadd_rn(__fadd_rn(pl, qv), bq[i]));
+            m = __fadd_rn(m, tanh_fast(__fadd_rn(__fadd_rn(pr, qv), bq[i])));
+            h[i] = __fadd_rn(h[i], m);
+          }
         }
         *reinterpret_cast<f4v *>(act2 + o) = h;
       }
@@ -587,7 +598,10 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
       for (int g = 0; g < NC; ++g) {
         f4v o;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = tanh_fast(__fadd_rn(acc[0][g][i], bo[i]));
+        for (int i = 0; i < 4; i += 2) {  // packed pairs (bit-identical to tanh_fast)
+          const hf_f2 t = tanh_fast2(hf_f2{acc[0][g][i], acc[0][g][i + 1]} + hf_f2{bo[i], bo[i + 1]});
+          o[i] = t.x, o[i + 1] = t.y;
+        }
         *reinterpret_cast<f4v *>(act2 + ((u * NC + g) * 64 + lane) * 4) = o;
       }
     }

@@ -65,3 +65,25 @@ def test_tanh_fast_accuracy():
             assert err[np.abs(x) >= thr].max() <= (2.0 if eu == ru == 0 else 4.0)  # the exp / rcp branch
     y, _ = _tanh_fast(np.float32([np.nan, np.inf, -np.inf, 40.0, -40.0]))
     assert np.isnan(y[0]) and y[1] == 1 and y[2] == -1 and y[3] == 1 and y[4] == -1
+
+
+def test_tanh_fast2_same_arithmetic():
+    """tanh_fast2 (the packed pair) carries tanh_fast's constants in the same
+    order and the same threshold, so the two are the same f32 arithmetic (the
+    GPU A/B in profiles/r05_puregnn_tanh2_ab.txt found the rollouts bitwise
+    equal)."""
+    with open(HDR) as f:
+        src = f.read()
+    num = r"(-?\d+\.\d+)f"
+
+    def body(sig):
+        b = src[src.index(sig):]
+        return b[:b.index("\n}\n")]
+
+    one, two = body("float tanh_fast(float x)"), body("hf_f2 tanh_fast2(hf_f2 x)")
+    poly1 = re.findall(r"p = (?:__builtin_fmaf\(p, x2, )?" + num, one)
+    poly2 = re.findall(r"p = (?:__builtin_elementwise_fma\(p, x2, )?hf_f2\(" + num, two)
+    assert len(poly1) == 5 and poly2 == poly1
+    assert re.findall(r"ax \* " + num, one) == re.findall(r"ax \* " + num, two)
+    assert re.findall(r"ax < " + num, one) * 2 == re.findall(r"ax\.[xy] < " + num, two)
+    assert set(re.findall(num, one)) == set(re.findall(num, two))

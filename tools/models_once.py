@@ -1,7 +1,8 @@
 """The PureGNN and PINN one-launch rollouts of bench.py's other_models
 (4096 ICs x 64 cells, 30 steps, trajectory recorded), warmed, then one
 rollout each: a short program for rocprofv3 counter passes
-(tools/gpu_models_l2.sh).  Prints each rollout's HIP-event time."""
+(tools/gpu_models_l2.sh).  Prints each rollout's HIP-event time; with a path
+argument, also saves both rollouts there (.npz)."""
 import os
 import sys
 import time
@@ -38,6 +39,13 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         print(f"{name} {e0.elapsed_time(e1):.3f} ms", flush=True)
+    if len(sys.argv) > 1:  # save both rollouts (bitwise A/B of library builds)
+        out = {}
+        for name, r in (("pure_gnn", pg.rollout(ics, K, solver.x)), ("pinn", pn.rollout(ics, K))):
+            for k, v in r.items():
+                if torch.is_tensor(v):
+                    out[f"{name}.{k}"] = v.detach().cpu().numpy()
+        np.savez(sys.argv[1], **out)
 
 
 if __name__ == "__main__":
