@@ -76,14 +76,23 @@ inline unsigned part_reduce_blocks(int64_t I, int64_t J, int64_t nbias) {
 }
 
 // The same reduction with float4 loads (J % 4 == 0, nbias % 4 == 0, I % 4 ==
-// 0): a block is 32 float4 columns (128 outputs) x 8 split slices; slice q sums
-// splits [qS/8, (q+1)S/8) in order, then the 8 slice sums are added in a fixed
-// tree (deterministic).  1 KiB per wave load instead of 256 B.
-__global__ __launch_bounds__(256) void part_reduce4_kernel(const float *__restrict__ part, int S, int64_t I, int64_t J,
-                                                           float *out, int ish, int64_t ld, int64_t hoff,
-                                                           const float *__restrict__ bias_part, int64_t nbias,
-                                                           float *bias) {
-  __shared__ f4 s_q[8][32];
+// 0): a block is 32 float4 columns (128 outputs) x kPrSlices split slices;
+// slice q sums splits [qS/SL, (q+1)S/SL) in order, then the slice sums are
+// added in a fixed pairwise tree (deterministic).  1 KiB per wave load
+// instead of 256 B.
+#ifndef HF_PR_SLICES
+#define HF_PR_SLICES 16
+#endif
+#ifndef HF_PR_UNROLL
+#define HF_PR_UNROLL 4
+#endif
+constexpr int kPrSlices = HF_PR_SLICES;
+static_assert(kPrSlices == 8 || kPrSlices == 16, "slices: a power of two, 32 x slices threads");
+__global__ __launch_bounds__(32 * kPrSlices) void part_reduce4_kernel(const float *__restrict__ part, int S, int64_t I,
+                                                                      int64_t J, float *out, int ish, int64_t ld,
+                                                                      int64_t hoff, const float *__restrict__ bias_part,
+                                                                      int64_t nbias, float *bias) {
+  __shared__ f4 s_q[kPrSlices][32];
   const int c = threadIdx.x & 31, q = threadIdx.x >> 5;
   const int64_t n4 = I * J / 4, wblocks = (n4 + 31) / 32;
   const bool wb = blockIdx.x < wblocks;
@@ -91,10 +100,10 @@ __global__ __launch_bounds__(256) void part_reduce4_kernel(const float *__restri
   const bool ok = t < (wb ? n4 : (bias ? nbias / 4 : 0));
   const f4 *src = reinterpret_cast<const f4 *>(wb ? part : bias_part);
   const int64_t per = wb ? n4 : I / 4;  // float4s per split
-  const int s0 = (int)((int64_t)S * q / 8), s1 = (int)((int64_t)S * (q + 1) / 8);
+  const int s0 = (int)((int64_t)S * q / kPrSlices), s1 = (int)((int64_t)S * (q + 1) / kPrSlices);
   f4 v = f4{0.f, 0.f, 0.f, 0.f};
   if (ok) {
-#pragma unroll 4
+#pragma unroll HF_PR_UNROLL
     for (int sp = s0; sp < s1; ++sp) {
       const f4 x = src[(int64_t)sp * per + t];
 #pragma unroll
@@ -104,19 +113,23 @@ __global__ __launch_bounds__(256) void part_reduce4_kernel(const float *__restri
   s_q[q][c] = v;
   __syncthreads();
   if (q == 0 && ok) {
-    f4 r;
+    f4 r[kPrSlices];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      r[e] = __fadd_rn(__fadd_rn(__fadd_rn(s_q[0][c][e], s_q[1][c][e]), __fadd_rn(s_q[2][c][e], s_q[3][c][e])),
-                       __fadd_rn(__fadd_rn(s_q[4][c][e], s_q[5][c][e]), __fadd_rn(s_q[6][c][e], s_q[7][c][e])));
+    for (int k = 0; k < kPrSlices; ++k) r[k] = s_q[k][c];
+#pragma unroll
+    for (int w = kPrSlices / 2; w >= 1; w /= 2)  // ((0 + 1) + (2 + 3)) + ...
+#pragma unroll
+      for (int k = 0; k < w; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[k][e] = __fadd_rn(r[2 * k][e], r[2 * k + 1][e]);
     if (wb) {
       const int64_t i = 4 * t / J, j = 4 * t - i * J;
       float *o = out + (i & ((int64_t(1) << ish) - 1)) * ld + (i >> ish) * hoff + j;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = r[e];
+      for (int e = 0; e < 4; ++e) o[e] = r[0][e];
     } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bias[4 * t + e] = r[e];
+      for (int e = 0; e < 4; ++e) bias[4 * t + e] = r[0][e];
     }
   }
 }
@@ -130,7 +143,7 @@ inline unsigned part_reduce4_blocks(int64_t I, int64_t J, int64_t nbias) {
 inline void launch_part_reduce(const float *part, int S, int64_t I, int64_t J, float *out, int ish, int64_t ld,
                                int64_t hoff, const float *bias_part, int64_t nbias, float *bias, hipStream_t s) {
   if (HF_PART_REDUCE4 && J % 4 == 0 && I % 4 == 0 && nbias % 4 == 0)
-    hipLaunchKernelGGL(part_reduce4_kernel, dim3(part_reduce4_blocks(I, J, nbias)), dim3(256), 0, s, part, S, I, J,
+    hipLaunchKernelGGL(part_reduce4_kernel, dim3(part_reduce4_blocks(I, J, nbias)), dim3(32 * kPrSlices), 0, s, part, S, I, J,
                        out, ish, ld, hoff, bias_part, nbias, bias);
   else
     hipLaunchKernelGGL(part_reduce_kernel, dim3(part_reduce_blocks(I, J, nbias)), dim3(256), 0, s, part, S, I, J, out,
