@@ -274,7 +274,7 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
         progress(f"training line: {mode}")
         graphed = mode == "graphed"
         torch.manual_seed(0)
-        m = FluxGNN(4, 128, 4).to(dev)
+        m = FluxGNN(4, 128, 4).to(dev).flatten_parameters_()
         # graphed: the fused Adam kernel in its capturable form (the multi-tensor
         # capturable Adam costs ~60 us more per step inside the graph)
         opt = (torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=graphed) if mode != "eager" else

@@ -468,6 +468,18 @@ int hf_ablation_loss(const float *fe, const float *st, const float *ft, const fl
   return HF_OK;
 }
 
+int hf_chain_batch_gather(const int64_t *idx, int B, const float *st_all, const float *ft_all, const float *sn_all,
+                          int64_t N, int nx, const float *x, float *st, float *ft, float *sn, float *nf,
+                          void *stream) {
+  if (B < 0 || nx < 1 || N < 1) return fail(HF_EINVAL, "hf_chain_batch_gather: need B >= 0, nx >= 1, N >= 1");
+  if (B > 0 && (!idx || !st_all || !ft_all || !sn_all || !x || !st || !ft || !sn || !nf))
+    return fail(HF_EINVAL, "hf_chain_batch_gather: NULL pointer");
+  HF_CHECK_HIP(hf::launch_chain_batch_gather(idx, B, st_all, ft_all, sn_all, N, nx, x, st, ft, sn, nf,
+                                             as_stream(stream)),
+               "hf_chain_batch_gather");
+  return HF_OK;
+}
+
 // ------------------------------------------------------- PureGNN / PINN
 int64_t hf_pure_gnn_param_count(int in_dim, int hidden, int layers) {
   if (in_dim < 1 || hidden < 1 || layers < 0) return -1;

@@ -251,6 +251,10 @@ int64_t ablation_loss_ws_bytes(int B, int nx);
 hipError_t launch_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx,
                                 float c, float dx, const float *lam, const double *pc, float *loss, float *flux_loss,
                                 float *dfe, void *ws, hipStream_t s);
+// The trainer's batch gather + chain node features (train_chain.hip).
+hipError_t launch_chain_batch_gather(const int64_t *idx, int B, const float *st_all, const float *ft_all,
+                                     const float *sn_all, int64_t N, int nx, const float *x, float *st, float *ft,
+                                     float *sn, float *nf, hipStream_t s);
 hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei,
                              int64_t E, float *flux, void *ws, hipStream_t s);
 

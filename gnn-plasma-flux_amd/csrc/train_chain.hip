@@ -823,4 +823,40 @@ hipError_t launch_ablation_loss(const float *fe, const float *st, const float *f
   return hipGetLastError();
 }
 
+// The trainer's batch (train_ablation.py:27-44 FluxDataset indexed by a
+// DataLoader batch) and its chain node features [n, u, E, x]
+// (src/graph_constructor.py:6-39 build_chain_graph, batched) in one pass: one
+// thread per (sample, cell).  Indices wrap once from the end (as torch
+// indexing) and are clamped to [0, N) beyond that (a device index cannot raise).
+__global__ __launch_bounds__(256) void chain_batch_gather_kernel(const int64_t *__restrict__ idx, int B,
+                                                                 const float *__restrict__ st_all,
+                                                                 const float *__restrict__ ft_all,
+                                                                 const float *__restrict__ sn_all, int64_t N, int nx,
+                                                                 const float *__restrict__ x, float *st, float *ft,
+                                                                 float *sn, float *nf) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)B * nx) return;
+  const int64_t b = t / nx;
+  const int i = (int)(t - b * nx);
+  int64_t r = idx[b];
+  r = r < 0 ? r + N : r;
+  r = r < 0 ? 0 : (r >= N ? N - 1 : r);
+  const float *ps = st_all + r * 3 * nx + i, *pn = sn_all + r * 3 * nx + i;
+  const float n = ps[0], u = ps[nx], E = ps[2 * nx];
+  float *os = st + b * 3 * nx + i, *on = sn + b * 3 * nx + i;
+  os[0] = n, os[nx] = u, os[2 * nx] = E;
+  on[0] = pn[0], on[nx] = pn[nx], on[2 * nx] = pn[2 * nx];
+  ft[b * nx + i] = ft_all[r * nx + i];
+  *reinterpret_cast<f4 *>(nf + 4 * t) = f4{n, u, E, x[i]};
+}
+
+hipError_t launch_chain_batch_gather(const int64_t *idx, int B, const float *st_all, const float *ft_all,
+                                     const float *sn_all, int64_t N, int nx, const float *x, float *st, float *ft,
+                                     float *sn, float *nf, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(chain_batch_gather_kernel, dim3((unsigned)(((int64_t)B * nx + 255) / 256)), dim3(256), 0, s, idx,
+                     B, st_all, ft_all, sn_all, N, nx, x, st, ft, sn, nf);
+  return hipGetLastError();
+}
+
 }  // namespace hf

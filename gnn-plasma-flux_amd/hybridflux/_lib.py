@@ -90,6 +90,8 @@ SIGNATURES = {
     "hf_ablation_loss_workspace_bytes": (c_int64, [c_int, c_int]),
     "hf_ablation_loss": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "hf_chain_batch_gather": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -426,6 +426,36 @@ def rollout_summary(metrics, mse=None, metrics_ref=None, drift=False):
     return summ, dr
 
 
+def chain_batch(idx, state_t, flux_t, state_next, x):
+    """hf_chain_batch_gather: a training batch of a device dataset
+    (train_ablation.py:27-44, indexed by the batch) and its chain node
+    features [n, u, E, x] (src/graph_constructor.py:6-39, batched) in one pass.
+    idx [B] sample indices; state_t / state_next [N,3,nx], flux_t [N,nx]
+    float32 device tensors; x [nx].  Returns (st [B,3,nx], ft [B,nx],
+    sn [B,3,nx], node_features [B*nx,4])."""
+    for t, what in ((state_t, "state_t"), (flux_t, "flux_t"), (state_next, "state_next")):
+        require_device(t, what)
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"chain batch: {what} must be a contiguous float32 tensor")
+    N, _, nx = state_t.shape
+    dev = state_t.device
+    if state_next.shape != state_t.shape or flux_t.shape != (N, nx):
+        raise ValueError("chain batch: dataset shapes must be state [N,3,nx], flux_t [N,nx]")
+    idx = torch.as_tensor(idx, device=dev).to(torch.long).reshape(-1).contiguous()
+    x = torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1).contiguous()
+    if x.numel() != nx:
+        raise ValueError("chain batch: x must hold nx positions")
+    B = idx.numel()
+    st = torch.empty(B, 3, nx, device=dev)
+    ft = torch.empty(B, nx, device=dev)
+    sn = torch.empty(B, 3, nx, device=dev)
+    nf = torch.empty(B * nx, 4, device=dev)
+    with torch.cuda.device(dev):
+        check(lib().hf_chain_batch_gather(ptr(idx), B, ptr(state_t), ptr(flux_t), ptr(state_next), N, nx, ptr(x),
+                                          ptr(st), ptr(ft), ptr(sn), ptr(nf), stream_of(dev)))
+    return st, ft, sn, nf
+
+
 def ablation_loss_terms(grid, flux_edge, st, ft, sn, lam):
     """hf_ablation_loss: the single-step terms of the reference trainer's loss
     (scripts/training/train_ablation.py:120-170) for B samples.  flux_edge

@@ -34,13 +34,29 @@ from . import engine
 from .graph_constructor import chain_edge_index, chain_tag
 
 
+def _flat_view(params, dev):
+    """The parameters as one flat float32 tensor, without a copy, when they are
+    consecutive contiguous pieces of one device buffer (after
+    FluxGNN.flatten_parameters_); otherwise None."""
+    p0 = params[0]
+    base, off, n = p0.untyped_storage().data_ptr(), p0.storage_offset(), 0
+    for q in params:
+        if (q.device != dev or q.dtype != torch.float32 or not q.is_contiguous()
+                or q.untyped_storage().data_ptr() != base or q.storage_offset() != off + n):
+            return None
+        n += q.numel()
+    return p0.detach().as_strided((n,), (1,), off)
+
+
 class _TrainForward(torch.autograd.Function):
     """FluxGNN.forward with HIP backward kernels (parameter order = state dict)."""
 
     @staticmethod
     def forward(ctx, node_features, edge_index, dims, *params):
         dev = engine.compute_device(node_features, "node_features")
-        flat = torch.cat([q.detach().reshape(-1).to(device=dev, dtype=torch.float32) for q in params])
+        flat = _flat_view(params, dev)
+        if flat is None:
+            flat = torch.cat([q.detach().reshape(-1).to(device=dev, dtype=torch.float32) for q in params])
         flux, tape, nf, ei, chain_nx = engine.graph_forward_train(flat, dims, node_features.detach().to(dev),
                                                                   edge_index)
         ctx.save_for_backward(flat, tape, nf, ei)
@@ -101,6 +117,24 @@ class FluxGNN(nn.Module):
             sd = {k: v for k, v in self.state_dict().items()}
             self._packed[key] = (sig, engine.DeviceModel(sd, device, self.precision))
         return self._packed[key][1]
+
+    def flatten_parameters_(self):
+        """Re-home every parameter into one contiguous float32 buffer in
+        state-dict order (the parameters keep their identity, so an optimizer
+        made before still holds them): the training forward then hands the
+        kernels that buffer instead of concatenating the parameters each step.
+        .to() / .cuda() afterwards undo it (the forward falls back to the copy)."""
+        params = list(self.parameters())
+        flat = torch.cat([q.detach().reshape(-1).to(torch.float32) for q in params])
+        o = 0
+        with torch.no_grad():
+            for q in params:
+                q.data = flat[o:o + q.numel()].view(q.shape)
+                o += q.numel()
+        for _, (_, dm) in list(self._packed.items()):
+            dm.close()
+        self._packed = {}
+        return self
 
     def _apply(self, fn, *args, **kwargs):  # .to()/.cuda() invalidate packed copies
         out = super()._apply(fn, *args, **kwargs)

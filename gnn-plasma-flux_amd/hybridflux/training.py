@@ -30,7 +30,7 @@ from . import engine
 from .baseline_solver import BaselineSolver
 from .config import ABLATION_CONFIGS, MODEL_CONFIG
 from .flux_gnn import FluxGNN
-from .graph_constructor import build_chain_graph_batch
+from .graph_constructor import build_chain_graph_batch, chain_edge_index
 
 
 def _mse(a, b):
@@ -60,16 +60,20 @@ class _StepLoss(torch.autograd.Function):
         return dfe * g_loss, None, None, None, None, None
 
 
-def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0, fused=True):
+def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0, fused=True, nf=None):
     """Loss of train_ablation.py:107-200 for a batch: st, st_next [B,3,nx], ft [B,nx]
     on the device.  Returns (loss, flux_loss); B=1 is the reference formula.
     fused: the single-step terms (:124-170) in one HIP pass (hf_ablation_loss)
     instead of the torch expressions below (kept as the readable statement of
-    the same arithmetic, and for the comparison test)."""
+    the same arithmetic, and for the comparison test).  nf: the batch's chain
+    node features when the caller has them (FluxDataset.batch with x)."""
     B, _, nx = st.shape
     n_t, u_t = st[:, 0], st[:, 1]
     n_next_true, u_next_true, E_next_true = st_next[:, 0], st_next[:, 1], st_next[:, 2]
-    nf, ei = build_chain_graph_batch(st, x)
+    if nf is None:
+        nf, ei = build_chain_graph_batch(st, x)
+    else:
+        ei = chain_edge_index(nx, B, st.device)
     flux_edge = model(nf, ei).reshape(B, 2 * nx)
     if fused and n0 == 1.0 and abs(dt / dx - grid.dt / grid.dx) <= 1e-12 * abs(dt / dx):
         lam = (cfg["lambda_state"], cfg["lambda_poisson"], cfg["lambda_charge"], cfg["lambda_energy_one"])
@@ -129,8 +133,13 @@ class FluxDataset:
     def __len__(self):
         return self.N
 
-    def batch(self, idx):
-        return self.state_t[idx], self.flux_t[idx], self.state_next[idx]
+    def batch(self, idx, x=None):
+        """(state_t, flux_t, state_next)[idx]; with x (the grid positions [nx])
+        also the batch's chain node features, all four from one HIP pass
+        (engine.chain_batch): (st, ft, sn, node_features)."""
+        if x is None:
+            return self.state_t[idx], self.flux_t[idx], self.state_next[idx]
+        return engine.chain_batch(idx, self.state_t, self.flux_t, self.state_next, x)
 
 
 class GraphedStep:
@@ -153,8 +162,8 @@ class GraphedStep:
 
     def _body(self):
         model, opt, data, x, dt, dx, cfg, grid = self.args
-        st, ft, sn = data.batch(self.idx)
-        loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid)
+        st, ft, sn, nf = data.batch(self.idx, x)
+        loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid, nf=nf)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
@@ -200,8 +209,8 @@ def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid, graph
             else:
                 loss, flux_loss = graphed(idx)
         else:
-            st, ft, sn = data.batch(idx)
-            loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid)
+            st, ft, sn, nf = data.batch(idx, x)
+            loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid, nf=nf)
             opt.zero_grad()
             loss.backward()
             opt.step()
@@ -227,6 +236,7 @@ def train_model(state_t, flux_t, state_next, x, dt, dx, nu, config_name, stencil
     grid = BaselineSolver(nx=data.nx, dt=dt, nu=nu, device=device).grid
     x_dev = torch.as_tensor(np.asarray(x, dtype=np.float32), device=device)
     model = FluxGNN(MODEL_CONFIG["input_dim"], MODEL_CONFIG["hidden_dim"], MODEL_CONFIG["num_layers"]).to(device)
+    model.flatten_parameters_()  # one parameter buffer: no per-step concat in the training forward
     opt = torch.optim.Adam(model.parameters(), lr=lr)
     gen = torch.Generator().manual_seed(0 if seed is None else seed)
     history = {"epoch": [], "loss": [], "flux_loss": [], "seconds": []}
@@ -244,7 +254,8 @@ def train_model(state_t, flux_t, state_next, x, dt, dx, nu, config_name, stencil
             log(f"[Epoch {epoch}/{epochs}] Loss: {history['loss'][-1]:.6e}, Flux: {history['flux_loss'][-1]:.6e}")
     if save_dir is not None:
         os.makedirs(save_dir, exist_ok=True)
-        torch.save(model.state_dict(), os.path.join(save_dir, f"hybrid_{config_name}_r{stencil_radius}.pt"))
+        # (cloned: one storage per tensor, as the reference's checkpoints, not views of the flat buffer)
+        torch.save({k: v.clone() for k, v in model.state_dict().items()}, os.path.join(save_dir, f"hybrid_{config_name}_r{stencil_radius}.pt"))
         with open(os.path.join(save_dir, f"history_{config_name}_r{stencil_radius}.json"), "w") as f:
             json.dump(history, f, indent=2)
     return model, history

@@ -182,6 +182,22 @@ int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const
                      void *dev_workspace, int64_t workspace_bytes, void *stream);
 
 /*
+ * Replaces: one training batch of the reference trainer (its dataset of
+ * (state_t, flux_t, state_next) triples indexed by a DataLoader batch,
+ * scripts/training/train_ablation.py:27-44) and the batch's chain node
+ * features (src/graph_constructor.py:6-39 build_chain_graph: [n, u, E, x] per
+ * cell, batched), in one pass.  dev_idx [B] int64 sample indices (negative
+ * ones wrap once, as torch indexing; beyond [-N, N) they are clamped);
+ * dataset dev_state_t_all / dev_state_next_all [N][3][nx], dev_flux_t_all
+ * [N][nx]; dev_x [nx].  Writes dev_state_t / dev_state_next [B][3][nx],
+ * dev_flux_t [B][nx], dev_node_features [B*nx][4].
+ */
+int hf_chain_batch_gather(const int64_t *dev_idx, int B, const float *dev_state_t_all,
+                          const float *dev_flux_t_all, const float *dev_state_next_all, int64_t N, int nx,
+                          const float *dev_x, float *dev_state_t, float *dev_flux_t, float *dev_state_next,
+                          float *dev_node_features, void *stream);
+
+/*
  * The reference's other rollout models, inference.
  * dev_params: every parameter, float32, state-dict order, on the device.
  *

@@ -368,3 +368,51 @@ def test_fused_step_loss_equals_torch_terms(hf, cfg_name):
     assert abs(out[0][1] - out[1][1]) <= 2e-6 * abs(out[1][1])
     for k in out[0][2]:
         grads_close(out[0][2][k], out[1][2][k], 1e-5)
+
+
+def test_chain_batch_gather_equals_indexing(hf):
+    """hf_chain_batch_gather (FluxDataset.batch with x: the batch and its chain
+    node features in one pass) equals torch indexing + build_chain_graph_batch
+    bit for bit, negative indices included (train_ablation.py:27-44,
+    src/graph_constructor.py:6-39)."""
+    from hybridflux.training import FluxDataset
+    g = torch.Generator().manual_seed(3)
+    N, nx, B = 37, 64, 300
+    st, sn = torch.randn(N, 3, nx, generator=g), torch.randn(N, 3, nx, generator=g)
+    ft = torch.randn(N, nx, generator=g)
+    data = FluxDataset(st.numpy(), ft.numpy(), sn.numpy(), DEV)
+    idx = torch.randint(-N, N, (B,), generator=g).to(DEV)
+    x = torch.linspace(0, 2 * np.pi, nx + 1)[:-1].to(DEV)
+    st_b, ft_b, sn_b, nf = data.batch(idx, x)
+    ref = data.batch(idx)
+    for a, b in zip((st_b, ft_b, sn_b), ref):
+        assert torch.equal(a, b)
+    nf_ref, _ = hf.build_chain_graph_batch(ref[0], x)
+    assert torch.equal(nf, nf_ref)
+    e = data.batch(idx[:0], x)
+    assert e[0].shape == (0, 3, nx) and e[3].shape == (0, 4)
+
+
+def test_flattened_parameters_same_step(hf):
+    """FluxGNN.flatten_parameters_ (one parameter buffer, no per-step concat)
+    changes nothing: the same flux, gradients and Adam update bit for bit."""
+    import copy
+    torch.manual_seed(4)
+    a = hf.FluxGNN(4, 128, 4).to(DEV)
+    b = copy.deepcopy(a).flatten_parameters_()
+    assert hf.flux_gnn._flat_view(list(b.parameters()), torch.device(DEV)) is not None
+    assert hf.flux_gnn._flat_view(list(a.parameters()), torch.device(DEV)) is None
+    st = torch.randn(6, 3, 64, device=DEV)
+    x = torch.linspace(0, 2 * np.pi, 65, device=DEV)[:-1]
+    out = []
+    for m in (a, b):
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        nf, ei = hf.build_chain_graph_batch(st, x)
+        fl = m(nf, ei)
+        (fl ** 2).sum().backward()
+        grads = [q.grad.clone() for q in m.parameters()]
+        opt.step()
+        out.append((fl.detach(), grads, [q.detach().clone() for q in m.parameters()]))
+    assert torch.equal(out[0][0], out[1][0])
+    for u, v in zip(out[0][1] + out[0][2], out[1][1] + out[1][2]):
+        assert torch.equal(u, v)

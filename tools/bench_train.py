@@ -50,6 +50,8 @@ def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False,
     from hybridflux.training import GraphedStep, train_steps
     torch.manual_seed(0)
     m = hf.FluxGNN(4, 128, 4).to("cuda")
+    if not os.environ.get("HF_AB_NO_FLAT"):  # A/B switch: the per-step parameter concat
+        m.flatten_parameters_()
     opt = (torch.optim.Adam(m.parameters(), lr=1e-3, fused=True) if fused_adam else
            torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True, fused=True) if graphed else
            torch.optim.Adam(m.parameters(), lr=1e-3))
@@ -105,6 +107,10 @@ def main():
     ap.add_argument("--warm-s", type=float, default=0.3, help="seconds of the timed workload run before timing it")
     ap.add_argument("--cpu-samples", type=int, default=100)
     args = ap.parse_args()
+    if os.environ.get("HF_AB_PLAIN_BATCH"):  # A/B switch: torch indexing + build_chain_graph_batch per step
+        from hybridflux import training as T
+        _batch = T.FluxDataset.batch
+        T.FluxDataset.batch = lambda self, idx, x=None: (*_batch(self, idx), None)
     import hybridflux as hf
     from hybridflux.datagen import generate_dataset
     from hybridflux.training import FluxDataset
