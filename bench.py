@@ -249,15 +249,16 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
     the reference dataset recipe (DATASET_CONFIG: 50 ICs x 40 steps, nx = 64,
     generated on the GPU by hybridflux.datagen), FluxGNN(4,128,4) random-init
     (torch.manual_seed(0)).  Eager with torch's default (multi-tensor) Adam,
-    eager with its single-kernel fused=True Adam (the same update), and
-    replaying the captured step (hybridflux.training.GraphedStep, fused
-    capturable Adam); each warmed for warm_s, then `steps`
+    eager with its single-kernel fused=True Adam (the same update), replaying
+    the captured step (hybridflux.training.GraphedStep, fused capturable
+    Adam), and eager / replayed with hybridflux's FlatAdam (the same update in
+    one launch over the parameter buffer); each warmed for warm_s, then `steps`
     steps timed with HIP events + the wall clock.  FLOPs per sample: FluxGNN
     forward + backward (tools/bench_train.py flop_per_sample); the loss terms,
     FV updates and Adam are inside the timed step but not counted."""
     from hybridflux import ABLATION_CONFIGS, BaselineSolver, FluxGNN
     from hybridflux.datagen import generate_dataset
-    from hybridflux.training import FluxDataset, GraphedStep, train_steps
+    from hybridflux.training import FlatAdam, FluxDataset, GraphedStep, train_steps
     from tools.bench_train import flop_per_sample
     st, ft, sn, x, dt, dx, nu = generate_dataset(out_path=None, device=dev, num_initial_conditions=50,
                                                  steps_per_ic=40)
@@ -270,14 +271,16 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
            "batch": batch, "steps": steps, "flop_per_sample": fps,
            "dataset": "DATASET_CONFIG recipe: 50 ICs x 40 steps, nx=64 (GPU classical rollout)"}
     best = None
-    for mode in ("eager", "eager_fused_adam", "graphed"):
+    for mode in ("eager", "eager_fused_adam", "graphed", "eager_flat_adam", "graphed_flat_adam"):
         progress(f"training line: {mode}")
-        graphed = mode == "graphed"
+        graphed = mode.startswith("graphed")
         torch.manual_seed(0)
         m = FluxGNN(4, 128, 4).to(dev).flatten_parameters_()
         # graphed: the fused Adam kernel in its capturable form (the multi-tensor
-        # capturable Adam costs ~60 us more per step inside the graph)
-        opt = (torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=graphed) if mode != "eager" else
+        # capturable Adam costs ~60 us more per step inside the graph); *_flat_adam:
+        # the same update in one HIP launch over the parameter buffer (FlatAdam)
+        opt = (FlatAdam(m.parameters(), lr=1e-3) if mode.endswith("flat_adam") else
+               torch.optim.Adam(m.parameters(), lr=1e-3, fused=True, capturable=graphed) if mode != "eager" else
                torch.optim.Adam(m.parameters(), lr=1e-3))
         gs = GraphedStep(m, opt, data, batch, x_dev, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
         gen = torch.Generator().manual_seed(1)

@@ -480,6 +480,18 @@ int hf_chain_batch_gather(const int64_t *idx, int B, const float *st_all, const 
   return HF_OK;
 }
 
+int hf_adam_flat(float *params, const float *grads, float *exp_avg, float *exp_avg_sq, int64_t n, float *step,
+                 unsigned *done, float lr, float beta1, float beta2, float eps, void *stream) {
+  if (n < 0) return fail(HF_EINVAL, "hf_adam_flat: n < 0");
+  if (n > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !step || !done))
+    return fail(HF_EINVAL, "hf_adam_flat: NULL pointer");
+  if (n == 0) return HF_OK;
+  HF_CHECK_HIP(hf::launch_adam_flat(params, grads, exp_avg, exp_avg_sq, n, step, done, lr, beta1, beta2, eps,
+                                    as_stream(stream)),
+               "hf_adam_flat");
+  return HF_OK;
+}
+
 // ------------------------------------------------------- PureGNN / PINN
 int64_t hf_pure_gnn_param_count(int in_dim, int hidden, int layers) {
   if (in_dim < 1 || hidden < 1 || layers < 0) return -1;

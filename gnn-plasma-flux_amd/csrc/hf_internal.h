@@ -255,6 +255,9 @@ hipError_t launch_ablation_loss(const float *fe, const float *st, const float *f
 hipError_t launch_chain_batch_gather(const int64_t *idx, int B, const float *st_all, const float *ft_all,
                                      const float *sn_all, int64_t N, int nx, const float *x, float *st, float *ft,
                                      float *sn, float *nf, hipStream_t s);
+// Adam over one flat parameter buffer, step count on the device (train_chain.hip).
+hipError_t launch_adam_flat(float *p, const float *g, float *m, float *v, int64_t n, float *step, unsigned *done,
+                            float lr, float b1, float b2, float eps, hipStream_t s);
 hipError_t launch_graph_flux(const GraphW &w, const float *nf, int64_t N, const int64_t *ei,
                              int64_t E, float *flux, void *ws, hipStream_t s);
 

@@ -859,4 +859,47 @@ hipError_t launch_chain_batch_gather(const int64_t *idx, int B, const float *st_
   return hipGetLastError();
 }
 
+// torch.optim.Adam's update (no weight decay, no amsgrad; the arithmetic of
+// torch's fused Adam functor) over one flat parameter buffer: the training
+// step's optimizer (train_ablation.py:208-209) in one launch wide enough to
+// stream the buffer, instead of a multi-tensor launch of a few workgroups.
+// The step count lives on the device (capturable): every workgroup reads it
+// first, and the last workgroup to finish (a done-counter it resets) stores
+// the incremented count.
+__global__ __launch_bounds__(256) void adam_flat_kernel(float *__restrict__ p, const float *__restrict__ g,
+                                                        float *__restrict__ m, float *__restrict__ v, int64_t n,
+                                                        float *step, unsigned *done, float lr, float b1, float b2,
+                                                        float eps) {
+  const float s = step[0] + 1.0f;
+  const float bc1 = (float)(1.0 - pow((double)b1, (double)s));
+  const float bc2s = (float)sqrt(1.0 - pow((double)b2, (double)s));
+  const float step_size = lr / bc1, c1 = 1.0f - b1, c2 = 1.0f - b2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = g[i];
+    const float mi = b1 * m[i] + c1 * gi;
+    const float vi = b2 * v[i] + c2 * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    p[i] = p[i] - step_size * mi / denom;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(done, 1u) == gridDim.x - 1) {
+      step[0] = s;
+      done[0] = 0u;
+      __threadfence();
+    }
+  }
+}
+
+hipError_t launch_adam_flat(float *p, const float *g, float *m, float *v, int64_t n, float *step, unsigned *done,
+                            float lr, float b1, float b2, float eps, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n + 1023) / 1024, 1), 2048);
+  hipLaunchKernelGGL(adam_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, g, m, v, n, step, done, lr, b1, b2,
+                     eps);
+  return hipGetLastError();
+}
+
 }  // namespace hf

@@ -92,6 +92,8 @@ SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "hf_chain_batch_gather": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hf_adam_flat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_float, c_float,
+                             c_float, c_float, c_void_p]),
 }
 
 _lib = None

@@ -456,6 +456,27 @@ def chain_batch(idx, state_t, flux_t, state_next, x):
     return st, ft, sn, nf
 
 
+def adam_flat(params, grads, exp_avg, exp_avg_sq, step, done, lr, beta1, beta2, eps):
+    """hf_adam_flat: torch.optim.Adam's update on one flat float32 parameter
+    buffer (train_ablation.py:208-209), the step count `step` (float32 [1]) on
+    the device and incremented by the call; `done` a uint32-sized zeroed
+    buffer the kernel leaves zero."""
+    for t, what in ((params, "params"), (grads, "grads"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq"),
+                    (step, "step"), (done, "done")):
+        require_device(t, what)
+        if not t.is_contiguous():
+            raise ValueError(f"adam_flat: {what} must be contiguous")
+    n = params.numel()
+    if any(t.numel() != n or t.dtype != torch.float32 for t in (grads, exp_avg, exp_avg_sq)) or \
+            params.dtype != torch.float32 or step.dtype != torch.float32 or step.numel() < 1 or done.numel() * \
+            done.element_size() < 4:
+        raise ValueError("adam_flat: float32 buffers of one size, a float32 step and a 4-byte done counter")
+    dev = params.device
+    with torch.cuda.device(dev):
+        check(lib().hf_adam_flat(ptr(params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq), n, ptr(step), ptr(done),
+                                 float(lr), float(beta1), float(beta2), float(eps), stream_of(dev)))
+
+
 def ablation_loss_terms(grid, flux_edge, st, ft, sn, lam):
     """hf_ablation_loss: the single-step terms of the reference trainer's loss
     (scripts/training/train_ablation.py:120-170) for B samples.  flux_edge

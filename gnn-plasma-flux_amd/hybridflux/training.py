@@ -142,6 +142,52 @@ class FluxDataset:
         return engine.chain_batch(idx, self.state_t, self.flux_t, self.state_next, x)
 
 
+class FlatAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (weight decay 0, no amsgrad: the reference trainer's
+    optimizer, train_ablation.py:82, :208-209) for a model whose parameters
+    share one buffer (FluxGNN.flatten_parameters_): the update of every
+    parameter in one HIP launch (hf_adam_flat) with the step count on the
+    device, so it is capturable (GraphedStep) and needs no host sync.  The
+    gradients are read as one buffer when they are (the chain training
+    backward returns them as pieces of one), otherwise concatenated first."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        from .flux_gnn import _flat_view
+        self._flat_view = _flat_view
+        for group in self.param_groups:
+            ps = group["params"]
+            flat = _flat_view(ps, ps[0].device)
+            if flat is None:
+                raise ValueError("FlatAdam: the parameters must share one float32 buffer in order "
+                                 "(call model.flatten_parameters_() first)")
+            st = self.state[ps[0]]
+            st["flat"] = flat
+            st["exp_avg"] = torch.zeros_like(flat)
+            st["exp_avg_sq"] = torch.zeros_like(flat)
+            st["step"] = torch.zeros(1, dtype=torch.float32, device=flat.device)
+            st["done"] = torch.zeros(1, dtype=torch.int32, device=flat.device)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            ps = group["params"]
+            st = self.state[ps[0]]
+            if any(p.grad is None for p in ps):
+                raise RuntimeError("FlatAdam: every parameter needs a gradient")
+            g = self._flat_view([p.grad for p in ps], ps[0].device)
+            if g is None:
+                g = torch.cat([p.grad.reshape(-1) for p in ps])
+            b1, b2 = group["betas"]
+            engine.adam_flat(st["flat"], g, st["exp_avg"], st["exp_avg_sq"], st["step"], st["done"], group["lr"],
+                             b1, b2, group["eps"])
+        return loss
+
+
 class GraphedStep:
     """One optimizer step of the reference trainer's loop (ablation_loss ->
     backward -> optimizer step, train_ablation.py:107-210) on a fixed batch

@@ -198,6 +198,18 @@ int hf_chain_batch_gather(const int64_t *dev_idx, int B, const float *dev_state_
                           float *dev_node_features, void *stream);
 
 /*
+ * Replaces: the reference trainer's optimizer step (torch.optim.Adam,
+ * scripts/training/train_ablation.py:208-209; weight decay 0, no amsgrad) on
+ * one flat float32 parameter buffer of n values, in one launch.  dev_step: the
+ * step count (float, on the device; read, then incremented by the call, so a
+ * captured graph replays it); dev_done: one unsigned, 0 before the first call
+ * (the call leaves it 0).  Update per value: m = b1 m + (1 - b1) g, v = b2 v +
+ * (1 - b2) g^2, p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps).
+ */
+int hf_adam_flat(float *dev_params, const float *dev_grads, float *dev_exp_avg, float *dev_exp_avg_sq, int64_t n,
+                 float *dev_step, unsigned *dev_done, float lr, float beta1, float beta2, float eps, void *stream);
+
+/*
  * The reference's other rollout models, inference.
  * dev_params: every parameter, float32, state-dict order, on the device.
  *

@@ -416,3 +416,57 @@ def test_flattened_parameters_same_step(hf):
     assert torch.equal(out[0][0], out[1][0])
     for u, v in zip(out[0][1] + out[0][2], out[1][1] + out[1][2]):
         assert torch.equal(u, v)
+
+
+def test_flat_adam_matches_torch_adam(hf):
+    """FlatAdam (hf_adam_flat: torch.optim.Adam's update over the flattened
+    parameter buffer, step count on the device) against torch.optim.Adam on
+    the same gradients for 12 steps: equal within f32 rounding of the bias
+    corrections (relative 1e-6 of the parameter scale), and the step count
+    advanced on the device."""
+    from hybridflux.training import FlatAdam
+    torch.manual_seed(6)
+    a = hf.FluxGNN(4, 128, 2).to(DEV)
+    b = hf.FluxGNN(4, 128, 2).to(DEV)
+    b.load_state_dict(a.state_dict())
+    b.flatten_parameters_()
+    oa, ob = torch.optim.Adam(a.parameters(), lr=1e-3), FlatAdam(b.parameters(), lr=1e-3)
+    for k in range(12):
+        grads = [torch.randn_like(p) * 10 ** (k % 3 - 1) for p in a.parameters()]
+        for m in (a, b):
+            for p, gr in zip(m.parameters(), grads):
+                p.grad = gr.clone()
+        oa.step()
+        ob.step()
+    for (ka, pa), (kb, pb) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert ka == kb
+        assert (pa - pb).abs().max().item() <= 1e-6 * max(1.0, pa.abs().max().item()), ka
+    st = ob.state[next(iter(b.parameters()))]
+    assert st["step"].item() == 12.0 and st["done"].item() == 0
+    with pytest.raises(ValueError):
+        FlatAdam(a.parameters())  # not flattened
+
+
+def test_graphed_flat_adam_equals_eager(hf):
+    """GraphedStep replaying FlatAdam (its device step count advancing inside
+    the graph) makes the eager loop's updates bit for bit."""
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import FlatAdam, FluxDataset, GraphedStep, train_steps
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=4, steps_per_ic=32, out_path=None, device=DEV)
+    data = FluxDataset(st, ft, sn, DEV)
+    solver = hf.BaselineSolver(64, device=DEV)
+    xd = torch.as_tensor(x, device=DEV)
+    cfg = hf.ABLATION_CONFIGS["physics"]
+    order = torch.randperm(len(data), generator=torch.Generator().manual_seed(5))[:128].to(DEV)
+    res = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        m = hf.FluxGNN(4, 128, 4).to(DEV).flatten_parameters_()
+        opt = FlatAdam(m.parameters(), lr=1e-3)
+        gs = GraphedStep(m, opt, data, 16, xd, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
+        tot, _, steps = train_steps(m, opt, data, order, 16, xd, solver.dt, solver.dx, cfg, solver.grid, graphed=gs)
+        assert steps == 8 and (gs is None or gs.graph is not None)
+        res.append((tot, {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}))
+    assert res[0][0] == res[1][0]
+    for k in res[0][1]:
+        assert np.array_equal(res[0][1][k], res[1][1][k]), k

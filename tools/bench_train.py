@@ -52,9 +52,13 @@ def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False,
     m = hf.FluxGNN(4, 128, 4).to("cuda")
     if not os.environ.get("HF_AB_NO_FLAT"):  # A/B switch: the per-step parameter concat
         m.flatten_parameters_()
-    opt = (torch.optim.Adam(m.parameters(), lr=1e-3, fused=True) if fused_adam else
-           torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True, fused=True) if graphed else
-           torch.optim.Adam(m.parameters(), lr=1e-3))
+    if fused_adam == "flat":
+        from hybridflux.training import FlatAdam
+        opt = FlatAdam(m.parameters(), lr=1e-3)
+    else:
+        opt = (torch.optim.Adam(m.parameters(), lr=1e-3, fused=True) if fused_adam else
+               torch.optim.Adam(m.parameters(), lr=1e-3, capturable=True, fused=True) if graphed else
+               torch.optim.Adam(m.parameters(), lr=1e-3))
     cfg = hf.ABLATION_CONFIGS[cfg_name]
     gen = torch.Generator().manual_seed(1)
     gs = GraphedStep(m, opt, data, batch, x, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
@@ -129,10 +133,15 @@ def main():
         except (RuntimeError, TypeError) as e:  # fused Adam unavailable in this torch build
             print(f"fused Adam: {e}", file=sys.stderr)
             rf = 0.0
-        best = max(r, rg, rf)
+        ra, _ = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, fused_adam="flat",
+                         warm_s=args.warm_s)
+        rga, _ = gpu_rate(hf, args.config, b, steps, args.warmup, data, x_dev, solver, graphed=True, fused_adam="flat",
+                          warm_s=args.warm_s)
+        best = max(r, rg, rf, ra, rga)
         rates[str(b)] = {"samples_per_s": round(best, 1), "ms_per_step": round(b / best * 1e3, 3), "steps": steps,
                          "eager_samples_per_s": round(r, 1), "graphed_samples_per_s": round(rg, 1),
-                         "eager_fused_adam_samples_per_s": round(rf, 1)}
+                         "eager_fused_adam_samples_per_s": round(rf, 1), "eager_flat_adam_samples_per_s": round(ra, 1),
+                         "graphed_flat_adam_samples_per_s": round(rga, 1)}
         print(f"batch {b}: {r:.1f} samples/s eager ({ms:.3f} ms/step), {rg:.1f} graphed ({msg:.3f} ms/step)",
               file=sys.stderr, flush=True)
     cpu = None
