@@ -283,7 +283,7 @@ def train_model(state_t, flux_t, state_next, x, dt, dx, nu, config_name, stencil
     x_dev = torch.as_tensor(np.asarray(x, dtype=np.float32), device=device)
     model = FluxGNN(MODEL_CONFIG["input_dim"], MODEL_CONFIG["hidden_dim"], MODEL_CONFIG["num_layers"]).to(device)
     model.flatten_parameters_()  # one parameter buffer: no per-step concat in the training forward
-    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    opt = FlatAdam(model.parameters(), lr=lr)  # torch.optim.Adam's update (:82), one launch per step
     gen = torch.Generator().manual_seed(0 if seed is None else seed)
     history = {"epoch": [], "loss": [], "flux_loss": [], "seconds": []}
     model.train()
