@@ -28,6 +28,7 @@
 #include <cstdint>
 #include <type_traits>
 
+#include "hf_device.h"
 #include "hf_internal.h"
 #include "tgemm.h"
 
@@ -553,7 +554,62 @@ __global__ __launch_bounds__(256) void loss_terms_kernel(const float *__restrict
   }
 }
 
-// loss = flux MSE + lam_s state MSE + lam_p Poisson MSE + lam_c charge + lam_e energy
+// loss_update_kernel + the detached Poisson solve (poisson_kernel's circulant
+// sum, poisson_cell) + loss_terms_kernel in one launch at the circulant sizes
+// (not an FFT size, nx <= kLossFusedMaxNx): n' and rho' = n' - 1 stay in LDS,
+// E' is formed per cell where the terms use it.  Term for term the three
+// kernels' arithmetic.
+constexpr int kLossFusedMaxNx = 2048;
+__global__ __launch_bounds__(256) void loss_step_kernel(const float *__restrict__ fe, const float *__restrict__ st,
+                                                        const float *__restrict__ ft, const float *__restrict__ sn,
+                                                        const double *__restrict__ pc, int B, int nx, float c,
+                                                        float lam_s, float *__restrict__ part,
+                                                        float *__restrict__ dfe) {
+  extern __shared__ double s_cd[];  // c [nx] (double), then rho' [nx], n' [nx] (float)
+  float *s_rho = reinterpret_cast<float *>(s_cd + nx), *s_np = s_rho + nx;
+  __shared__ float sh[256];
+  const int b = blockIdx.x;
+  const float *f = fe + (int64_t)b * 2 * nx, *n = st + (int64_t)b * 3 * nx, *F_t = ft + (int64_t)b * nx;
+  const float *nt = sn + (int64_t)b * 3 * nx, *ut = nt + nx, *Et = nt + 2 * nx;
+  for (int i = threadIdx.x; i < nx; i += blockDim.x) {
+    s_cd[i] = pc[i];
+    const float Fi = face_of(f, nx, i), Fl = face_of(f, nx, i == 0 ? nx - 1 : i - 1);
+    const float v = __fsub_rn(n[i], __fmul_rn(c, __fsub_rn(Fi, Fl)));
+    s_np[i] = v;
+    s_rho[i] = __fsub_rn(v, 1.0f);  // rho = n - n0 (baseline_solver.py:60)
+  }
+  __syncthreads();
+  const float inv = 2.0f / ((float)B * (float)nx);
+  float sacc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = threadIdx.x; i < nx; i += blockDim.x) {
+    const float Ep = poisson_cell(s_rho, s_cd, i, nx);
+    const float Fi = face_of(f, nx, i), dF = __fsub_rn(Fi, F_t[i]);
+    const float r = __fsub_rn(s_np[i], nt[i]);
+    const int ip = i == nx - 1 ? 0 : i + 1;
+    const float rn = __fsub_rn(s_np[ip], nt[ip]);
+    const float dE = __fsub_rn(Ep, Et[i]);
+    sacc[0] = fmaf(dF, dF, sacc[0]);
+    sacc[1] = fmaf(r, r, sacc[1]);
+    sacc[2] = fmaf(dE, dE, sacc[2]);
+    sacc[3] = __fadd_rn(sacc[3], __fsub_rn(n[i], 1.0f));
+    sacc[4] = __fadd_rn(sacc[4], __fsub_rn(s_np[i], 1.0f));
+    sacc[5] = __fadd_rn(sacc[5], __fadd_rn(__fmul_rn(ut[i], ut[i]), __fmul_rn(Ep, Ep)));
+    sacc[6] = __fadd_rn(sacc[6], __fadd_rn(__fmul_rn(ut[i], ut[i]), __fmul_rn(Et[i], Et[i])));
+    const float g = lam_s > 0.f
+                        ? __fadd_rn(__fmul_rn(inv, dF), __fmul_rn(lam_s, __fmul_rn(__fmul_rn(inv, c), __fsub_rn(rn, r))))
+                        : __fmul_rn(inv, dF);
+    const float h = __fmul_rn(0.5f, g);
+    dfe[(int64_t)b * 2 * nx + i] = h;
+    dfe[(int64_t)b * 2 * nx + nx + i] = h;
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const float v = block_sum256(sacc[k], sh);
+    if (threadIdx.x == 0) part[(int64_t)b * 7 + k] = v;
+  }
+}
+
+// loss = flux MSE + lam_s state MSE + lam_p Poisson MSE + lam_c charge + lam_e energy// loss = flux MSE + lam_s state MSE + lam_p Poisson MSE + lam_c charge + lam_e energy
 // (terms with lambda 0 are left out, as the reference does), one block, fixed order.
 __global__ __launch_bounds__(256) void loss_final_kernel(const float *__restrict__ part, int B, int nx, float dx,
                                                          float lam_s, float lam_p, float lam_c, float lam_e,
@@ -813,11 +869,19 @@ hipError_t launch_ablation_loss(const float *fe, const float *st, const float *f
   float *nn = reinterpret_cast<float *>(p);
   float *En = reinterpret_cast<float *>(p + al256(sizeof(float) * (size_t)B * nx));
   float *part = reinterpret_cast<float *>(p + 2 * al256(sizeof(float) * (size_t)B * nx));
-  hipLaunchKernelGGL(loss_update_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, nx, c, nn);
-  hipError_t e = launch_poisson(nn, nx, En, nx, pc, B, nx, HF_POISSON_SPECTRAL, s);  // detached E' (:138-145)
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(loss_terms_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, ft, sn, nn, En, B, nx, c, lam[0],
-                     part, dfe);
+#ifndef HF_LOSS_FUSED
+#define HF_LOSS_FUSED 1
+#endif
+  if (HF_LOSS_FUSED && !poisson_uses_fft(nx) && nx <= kLossFusedMaxNx) {
+    hipLaunchKernelGGL(loss_step_kernel, dim3((unsigned)B), dim3(256), (size_t)nx * (sizeof(double) + 2 * sizeof(float)),
+                       s, fe, st, ft, sn, pc, B, nx, c, lam[0], part, dfe);
+  } else {
+    hipLaunchKernelGGL(loss_update_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, nx, c, nn);
+    hipError_t e = launch_poisson(nn, nx, En, nx, pc, B, nx, HF_POISSON_SPECTRAL, s);  // detached E' (:138-145)
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(loss_terms_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, ft, sn, nn, En, B, nx, c, lam[0],
+                       part, dfe);
+  }
   hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, s, part, B, nx, dx, lam[0], lam[1], lam[2], lam[3],
                      loss, flux_loss);
   return hipGetLastError();
