@@ -206,6 +206,20 @@ def test_training_entry_points_validate_before_device():
     assert P > 0
 
 
+def test_trainer_entry_points_validate_before_device():
+    """hf_chain_batch_gather and hf_adam_flat refuse bad sizes and NULL
+    buffers before any HIP call (runs without a GPU); empty work is a no-op."""
+    lib = _lib.lib()
+    d = ctypes.c_void_p(1)
+    assert lib.hf_chain_batch_gather(d, 4, d, d, d, 0, 64, d, d, d, d, d, None) == _lib.HF_EINVAL   # N < 1
+    assert lib.hf_chain_batch_gather(d, 4, d, d, d, 10, 0, d, d, d, d, d, None) == _lib.HF_EINVAL   # nx < 1
+    assert lib.hf_chain_batch_gather(d, 4, None, d, d, 10, 64, d, d, d, d, d, None) == _lib.HF_EINVAL
+    assert b"NULL" in lib.hf_last_error()
+    assert lib.hf_adam_flat(d, d, d, d, -1, d, d, 1e-3, 0.9, 0.999, 1e-8, None) == _lib.HF_EINVAL
+    assert lib.hf_adam_flat(d, d, None, d, 10, d, d, 1e-3, 0.9, 0.999, 1e-8, None) == _lib.HF_EINVAL
+    assert lib.hf_adam_flat(None, None, None, None, 0, None, None, 1e-3, 0.9, 0.999, 1e-8, None) == _lib.HF_OK
+
+
 def test_workspace_need_classical():
     """hf_workspace_need is a host-side size query: exact per path, -1 on bad arguments."""
     from hybridflux._lib import HF_OP_COMPARE, HF_OP_RUN, HF_OP_STEP
