@@ -161,12 +161,12 @@ class FlatAdam(torch.optim.Optimizer):
             if flat is None:
                 raise ValueError("FlatAdam: the parameters must share one float32 buffer in order "
                                  "(call model.flatten_parameters_() first)")
-            st = self.state[ps[0]]
-            st["flat"] = flat
+            st = self.state[ps[0]]  # (the buffer itself is found again each step: state_dict() stays plain)
             st["exp_avg"] = torch.zeros_like(flat)
             st["exp_avg_sq"] = torch.zeros_like(flat)
             st["step"] = torch.zeros(1, dtype=torch.float32, device=flat.device)
-            st["done"] = torch.zeros(1, dtype=torch.int32, device=flat.device)
+            # the kernel's done-counter: 4 zero bytes (float32 so that load_state_dict's cast keeps them 0)
+            st["done"] = torch.zeros(1, dtype=torch.float32, device=flat.device)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -177,13 +177,19 @@ class FlatAdam(torch.optim.Optimizer):
         for group in self.param_groups:
             ps = group["params"]
             st = self.state[ps[0]]
+            flat = self._flat_view(ps, ps[0].device)
+            if flat is None:
+                raise RuntimeError("FlatAdam: the parameters no longer share one buffer (moved or re-created?)")
             if any(p.grad is None for p in ps):
                 raise RuntimeError("FlatAdam: every parameter needs a gradient")
+            for k in ("exp_avg", "exp_avg_sq", "step", "done"):  # (a state_dict loaded elsewhere)
+                if st[k].device != flat.device or st[k].dtype != torch.float32 or not st[k].is_contiguous():
+                    st[k] = st[k].to(device=flat.device, dtype=torch.float32).contiguous()
             g = self._flat_view([p.grad for p in ps], ps[0].device)
             if g is None:
                 g = torch.cat([p.grad.reshape(-1) for p in ps])
             b1, b2 = group["betas"]
-            engine.adam_flat(st["flat"], g, st["exp_avg"], st["exp_avg_sq"], st["step"], st["done"], group["lr"],
+            engine.adam_flat(flat, g, st["exp_avg"], st["exp_avg_sq"], st["step"], st["done"], group["lr"],
                              b1, b2, group["eps"])
         return loss
 

@@ -424,6 +424,7 @@ def test_flat_adam_matches_torch_adam(hf):
     the same gradients for 12 steps: equal within f32 rounding of the bias
     corrections (relative 1e-6 of the parameter scale), and the step count
     advanced on the device."""
+    import copy
     from hybridflux.training import FlatAdam
     torch.manual_seed(6)
     a = hf.FluxGNN(4, 128, 2).to(DEV)
@@ -445,6 +446,22 @@ def test_flat_adam_matches_torch_adam(hf):
     assert st["step"].item() == 12.0 and st["done"].item() == 0
     with pytest.raises(ValueError):
         FlatAdam(a.parameters())  # not flattened
+    # state_dict round trip (through the host): the same moments and step count
+    sd = ob.state_dict()
+    sd["state"] = {k: {n: t.cpu() for n, t in v.items()} for k, v in sd["state"].items()}
+    oc = FlatAdam(b.parameters(), lr=1e-3)
+    oc.load_state_dict(sd)
+    for p in b.parameters():
+        p.grad = torch.ones_like(p)
+    ref = copy.deepcopy(b)
+    ob.step()
+    after_ob = [q.detach().clone() for q in b.parameters()]
+    with torch.no_grad():
+        for q, r in zip(b.parameters(), ref.parameters()):
+            q.copy_(r)
+    oc.step()
+    for u, v in zip(after_ob, b.parameters()):
+        assert torch.equal(u, v)
 
 
 def test_graphed_flat_adam_equals_eager(hf):
