@@ -487,3 +487,31 @@ def test_graphed_flat_adam_equals_eager(hf):
     assert res[0][0] == res[1][0]
     for k in res[0][1]:
         assert np.array_equal(res[0][1][k], res[1][1][k]), k
+
+
+@pytest.mark.parametrize("nx", [1, 16, 100, 256])
+def test_loss_terms_any_nx(hf, nx):
+    """hf_ablation_loss at chain lengths other than the trainer's 64: the
+    one-launch terms (circulant sizes: nx = 1, 16, 100) and the three-launch
+    form around the FFT Poisson (nx = 256) against the torch expressions of
+    the same loss ('physics' weights; loss, flux loss and d loss / d flux_edge)."""
+    from hybridflux.training import ablation_loss
+    g = torch.Generator().manual_seed(nx)
+    B = 37
+    st = (1.0 + 0.1 * torch.randn(B, 3, nx, generator=g)).to(DEV)
+    sn = (1.0 + 0.1 * torch.randn(B, 3, nx, generator=g)).to(DEV)
+    ft = (0.1 * torch.randn(B, nx, generator=g)).to(DEV)
+    fe0 = (0.1 * torch.randn(B * 2 * nx, generator=g)).to(DEV)
+    solver = hf.BaselineSolver(nx, device=DEV)
+    x = torch.as_tensor(solver.x, dtype=torch.float32, device=DEV)
+    cfg = hf.ABLATION_CONFIGS["physics"]
+    out = []
+    for fused in (True, False):
+        fe = fe0.clone().requires_grad_(True)
+        loss, fl = ablation_loss(lambda nf, ei: fe, st, ft, sn, x, solver.dt, solver.dx, cfg, solver.grid,
+                                 fused=fused)
+        loss.backward()
+        out.append((loss.item(), fl.item(), fe.grad.detach().clone()))
+    assert abs(out[0][0] - out[1][0]) <= 2e-6 * abs(out[1][0])
+    assert abs(out[0][1] - out[1][1]) <= 2e-6 * abs(out[1][1])
+    torch.testing.assert_close(out[0][2], out[1][2], rtol=1e-5, atol=1e-10)
