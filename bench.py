@@ -242,7 +242,7 @@ def other_models(dev, B, K, warm_s=0.3):
     return out
 
 
-def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
+def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3, more=("full", "rollout_only")):
     """SURVEY.md 8(f2), timed inside the driver's bench: one optimizer step of
     the reference trainer's loop (scripts/training/train_ablation.py:119-206:
     the cfg_name ablation loss, loss.backward(), Adam) on `batch` samples of
@@ -253,26 +253,24 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
     the captured step (hybridflux.training.GraphedStep, fused capturable
     Adam), and eager / replayed with hybridflux's FlatAdam (the same update in
     one launch over the parameter buffer); each warmed for warm_s, then `steps`
-    steps timed with HIP events + the wall clock.  FLOPs per sample: FluxGNN
-    forward + backward (tools/bench_train.py flop_per_sample); the loss terms,
-    FV updates and Adam are inside the timed step but not counted."""
+    steps timed with HIP events + the wall clock.  Then the configs of `more`
+    (the rollout-loss ablations 'full' and 'rollout_only', half of the
+    reference's checkpoints) in the best mode.  FLOPs per sample: FluxGNN
+    forward + backward (hybridflux.training.train_flop_per_sample: algorithmic,
+    no redundant rollout forwards); the loss terms, FV updates and Adam are
+    inside the timed step but not counted."""
     from hybridflux import ABLATION_CONFIGS, BaselineSolver, FluxGNN
     from hybridflux.datagen import generate_dataset
-    from hybridflux.training import FlatAdam, FluxDataset, GraphedStep, train_steps
-    from tools.bench_train import flop_per_sample
+    from hybridflux.training import FlatAdam, FluxDataset, GraphedStep, train_flop_per_sample, train_steps
     st, ft, sn, x, dt, dx, nu = generate_dataset(out_path=None, device=dev, num_initial_conditions=50,
                                                  steps_per_ic=40)
     data = FluxDataset(st, ft, sn, dev)
     solver = BaselineSolver(64, device=dev)
     x_dev = torch.as_tensor(x, device=dev)
-    cfg = ABLATION_CONFIGS[cfg_name]
-    fps = flop_per_sample(cfg_name)
-    out = {"metric": f"FluxGNN training samples/s ('{cfg_name}' ablation loss, Adam)", "unit": "samples/s",
-           "batch": batch, "steps": steps, "flop_per_sample": fps,
-           "dataset": "DATASET_CONFIG recipe: 50 ICs x 40 steps, nx=64 (GPU classical rollout)"}
-    best = None
-    for mode in ("eager", "eager_fused_adam", "graphed", "eager_flat_adam", "graphed_flat_adam"):
-        progress(f"training line: {mode}")
+
+    def arm(name, mode):
+        cfg = ABLATION_CONFIGS[name]
+        fps = train_flop_per_sample(cfg)
         graphed = mode.startswith("graphed")
         torch.manual_seed(0)
         m = FluxGNN(4, 128, 4).to(dev).flatten_parameters_()
@@ -290,14 +288,29 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3):
         wall, kms = timed(lambda: train_steps(m, opt, data, order, batch, x_dev, solver.dt, solver.dx, cfg,
                                               solver.grid, graphed=gs), dev, 1, warm_s)
         rate = steps * batch / wall
-        out[mode] = {"value": round(rate, 1), "ms_per_step": round(wall / steps * 1e3, 4),
-                     "kernel_ms": round(kms, 3),
-                     "mfma_frac": round(fps * steps * batch / (kms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)}
+        del m, opt, gs
+        return rate, {"value": round(rate, 1), "ms_per_step": round(wall / steps * 1e3, 4),
+                      "kernel_ms": round(kms, 3), "flop_per_sample": fps,
+                      "mfma_frac": round(fps * steps * batch / (kms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)}
+
+    out = {"metric": f"FluxGNN training samples/s ('{cfg_name}' ablation loss, Adam)", "unit": "samples/s",
+           "batch": batch, "steps": steps, "flop_per_sample": train_flop_per_sample(cfg_name),
+           "dataset": "DATASET_CONFIG recipe: 50 ICs x 40 steps, nx=64 (GPU classical rollout)"}
+    best = None
+    for mode in ("eager", "eager_fused_adam", "graphed", "eager_flat_adam", "graphed_flat_adam"):
+        progress(f"training line: {mode}")
+        rate, out[mode] = arm(cfg_name, mode)
         if best is None or rate > best[1]:
             best = (mode, rate)
-        del m, opt, gs
     out["value"] = round(best[1], 1)
     out["best"] = best[0]
+    for name in more:  # the rollout-loss configs, same step, best mode
+        progress(f"training line: '{name}' ({best[0]})")
+        rate, r = arm(name, best[0])
+        r.update(mode=best[0], vs_physics=round(rate / best[1], 4),
+                 note="rollout energy term (train_ablation.py:172-206) in the loss pass, no redundant forwards "
+                      "(the reference's 3 rollout forwards reach no energy)")
+        out[name] = r
     return out
 
 
@@ -345,6 +358,38 @@ def headline_parity(traj_buf, nx, K, weights_path, precision):
             "gate": "|gpu - ref| <= 2e-6 + 2e-6*|ref| (tests/test_gpu_parity.py ROLL_ATOL/ROLL_RTOL)",
             "within_gate": bool(excess <= 0.0 and np.isfinite(got).all()),
             "reference": "tests/golden/hybrid_W1_r3_nx64.npz (seeds 1000..1015, reference CPU HybridSolver)"}
+
+
+def rank_report(wall, ics, group=None):
+    """The job's timing across ranks, from ONE all_gather of every rank's
+    (wall seconds, ICs processed): the max (the job's time: the slowest shard
+    ends it) plus, so that a multi-rank line checks itself, each rank's wall
+    and IC count and their min / max.  float64 on the CPU for gloo, on the
+    rank's HIP device for RCCL; without a process group, this rank alone."""
+    if dist.is_initialized():
+        backend = dist.get_backend(group)
+        dev = torch.device("cuda", torch.cuda.current_device()) if backend != "gloo" else torch.device("cpu")
+        world = dist.get_world_size(group)
+        mine = torch.tensor([float(wall), float(ics)], dtype=torch.float64, device=dev)
+        allr = torch.empty(world * 2, dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(allr, mine, group=group)
+        rows = allr.view(world, 2).cpu().tolist()
+    else:
+        rows = [[float(wall), float(ics)]]
+    walls = [r[0] for r in rows]
+    return {"wall_s_max": max(walls), "wall_s_min": min(walls), "wall_s_per_rank": [round(w, 6) for w in walls],
+            "ics_per_rank": [int(r[1]) for r in rows]}
+
+
+def collective_entry(coll, world, exchange_ms):
+    """The line's config.collective record of the end-of-rollout exchange
+    (COLLECTIVES as counted by hybridflux.rollout: one packed all_gather)."""
+    return {"op": "all_gather of the per-IC metric series [B,T+1,4] + summaries [B,8] (inside the timed region)",
+            "backend": {"nccl": "nccl (RCCL)", "gloo": "gloo"}[coll["backend"]],
+            "world_size": world, "calls": coll["calls"],
+            "bytes_sent_per_rank": coll["bytes_sent"],
+            "bytes_received_per_rank": coll["bytes_received"],
+            "exchange_ms": round(exchange_ms, 4)}
 
 
 class _StdoutToStderr:
@@ -482,7 +527,7 @@ def main():
 
     from hybridflux import HybridSolver, engine
     from hybridflux._lib import HF_OP_RUN, build_hash, diagnostic_build, version
-    from hybridflux.rollout import COLLECTIVES, gather_rollout, max_over_ranks, reset_collective_stats, shard_seeds
+    from hybridflux.rollout import COLLECTIVES, gather_rollout, reset_collective_stats, shard_seeds
     if diagnostic_build():
         # HF_DIAG_* / HF_EXP_* builds time deliberately broken or experimental
         # kernels: never a headline (tools/diag_*.py measure those)
@@ -648,7 +693,8 @@ def main():
         progress("training line")
     train = train_line(dev) if world == 1 and not args.no_other_configs and not args.no_train else None
 
-    wall_max = max_over_ranks(wall)
+    ranks = rank_report(wall, B)  # one all_gather: the max over ranks and each rank's wall / ICs
+    wall_max = ranks["wall_s_max"]
     finite = float(gathered["metrics"][:, -1, 2].float().mean().item())
     exploded = int((gathered["summary"][:, 0] >= 0).sum().item())
 
@@ -703,15 +749,11 @@ def main():
             "config": {"workload": f"{'cfg3' if (nx == 64 and B == 4096) else 'cfg2' if (nx == 64 and B == 256) else 'cfg4' if nx == 1024 else 'custom'}: {nx}-cell periodic chain, {B}-IC batch per GPU, FluxGNN(4,128,4) {args.precision}, "
                                    f"{K}-step persistent rollout{'' if args.no_traj else ' recording every state'}",
                        "nx": nx, "dt": dt, "ics_per_gpu": B, "global_ics": n_total, "parallelism": f"ic-shard x{world}",
-                       "collective": ({"op": "all_gather of the per-IC metric series [B,T+1,4] + summaries [B,8] "
-                                             "(inside the timed region)",
-                                       "backend": {"nccl": "nccl (RCCL)", "gloo": "gloo"}[coll["backend"]],
-                                       "world_size": world, "calls": coll["calls"],
-                                       "bytes_sent_per_rank": coll["bytes_sent"],
-                                       "bytes_received_per_rank": coll["bytes_received"],
-                                       "exchange_ms": round(exchange_ms, 4)}
-                                      if coll["calls"] else
-                                      ({"backend": "none", "error": group_error} if group_error else None))},
+                       "collective": (collective_entry(coll, world, exchange_ms) if coll["calls"] else
+                                      ({"backend": "none", "error": group_error} if group_error else None)),
+                       # per-rank timing, so that an N > 1 line checks itself (the value uses the max);
+                       # multi-GPU scaling of this path is unmeasured on hardware by this repo
+                       "ranks": ranks if world > 1 else None},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "traffic": traffic["traffic_bytes"] if traffic else None,

@@ -454,18 +454,31 @@ int64_t hf_ablation_loss_workspace_bytes(int B, int nx) {
   return hf::ablation_loss_ws_bytes(B, nx);
 }
 
-int hf_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx, float c,
-                     float dx, const float *lam, const double *pc, float *loss, float *flux_loss, float *dfe, void *ws,
-                     int64_t ws_bytes, void *stream) {
+int hf_ablation_loss_ex(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx, float c,
+                        float dx, const float *lam, int rollout_steps, float dt, const double *pc, float *loss,
+                        float *flux_loss, float *dfe, void *ws, int64_t ws_bytes, void *stream) {
   if (B < 1 || nx < 1) return fail(HF_EINVAL, "hf_ablation_loss: need B >= 1, nx >= 1");
   if (!fe || !st || !ft || !sn || !lam || !pc || !loss || !flux_loss || !dfe || !ws)
     return fail(HF_EINVAL, "hf_ablation_loss: NULL pointer");
   if (ws_bytes < hf::ablation_loss_ws_bytes(B, nx))
     return fail(HF_EINVAL, "hf_ablation_loss: workspace smaller than hf_ablation_loss_workspace_bytes");
-  HF_CHECK_HIP(hf::launch_ablation_loss(fe, st, ft, sn, B, nx, c, dx, lam, pc, loss, flux_loss, dfe, ws,
-                                        as_stream(stream)),
+  if (rollout_steps < 0) return fail(HF_EINVAL, "hf_ablation_loss_ex: rollout_steps < 0");
+  if (rollout_steps > hf::kLossMaxRollout && lam[4] > 0.f)
+    return fail(HF_EUNSUPPORTED, "hf_ablation_loss_ex: rollout_steps > 3 needs model forwards on later states "
+                                 "(pass lam[4] = 0 and add the term from those forwards)");
+  HF_CHECK_HIP(hf::launch_ablation_loss(fe, st, ft, sn, B, nx, c, dx, lam, rollout_steps, dt, pc, loss, flux_loss, dfe,
+                                        ws, as_stream(stream)),
                "hf_ablation_loss");
   return HF_OK;
+}
+
+int hf_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx, float c,
+                     float dx, const float *lam, const double *pc, float *loss, float *flux_loss, float *dfe, void *ws,
+                     int64_t ws_bytes, void *stream) {
+  if (!lam) return fail(HF_EINVAL, "hf_ablation_loss: NULL pointer");
+  const float lam5[5] = {lam[0], lam[1], lam[2], lam[3], 0.f};
+  return hf_ablation_loss_ex(fe, st, ft, sn, B, nx, c, dx, lam5, 0, 0.f, pc, loss, flux_loss, dfe, ws, ws_bytes,
+                             stream);
 }
 
 int hf_chain_batch_gather(const int64_t *idx, int B, const float *st_all, const float *ft_all, const float *sn_all,

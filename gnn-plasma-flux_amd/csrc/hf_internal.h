@@ -249,8 +249,9 @@ hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, floa
 // The ablation loss's single-step terms and d loss / d flux_edge (train_chain.hip).
 int64_t ablation_loss_ws_bytes(int B, int nx);
 hipError_t launch_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx,
-                                float c, float dx, const float *lam, const double *pc, float *loss, float *flux_loss,
-                                float *dfe, void *ws, hipStream_t s);
+                                float c, float dx, const float *lam, int roll, float dt, const double *pc, float *loss,
+                                float *flux_loss, float *dfe, void *ws, hipStream_t s);
+constexpr int kLossMaxRollout = 3;  // rollout energy term in the loss kernels: rollout_steps <= 3
 // The trainer's batch gather + chain node features (train_chain.hip).
 hipError_t launch_chain_batch_gather(const int64_t *idx, int B, const float *st_all, const float *ft_all,
                                      const float *sn_all, int64_t N, int nx, const float *x, float *st, float *ft,

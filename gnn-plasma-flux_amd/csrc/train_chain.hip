@@ -484,6 +484,28 @@ __global__ void input_dgrad_kernel(const float *__restrict__ d, const float *__r
 __device__ __forceinline__ float face_of(const float *fe, int nx, int i) {
   return __fmul_rn(0.5f, __fadd_rn(fe[i], fe[nx + i]));
 }
+// The multi-step rollout energy term's states (train_ablation.py:171-202),
+// of which the energies 0.5 mean(u_k^2), k < rollout_steps <= 3, use u_0..u_2
+// only: u_{k+1} = u_k - c (F_u(u_k) - roll(F_u(u_k), 1)) + dt E_k with
+// F_u = 0.5 u u (:193-196), E_0 the sample's E and E_1 the detached Poisson
+// E of n' — the n' of the main forward, which the rollout's first forward
+// repeats (same model, same state); the later forwards reach no energy.
+// Operation for operation the torch expressions' float32 arithmetic.
+__device__ __forceinline__ float burgers_flux(float u) { return __fmul_rn(__fmul_rn(0.5f, u), u); }
+__device__ __forceinline__ float rollout_u1(const float *u0, const float *E0, int nx, int j, float c, float dt) {
+  const int jl = j == 0 ? nx - 1 : j - 1;
+  return __fadd_rn(__fsub_rn(u0[j], __fmul_rn(c, __fsub_rn(burgers_flux(u0[j]), burgers_flux(u0[jl])))),
+                   __fmul_rn(dt, E0[j]));
+}
+// (u_1[i], u_2[i]) given E_1[i]
+__device__ __forceinline__ float2 rollout_u12(const float *u0, const float *E0, int nx, int i, float c, float dt,
+                                              float E1) {
+  const float a = rollout_u1(u0, E0, nx, i, c, dt), al = rollout_u1(u0, E0, nx, i == 0 ? nx - 1 : i - 1, c, dt);
+  const float b = __fadd_rn(__fsub_rn(a, __fmul_rn(c, __fsub_rn(burgers_flux(a), burgers_flux(al)))), __fmul_rn(dt, E1));
+  return make_float2(a, b);
+}
+constexpr int kLossParts = 10;  // per-sample sums: the 7 single-step ones, then sum u_k^2 for k = 0, 1, 2
+
 __global__ __launch_bounds__(256) void loss_update_kernel(const float *__restrict__ fe, const float *__restrict__ st,
                                                           int nx, float c, float *__restrict__ nn) {
   const int b = blockIdx.x;
@@ -516,16 +538,23 @@ __device__ __forceinline__ float block_sum256(float v, float *sh) {
 __global__ __launch_bounds__(256) void loss_terms_kernel(const float *__restrict__ fe, const float *__restrict__ st,
                                                          const float *__restrict__ ft, const float *__restrict__ sn,
                                                          const float *__restrict__ nn, const float *__restrict__ En,
-                                                         int B, int nx, float c, float lam_s, float *__restrict__ part,
-                                                         float *__restrict__ dfe) {
+                                                         int B, int nx, float c, float lam_s, float dt, int roll,
+                                                         float *__restrict__ part, float *__restrict__ dfe) {
   __shared__ float sh[256];
   const int b = blockIdx.x;
   const float *f = fe + (int64_t)b * 2 * nx, *n = st + (int64_t)b * 3 * nx, *F_t = ft + (int64_t)b * nx;
   const float *nt = sn + (int64_t)b * 3 * nx, *ut = nt + nx, *Et = nt + 2 * nx;
   const float *np = nn + (int64_t)b * nx, *Ep = En + (int64_t)b * nx;
+  const float *u0 = n + nx, *E0 = n + 2 * nx;
   const float inv = 2.0f / ((float)B * (float)nx);
-  float s[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float s[kLossParts] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int i = threadIdx.x; i < nx; i += blockDim.x) {
+    if (roll >= 2) {  // the rollout energies' u_0, u_1, u_2 (E_1 = E')
+      const float2 u12 = rollout_u12(u0, E0, nx, i, c, dt, Ep[i]);
+      s[7] = fmaf(u0[i], u0[i], s[7]);
+      s[8] = fmaf(u12.x, u12.x, s[8]);
+      s[9] = fmaf(u12.y, u12.y, s[9]);
+    }
     const float Fi = face_of(f, nx, i), dF = __fsub_rn(Fi, F_t[i]);
     const float r = __fsub_rn(np[i], nt[i]);
     const int ip = i == nx - 1 ? 0 : i + 1;
@@ -547,10 +576,10 @@ __global__ __launch_bounds__(256) void loss_terms_kernel(const float *__restrict
     dfe[(int64_t)b * 2 * nx + i] = h;
     dfe[(int64_t)b * 2 * nx + nx + i] = h;
   }
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
+  const int np_ = roll >= 2 ? kLossParts : 7;
+  for (int k = 0; k < np_; ++k) {
     const float v = block_sum256(s[k], sh);
-    if (threadIdx.x == 0) part[(int64_t)b * 7 + k] = v;
+    if (threadIdx.x == 0) part[(int64_t)b * kLossParts + k] = v;
   }
 }
 
@@ -563,7 +592,7 @@ constexpr int kLossFusedMaxNx = 2048;
 __global__ __launch_bounds__(256) void loss_step_kernel(const float *__restrict__ fe, const float *__restrict__ st,
                                                         const float *__restrict__ ft, const float *__restrict__ sn,
                                                         const double *__restrict__ pc, int B, int nx, float c,
-                                                        float lam_s, float *__restrict__ part,
+                                                        float lam_s, float dt, int roll, float *__restrict__ part,
                                                         float *__restrict__ dfe) {
   extern __shared__ double s_cd[];  // c [nx] (double), then rho' [nx], n' [nx] (float)
   float *s_rho = reinterpret_cast<float *>(s_cd + nx), *s_np = s_rho + nx;
@@ -580,9 +609,16 @@ __global__ __launch_bounds__(256) void loss_step_kernel(const float *__restrict_
   }
   __syncthreads();
   const float inv = 2.0f / ((float)B * (float)nx);
-  float sacc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float *u0 = n + nx, *E0 = n + 2 * nx;
+  float sacc[kLossParts] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int i = threadIdx.x; i < nx; i += blockDim.x) {
     const float Ep = poisson_cell(s_rho, s_cd, i, nx);
+    if (roll >= 2) {  // the rollout energies' u_0, u_1, u_2 (E_1 = E')
+      const float2 u12 = rollout_u12(u0, E0, nx, i, c, dt, Ep);
+      sacc[7] = fmaf(u0[i], u0[i], sacc[7]);
+      sacc[8] = fmaf(u12.x, u12.x, sacc[8]);
+      sacc[9] = fmaf(u12.y, u12.y, sacc[9]);
+    }
     const float Fi = face_of(f, nx, i), dF = __fsub_rn(Fi, F_t[i]);
     const float r = __fsub_rn(s_np[i], nt[i]);
     const int ip = i == nx - 1 ? 0 : i + 1;
@@ -602,22 +638,31 @@ __global__ __launch_bounds__(256) void loss_step_kernel(const float *__restrict_
     dfe[(int64_t)b * 2 * nx + i] = h;
     dfe[(int64_t)b * 2 * nx + nx + i] = h;
   }
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
+  const int np_ = roll >= 2 ? kLossParts : 7;
+  for (int k = 0; k < np_; ++k) {
     const float v = block_sum256(sacc[k], sh);
-    if (threadIdx.x == 0) part[(int64_t)b * 7 + k] = v;
+    if (threadIdx.x == 0) part[(int64_t)b * kLossParts + k] = v;
   }
 }
 
-// loss = flux MSE + lam_s state MSE + lam_p Poisson MSE + lam_c charge + lam_e energy// loss = flux MSE + lam_s state MSE + lam_p Poisson MSE + lam_c charge + lam_e energy
-// (terms with lambda 0 are left out, as the reference does), one block, fixed order.
+// loss = flux MSE + lam_s state MSE + lam_p Poisson MSE + lam_c charge + lam_e energy
+// + lam_m rollout energy drift mean_{k<K, b} (e_k - e_0)^2 (train_ablation.py:204-206;
+// roll = K, the term only when K > 0 and lam_m > 0) (terms with lambda 0 are left
+// out, as the reference does), one block, fixed order.
 __global__ __launch_bounds__(256) void loss_final_kernel(const float *__restrict__ part, int B, int nx, float dx,
                                                          float lam_s, float lam_p, float lam_c, float lam_e,
-                                                         float *loss, float *flux_loss) {
+                                                         float lam_m, int roll, float *loss, float *flux_loss) {
   __shared__ float sh[256];
-  float a[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float a[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const float *p = part + (int64_t)b * 7;
+    const float *p = part + (int64_t)b * kLossParts;
+    if (roll >= 2) {  // energies e_k = 0.5 mean(u_k^2) (:181); k = 0 adds (e_0 - e_0)^2 = 0
+      const float e0 = __fmul_rn(0.5f, __fdiv_rn(p[7], (float)nx));
+      for (int k = 1; k < roll; ++k) {
+        const float d = __fsub_rn(__fmul_rn(0.5f, __fdiv_rn(p[7 + k], (float)nx)), e0);
+        a[5] = fmaf(d, d, a[5]);
+      }
+    }
     a[0] = __fadd_rn(a[0], p[0]);
     a[1] = __fadd_rn(a[1], p[1]);
     a[2] = __fadd_rn(a[2], p[2]);
@@ -626,9 +671,9 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const float *__restrict
     const float de = __fsub_rn(__fmul_rn(0.5f, __fdiv_rn(p[5], (float)nx)), __fmul_rn(0.5f, __fdiv_rn(p[6], (float)nx)));
     a[4] = fmaf(de, de, a[4]);
   }
-  float t[5];
+  float t[6];
 #pragma unroll
-  for (int k = 0; k < 5; ++k) t[k] = block_sum256(a[k], sh);
+  for (int k = 0; k < 6; ++k) t[k] = block_sum256(a[k], sh);
   if (threadIdx.x == 0) {
     const float N = (float)B * (float)nx;
     const float fl = __fdiv_rn(t[0], N);
@@ -637,6 +682,7 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const float *__restrict
     if (lam_p > 0.f) L = __fadd_rn(L, __fmul_rn(lam_p, __fdiv_rn(t[2], N)));
     if (lam_c > 0.f) L = __fadd_rn(L, __fmul_rn(lam_c, __fdiv_rn(t[3], (float)B)));
     if (lam_e > 0.f) L = __fadd_rn(L, __fmul_rn(lam_e, __fdiv_rn(t[4], (float)B)));
+    if (roll > 0 && lam_m > 0.f) L = __fadd_rn(L, __fmul_rn(lam_m, __fdiv_rn(t[5], (float)roll * (float)B)));
     *loss = L;
     *flux_loss = fl;
   }
@@ -859,12 +905,13 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
 }
 
 int64_t ablation_loss_ws_bytes(int B, int nx) {
-  return (int64_t)(2 * al256(sizeof(float) * (size_t)B * nx) + al256(sizeof(float) * (size_t)B * 7));
+  return (int64_t)(2 * al256(sizeof(float) * (size_t)B * nx) + al256(sizeof(float) * (size_t)B * kLossParts));
 }
 
 hipError_t launch_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx,
-                                float c, float dx, const float *lam, const double *pc, float *loss, float *flux_loss,
-                                float *dfe, void *ws, hipStream_t s) {
+                                float c, float dx, const float *lam, int roll, float dt, const double *pc, float *loss,
+                                float *flux_loss, float *dfe, void *ws, hipStream_t s) {
+  const int r = lam[4] > 0.f ? roll : 0;  // the rollout energy term (K <= kLossMaxRollout)
   char *p = static_cast<char *>(ws);
   float *nn = reinterpret_cast<float *>(p);
   float *En = reinterpret_cast<float *>(p + al256(sizeof(float) * (size_t)B * nx));
@@ -874,16 +921,16 @@ hipError_t launch_ablation_loss(const float *fe, const float *st, const float *f
 #endif
   if (HF_LOSS_FUSED && !poisson_uses_fft(nx) && nx <= kLossFusedMaxNx) {
     hipLaunchKernelGGL(loss_step_kernel, dim3((unsigned)B), dim3(256), (size_t)nx * (sizeof(double) + 2 * sizeof(float)),
-                       s, fe, st, ft, sn, pc, B, nx, c, lam[0], part, dfe);
+                       s, fe, st, ft, sn, pc, B, nx, c, lam[0], dt, r, part, dfe);
   } else {
     hipLaunchKernelGGL(loss_update_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, nx, c, nn);
     hipError_t e = launch_poisson(nn, nx, En, nx, pc, B, nx, HF_POISSON_SPECTRAL, s);  // detached E' (:138-145)
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(loss_terms_kernel, dim3((unsigned)B), dim3(256), 0, s, fe, st, ft, sn, nn, En, B, nx, c, lam[0],
-                       part, dfe);
+                       dt, r, part, dfe);
   }
   hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, s, part, B, nx, dx, lam[0], lam[1], lam[2], lam[3],
-                     loss, flux_loss);
+                     lam[4], r, loss, flux_loss);
   return hipGetLastError();
 }
 

@@ -88,6 +88,9 @@ SIGNATURES = {
     "hf_traj_mse": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "hf_rollout_summary": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "hf_ablation_loss_workspace_bytes": (c_int64, [c_int, c_int]),
+    "hf_ablation_loss_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p,
+                                    c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                    c_void_p]),
     "hf_ablation_loss": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "hf_chain_batch_gather": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p,

@@ -17,6 +17,8 @@ import torch
 from . import _lib
 from ._lib import HF_NUM_METRICS, HF_OP_COMPARE, HF_OP_RUN, HF_OP_STEP, check, lib, ptr
 
+LOSS_MAX_ROLLOUT = 3  # hf_ablation_loss_ex forms the rollout energy term for rollout_steps <= 3
+
 PARAM_ORDER_DOC = "input_mlp.0.{weight,bias}, update_mlps.<l>.0.{weight,bias}, edge_mlp.0.*, edge_mlp.2.*"
 
 
@@ -150,9 +152,10 @@ class Grid:
         if self.pmode == _lib.HF_POISSON_SPECTRAL:
             self.plan = pc
         else:
-            self.plan = np.empty(lib().hf_poisson_plan_size(self.pmode, self.nx), dtype=np.float64)
-            if self.plan.size < 1:
+            n = int(lib().hf_poisson_plan_size(self.pmode, self.nx))
+            if n < 1:  # (-1: unsupported; checked before allocating)
                 raise ValueError(f"{poisson} Poisson does not support nx = {self.nx}")
+            self.plan = np.empty(n, dtype=np.float64)
             check(lib().hf_poisson_plan(self.pmode, self.nx, self.length, self.plan.ctypes.data_as(c_void_p)))
         self._dev = {}
 
@@ -477,12 +480,15 @@ def adam_flat(params, grads, exp_avg, exp_avg_sq, step, done, lr, beta1, beta2, 
                                  float(lr), float(beta1), float(beta2), float(eps), stream_of(dev)))
 
 
-def ablation_loss_terms(grid, flux_edge, st, ft, sn, lam):
-    """hf_ablation_loss: the single-step terms of the reference trainer's loss
-    (scripts/training/train_ablation.py:120-170) for B samples.  flux_edge
-    [B, 2nx], st / sn [B,3,nx], ft [B,nx] device tensors; lam = (lambda_state,
-    lambda_poisson, lambda_charge, lambda_energy_one).  Returns (loss, flux
-    MSE, d loss / d flux_edge [B, 2nx])."""
+def ablation_loss_terms(grid, flux_edge, st, ft, sn, lam, rollout_steps=0, dt=None):
+    """hf_ablation_loss_ex: the reference trainer's loss (scripts/training/
+    train_ablation.py:120-206) for B samples.  flux_edge [B, 2nx], st / sn
+    [B,3,nx], ft [B,nx] device tensors; lam = (lambda_state, lambda_poisson,
+    lambda_charge, lambda_energy_one[, lambda_energy_multi]); with
+    lambda_energy_multi > 0 and 0 < rollout_steps <= 3 the rollout energy term
+    (:172-206) is formed in the same pass from the main forward's flux (no
+    further model forward reaches it; include/hybridflux.h), with time step dt
+    (default the grid's).  Returns (loss, flux MSE, d loss / d flux_edge [B, 2nx])."""
     for t, what in ((flux_edge, "flux_edge"), (st, "state_t"), (ft, "flux_t"), (sn, "state_next")):
         require_device(t, what)
     B, _, nx = st.shape
@@ -495,10 +501,12 @@ def ablation_loss_terms(grid, flux_edge, st, ft, sn, lam):
     fl = torch.empty((), device=dev)
     dfe = torch.empty(B, 2 * nx, device=dev)
     ws = torch.empty(int(lib().hf_ablation_loss_workspace_bytes(B, nx)), dtype=torch.uint8, device=dev)
-    lam_h = np.asarray(lam, dtype=np.float32)
+    lam_h = np.zeros(5, dtype=np.float32)
+    lam_h[:len(lam)] = np.asarray(lam, dtype=np.float32)
+    dt32 = float(np.float32(grid.dt if dt is None else dt))
     pc = grid.spectral_plan(dev)
     with torch.cuda.device(dev):
-        check(lib().hf_ablation_loss(ptr(fe), ptr(st), ptr(ft), ptr(sn), B, nx, grid.c32, float(np.float32(grid.dx)),
-                                     ptr(lam_h), ptr(pc), ptr(loss), ptr(fl), ptr(dfe), ptr(ws),
-                                     ws.numel(), stream_of(dev)))
+        check(lib().hf_ablation_loss_ex(ptr(fe), ptr(st), ptr(ft), ptr(sn), B, nx, grid.c32,
+                                        float(np.float32(grid.dx)), ptr(lam_h), int(rollout_steps), dt32, ptr(pc),
+                                        ptr(loss), ptr(fl), ptr(dfe), ptr(ws), ws.numel(), stream_of(dev)))
     return loss, fl, dfe

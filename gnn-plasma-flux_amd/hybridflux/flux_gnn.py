@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import engine
-from .graph_constructor import chain_edge_index, chain_tag
+from .graph_constructor import chain_tag, shared_chain_edge_index
 
 
 def _flat_view(params, dev):
@@ -152,7 +152,7 @@ class FluxGNN(nn.Module):
             B, nx = tag
             return (B, nx) if B * nx == N else None
         if edge_index.dim() == 2 and edge_index.shape[0] == 2 and edge_index.shape[1] == 2 * N and N > 0:
-            ref = chain_edge_index(N, 1, edge_index.device)
+            ref = shared_chain_edge_index(N, 1, edge_index.device)
             if torch.equal(edge_index.to(torch.long), ref):
                 return 1, N
         return None

@@ -21,12 +21,20 @@ _EI_CACHE_MAX = 4
 def chain_edge_index(nx, batch=1, device=None):
     """Edge list of `batch` disjoint periodic chains of nx cells.  Per IC b the
     2*nx edges are (i -> i+1) for i < nx, then (i+1 -> i) — the order of
-    src/graph_constructor.py:34-38 — offset by b*nx nodes.
+    src/graph_constructor.py:34-38 — offset by b*nx nodes.  A fresh tensor per
+    call (the caller may modify it in place, e.g. add a node offset)."""
+    return _chain_edge_index(nx, batch, device)
 
-    The training loop builds the same graph every step (train_ablation.py:115
-    calls build_chain_graph per sample), so the tensor of a (nx, batch, device)
-    is built once and handed out again while it is unmodified (its autograd
-    _version unchanged): eight small device launches less per step."""
+
+def shared_chain_edge_index(nx, batch=1, device=None):
+    """chain_edge_index for the package's own callers (the training loss, the
+    chain check of FluxGNN.forward), which never modify it: the tensor of a
+    (nx, batch, device) is built once and handed out again while it is
+    unmodified (its autograd _version unchanged), so the training loop, which
+    builds the same graph every step (train_ablation.py:115 calls
+    build_chain_graph per sample), saves eight small device launches per step.
+    The result is shared: do not modify it in place (an in-place edit drops its
+    chain tag and the next call builds a fresh one, but earlier holders see it)."""
     key = (int(nx), int(batch), str(torch.device(device) if device is not None else torch.device("cpu")))
     hit = _EI_CACHE.get(key)
     if hit is not None and hit[0]._version == hit[1]:

@@ -30,7 +30,7 @@ from . import engine
 from .baseline_solver import BaselineSolver
 from .config import ABLATION_CONFIGS, MODEL_CONFIG
 from .flux_gnn import FluxGNN
-from .graph_constructor import build_chain_graph_batch, chain_edge_index
+from .graph_constructor import build_chain_graph_batch, shared_chain_edge_index
 
 
 def _mse(a, b):
@@ -43,13 +43,16 @@ def _poisson_detached(grid, n):
 
 
 class _StepLoss(torch.autograd.Function):
-    """The single-step loss terms as one HIP pass (hf_ablation_loss): forward
-    returns (loss, flux_loss) and keeps d loss / d flux_edge, which backward
-    scales by the incoming gradient.  flux_loss is for reporting only."""
+    """The loss terms as one HIP pass (hf_ablation_loss_ex): forward returns
+    (loss, flux_loss) and keeps d loss / d flux_edge, which backward scales by
+    the incoming gradient.  flux_loss is for reporting only.  roll = (K,
+    lambda_energy_multi, dt) adds the rollout energy term (K <= 3), which
+    carries no gradient."""
 
     @staticmethod
-    def forward(ctx, flux_edge, st, ft, sn, grid, lam):
-        loss, fl, dfe = engine.ablation_loss_terms(grid, flux_edge, st, ft, sn, lam)
+    def forward(ctx, flux_edge, st, ft, sn, grid, lam, roll):
+        K, lam_m, dt = roll
+        loss, fl, dfe = engine.ablation_loss_terms(grid, flux_edge, st, ft, sn, tuple(lam) + (lam_m,), K, dt)
         ctx.save_for_backward(dfe)
         ctx.mark_non_differentiable(fl)
         return loss, fl
@@ -57,28 +60,41 @@ class _StepLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_fl):
         (dfe,) = ctx.saved_tensors
-        return dfe * g_loss, None, None, None, None, None
+        return dfe * g_loss, None, None, None, None, None, None
 
 
-def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0, fused=True, nf=None):
-    """Loss of train_ablation.py:107-200 for a batch: st, st_next [B,3,nx], ft [B,nx]
+def _has_rollout(cfg):
+    return cfg["rollout_steps"] > 0 and cfg["lambda_energy_multi"] > 0  # train_ablation.py:172
+
+
+def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0, fused=True, nf=None, rollout="reuse"):
+    """Loss of train_ablation.py:107-206 for a batch: st, st_next [B,3,nx], ft [B,nx]
     on the device.  Returns (loss, flux_loss); B=1 is the reference formula.
-    fused: the single-step terms (:124-170) in one HIP pass (hf_ablation_loss)
-    instead of the torch expressions below (kept as the readable statement of
-    the same arithmetic, and for the comparison test).  nf: the batch's chain
-    node features when the caller has them (FluxDataset.batch with x)."""
+    fused: the terms (:124-170, and the rollout energy term for rollout_steps
+    <= 3) in one HIP pass (hf_ablation_loss_ex) instead of the torch
+    expressions below (kept as the readable statement of the same arithmetic,
+    and for the comparison tests).  nf: the batch's chain node features when
+    the caller has them (FluxDataset.batch with x).  rollout (torch form only):
+    "reuse" runs no model forward whose result cannot reach the loss
+    (_rollout_energies), "literal" the reference's loop of rollout_steps
+    forwards (_rollout_energies_literal); the two give the same loss bit for bit."""
     B, _, nx = st.shape
     n_t, u_t = st[:, 0], st[:, 1]
     n_next_true, u_next_true, E_next_true = st_next[:, 0], st_next[:, 1], st_next[:, 2]
     if nf is None:
         nf, ei = build_chain_graph_batch(st, x)
     else:
-        ei = chain_edge_index(nx, B, st.device)
+        ei = shared_chain_edge_index(nx, B, st.device)
     flux_edge = model(nf, ei).reshape(B, 2 * nx)
     if fused and n0 == 1.0 and abs(dt / dx - grid.dt / grid.dx) <= 1e-12 * abs(dt / dx):
         lam = (cfg["lambda_state"], cfg["lambda_poisson"], cfg["lambda_charge"], cfg["lambda_energy_one"])
-        loss, flux_loss = _StepLoss.apply(flux_edge, st, ft, st_next, grid, lam)
-        return _rollout_term(model, st, x, dt, dx, cfg, grid, B, nx, loss), flux_loss
+        K = cfg["rollout_steps"] if _has_rollout(cfg) else 0
+        in_kernel = K <= engine.LOSS_MAX_ROLLOUT
+        roll = (K, cfg["lambda_energy_multi"], dt) if in_kernel else (0, 0.0, dt)
+        loss, flux_loss = _StepLoss.apply(flux_edge, st, ft, st_next, grid, lam, roll)
+        if not in_kernel:  # later energies need forwards on later states
+            loss = _add_rollout_term(loss, cfg, _rollout_energies(model, st, flux_edge, x, dt, dx, cfg, grid))
+        return loss, flux_loss
     F_pred = 0.5 * (flux_edge[:, :nx] + flux_edge[:, nx:])                        # :124-126
     flux_loss = _mse(F_pred, ft)                                                   # :129
     loss = flux_loss
@@ -98,27 +114,91 @@ def ablation_loss(model, st, ft, st_next, x, dt, dx, cfg, grid, n0=1.0, fused=Tr
         e_p = 0.5 * torch.mean(u_next_true ** 2 + E_next_pred ** 2, dim=-1)
         e_t = 0.5 * torch.mean(u_next_true ** 2 + E_next_true ** 2, dim=-1)
         loss = loss + cfg["lambda_energy_one"] * _mse(e_p, e_t)
-    return _rollout_term(model, st, x, dt, dx, cfg, grid, B, nx, loss), flux_loss
+    if _has_rollout(cfg):
+        if rollout == "literal":
+            energies = _rollout_energies_literal(model, st, x, dt, dx, cfg, grid)
+        else:
+            energies = _rollout_energies(model, st, flux_edge, x, dt, dx, cfg, grid)
+        loss = _add_rollout_term(loss, cfg, energies)
+    return loss, flux_loss
 
 
-def _rollout_term(model, st, x, dt, dx, cfg, grid, B, nx, loss):
-    """+ lambda_energy_multi * the multi-step rollout energy term (:173-205)."""
-    if cfg["rollout_steps"] > 0 and cfg["lambda_energy_multi"] > 0:               # :173-200
-        state = st.clone()
-        energies = []
-        for _ in range(cfg["rollout_steps"]):
-            n_r, u_r, E_r = state[:, 0], state[:, 1], state[:, 2]
-            energies.append(0.5 * torch.mean(u_r ** 2, dim=-1))
-            nf_r, ei_r = build_chain_graph_batch(state, x)
-            fe_r = model(nf_r, ei_r).reshape(B, 2 * nx)
+def _add_rollout_term(loss, cfg, energies):
+    """+ lambda_energy_multi * mean((energies - energies[0])^2) (:204-206)."""
+    return loss + cfg["lambda_energy_multi"] * torch.mean((energies - energies[0]) ** 2)
+
+
+def _rollout_energies_literal(model, st, x, dt, dx, cfg, grid):
+    """The rollout energies [K, B] as the reference's loop computes them
+    (:173-204): K model forwards, one per rolled state."""
+    B, _, nx = st.shape
+    state = st.clone()
+    energies = []
+    for _ in range(cfg["rollout_steps"]):
+        n_r, u_r, E_r = state[:, 0], state[:, 1], state[:, 2]
+        energies.append(0.5 * torch.mean(u_r ** 2, dim=-1))                         # :181-182
+        nf_r, ei_r = build_chain_graph_batch(state, x)
+        fe_r = model(nf_r, ei_r).reshape(B, 2 * nx)
+        F_r = 0.5 * (fe_r[:, :nx] + fe_r[:, nx:])
+        n_next_r = n_r - (dt / dx) * (F_r - torch.roll(F_r, 1, dims=-1))
+        F_u = 0.5 * u_r * u_r
+        u_next_r = u_r - (dt / dx) * (F_u - torch.roll(F_u, 1, dims=-1)) + dt * E_r
+        state = torch.stack([n_next_r, u_next_r, _poisson_detached(grid, n_next_r)], dim=1)
+    return torch.stack(energies)                                                   # [K, B]
+
+
+def _rollout_energies(model, st, flux_edge, x, dt, dx, cfg, grid):
+    """The same energies [K, B] as _rollout_energies_literal, bit for bit, with
+    only the forwards whose results reach them.  The energy of step k is
+    0.5 mean(u_k^2) (:181) and u_{k+1} needs E_k (:196), which for k >= 1 is
+    the detached Poisson E of the n_k that forward k-1 produced (:191, :198-
+    200).  So the energies reach forwards 0 .. K-3 only, forward 0 is the main
+    forward (the same model on the same state: its flux_edge is reused), and
+    the others run untaped (no_grad: nothing differentiates through them — u
+    never depends on the parameters).  For the reference's K = 3: no forward."""
+    B, _, nx = st.shape
+    K = cfg["rollout_steps"]
+    n_r, u_r, E_r = st[:, 0], st[:, 1], st[:, 2]
+    fe_r = flux_edge.detach()
+    energies = []
+    for k in range(K):
+        energies.append(0.5 * torch.mean(u_r ** 2, dim=-1))
+        if k == K - 1:
+            break
+        F_u = 0.5 * u_r * u_r
+        u_next = u_r - (dt / dx) * (F_u - torch.roll(F_u, 1, dims=-1)) + dt * E_r
+        n_next = E_next = None
+        if k + 2 <= K - 1:  # E_{k+1} feeds u_{k+2}, the last energy's u at k + 2 = K - 1
+            if fe_r is None:
+                with torch.no_grad():
+                    nf_r, ei_r = build_chain_graph_batch(torch.stack([n_r, u_r, E_r], dim=1), x)
+                    fe_r = model(nf_r, ei_r).reshape(B, 2 * nx)
             F_r = 0.5 * (fe_r[:, :nx] + fe_r[:, nx:])
-            n_next_r = n_r - (dt / dx) * (F_r - torch.roll(F_r, 1, dims=-1))
-            F_u = 0.5 * u_r * u_r
-            u_next_r = u_r - (dt / dx) * (F_u - torch.roll(F_u, 1, dims=-1)) + dt * E_r
-            state = torch.stack([n_next_r, u_next_r, _poisson_detached(grid, n_next_r)], dim=1)
-        energies = torch.stack(energies)                                           # [K, B]
-        loss = loss + cfg["lambda_energy_multi"] * torch.mean((energies - energies[0]) ** 2)
-    return loss
+            n_next = n_r - (dt / dx) * (F_r - torch.roll(F_r, 1, dims=-1))
+            E_next = _poisson_detached(grid, n_next)
+        fe_r = None
+        n_r, u_r, E_r = n_next, u_next, E_next
+    return torch.stack(energies)
+
+
+def train_flop_per_sample(cfg, nx=64, H=128, L=4, F=4):
+    """Algorithmic FLOPs of one sample of the training step with the ablation
+    config `cfg` (a dict of ABLATION_CONFIGS or its name): FluxGNN forward +
+    backward (P/Q-split readout, as the inference count of SURVEY.md 8d):
+    forward 329,216 per cell (input 2FH, layers L*2*2H*H, readout 2*H*2H +
+    2 edges * 2H), backward = data gradients (layers L*2*2H*H, readout 2*2H*H)
+    + weight gradients (the same GEMM sizes, plus the input layer's 2FH).  The
+    rollout energy term ('full', 'rollout_only') adds only the forwards whose
+    results reach the loss, none for the reference's rollout_steps = 3
+    (_rollout_energies; the reference's own loop runs 3 forwards there, of
+    which none is needed), and no backward (the term has no gradient).  The
+    loss terms' elementwise FV updates and detached Poisson solves are not counted."""
+    if isinstance(cfg, str):
+        cfg = ABLATION_CONFIGS[cfg]
+    fwd = 2 * F * H + L * 2 * 2 * H * H + 2 * H * 2 * H + 2 * 2 * H
+    bwd = (L * 2 * 2 * H * H + 2 * 2 * H * H) * 2 + 2 * F * H
+    extra = max(0, cfg["rollout_steps"] - 3) if _has_rollout(cfg) else 0
+    return ((fwd + bwd) + extra * fwd) * nx
 
 
 class FluxDataset:
@@ -133,10 +213,24 @@ class FluxDataset:
     def __len__(self):
         return self.N
 
-    def batch(self, idx, x=None):
+    def check_indices(self, idx):
+        """IndexError unless every index lies in [-N, N) (torch indexing's
+        range; one host sync)."""
+        idx = torch.as_tensor(idx)
+        if idx.numel() and (int(idx.min()) < -self.N or int(idx.max()) >= self.N):
+            raise IndexError(f"sample index out of range for a dataset of {self.N} samples")
+
+    def batch(self, idx, x=None, check=True):
         """(state_t, flux_t, state_next)[idx]; with x (the grid positions [nx])
         also the batch's chain node features, all four from one HIP pass
-        (engine.chain_batch): (st, ft, sn, node_features)."""
+        (engine.chain_batch): (st, ft, sn, node_features).  Indices outside
+        [-N, N) raise IndexError as the reference's dataset indexing does
+        (check_indices: a host sync); check=False skips that for indices the
+        caller has already checked (train_steps checks a pass's order once),
+        and then the device gather clamps an out-of-range index to [0, N)
+        instead of raising (include/hybridflux.h hf_chain_batch_gather)."""
+        if check:
+            self.check_indices(idx)
         if x is None:
             return self.state_t[idx], self.flux_t[idx], self.state_next[idx]
         return engine.chain_batch(idx, self.state_t, self.flux_t, self.state_next, x)
@@ -191,6 +285,10 @@ class FlatAdam(torch.optim.Optimizer):
             b1, b2 = group["betas"]
             engine.adam_flat(flat, g, st["exp_avg"], st["exp_avg_sq"], st["step"], st["done"], group["lr"],
                              b1, b2, group["eps"])
+            # the kernel wrote the parameters behind autograd's back: bump their
+            # version counters as an in-place torch update would, so that a packed
+            # inference copy (FluxGNN.device_model keys on _version) is rebuilt
+            torch.autograd.graph.increment_version(ps)
         return loss
 
 
@@ -214,7 +312,7 @@ class GraphedStep:
 
     def _body(self):
         model, opt, data, x, dt, dx, cfg, grid = self.args
-        st, ft, sn, nf = data.batch(self.idx, x)
+        st, ft, sn, nf = data.batch(self.idx, x, check=False)  # (train_steps checked the order)
         loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid, nf=nf)
         opt.zero_grad(set_to_none=True)
         loss.backward()
@@ -234,6 +332,9 @@ class GraphedStep:
         if self.graph is None:
             return self._body()
         self.graph.replay()
+        # the replayed optimizer step changed the parameters without a host-side
+        # in-place op: bump their versions (FluxGNN.device_model keys on them)
+        torch.autograd.graph.increment_version(list(self.args[0].parameters()))
         return self.out[0].clone(), self.out[1].clone()
 
 
@@ -245,6 +346,7 @@ def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid, graph
     it is captured and every further full batch replays the graph."""
     tot, tot_flux, steps = 0.0, 0.0, 0
     losses = []
+    data.check_indices(order)  # once per pass; the steps gather with check=False
     for b0 in range(0, len(order), batch_size):
         idx = order[b0:b0 + batch_size]
         if graphed is not None and len(idx) == batch_size:
@@ -261,7 +363,7 @@ def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid, graph
             else:
                 loss, flux_loss = graphed(idx)
         else:
-            st, ft, sn, nf = data.batch(idx, x)
+            st, ft, sn, nf = data.batch(idx, x, check=False)
             loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid, nf=nf)
             opt.zero_grad()
             loss.backward()

@@ -182,6 +182,28 @@ int hf_ablation_loss(const float *dev_flux_edge, const float *dev_state_t, const
                      void *dev_workspace, int64_t workspace_bytes, void *stream);
 
 /*
+ * Replaces: the whole per-sample loss of the reference trainer, the
+ * multi-step rollout energy term included (scripts/training/
+ * train_ablation.py:120-206, the 'full' and 'rollout_only' configs).
+ * hf_ablation_loss plus lam[4] = lambda_energy_multi and rollout_steps = K,
+ * dt = f32(dt): adds lam[4] * mean_{k<K, b} (e_k - e_0)^2, e_k = 0.5 mean(u_k^2)
+ * (:172-206), when K > 0 and lam[4] > 0.  The energies use u_0..u_{K-1} only,
+ * and u is advanced with the sample's E (k = 0) and then the detached Poisson
+ * E of the previous n (:193-200); for K <= 3 that is u_0, u_1 and u_2 with E_1
+ * = E(n') of the main forward's n' (the rollout's first forward is the same
+ * model on the same state), so no further model forward reaches the loss and
+ * the term is formed here from the inputs alone.  It carries no gradient (u
+ * does not depend on the parameters), so dev_dflux_edge is hf_ablation_loss's.
+ * K > 3 with lam[4] > 0 is HF_EUNSUPPORTED (later energies need forwards on
+ * later states: pass lam[4] = 0 and add the term from them).  hf_ablation_loss
+ * is this call with lam[4] = 0, K = 0.  Same workspace.
+ */
+int hf_ablation_loss_ex(const float *dev_flux_edge, const float *dev_state_t, const float *dev_flux_t,
+                        const float *dev_state_next, int B, int nx, float c, float dx, const float *lam,
+                        int rollout_steps, float dt, const double *dev_c, float *dev_loss, float *dev_flux_loss,
+                        float *dev_dflux_edge, void *dev_workspace, int64_t workspace_bytes, void *stream);
+
+/*
  * Replaces: one training batch of the reference trainer (its dataset of
  * (state_t, flux_t, state_next) triples indexed by a DataLoader batch,
  * scripts/training/train_ablation.py:27-44) and the batch's chain node

@@ -220,6 +220,39 @@ def test_trainer_entry_points_validate_before_device():
     assert lib.hf_adam_flat(None, None, None, None, 0, None, None, 1e-3, 0.9, 0.999, 1e-8, None) == _lib.HF_OK
 
 
+def test_ablation_loss_ex_validates_before_device():
+    """hf_ablation_loss_ex refuses a negative rollout_steps, and rollout_steps
+    > 3 with lambda_energy_multi > 0 (later energies need model forwards), before
+    any HIP call (runs without a GPU)."""
+    import numpy as np
+    lib = _lib.lib()
+    d = ctypes.c_void_p(1)
+    ws = int(lib.hf_ablation_loss_workspace_bytes(4, 64))
+    lam = np.array([1.0, 0.1, 0.1, 0.05, 0.05], dtype=np.float32)
+    lp = lam.ctypes.data_as(ctypes.c_void_p)
+    assert lib.hf_ablation_loss_ex(d, d, d, d, 4, 64, 0.1, 0.1, lp, -1, 5e-3, d, d, d, d, d, ws, None) == _lib.HF_EINVAL
+    assert lib.hf_ablation_loss_ex(d, d, d, d, 4, 64, 0.1, 0.1, lp, 4, 5e-3, d, d, d, d, d, ws,
+                                   None) == _lib.HF_EUNSUPPORTED
+    assert lib.hf_ablation_loss_ex(d, d, d, d, 4, 64, 0.1, 0.1, lp, 3, 5e-3, d, d, d, d, d, ws - 1,
+                                   None) == _lib.HF_EINVAL
+    assert lib.hf_ablation_loss(d, d, d, d, 4, 64, 0.1, 0.1, None, d, d, d, d, d, ws, None) == _lib.HF_EINVAL
+
+
+def test_train_flop_model_counts_no_redundant_forwards():
+    """The training FLOP model is algorithmic: 'full' / 'rollout_only' cost one
+    forward + backward per sample like 'physics' (their 3 rollout forwards
+    reach no energy); a 5-step rollout adds 2 forwards."""
+    from hybridflux.config import ABLATION_CONFIGS
+    from hybridflux.training import train_flop_per_sample
+    fwd = 329_216
+    base = train_flop_per_sample("physics") // 64
+    assert base == fwd + (4 * 2 * 256 * 128 + 2 * 256 * 128) * 2 + 2 * 4 * 128
+    for name in ("baseline", "full", "rollout_only"):
+        assert train_flop_per_sample(name) == train_flop_per_sample("physics")
+    k5 = dict(ABLATION_CONFIGS["full"], rollout_steps=5)
+    assert train_flop_per_sample(k5) == train_flop_per_sample("full") + 2 * fwd * 64
+
+
 def test_workspace_need_classical():
     """hf_workspace_need is a host-side size query: exact per path, -1 on bad arguments."""
     from hybridflux._lib import HF_OP_COMPARE, HF_OP_RUN, HF_OP_STEP

@@ -60,18 +60,24 @@ def test_build_chain_graph_matches_reference_layout():
 
 
 def test_chain_edge_index_cache_is_safe():
-    """chain_edge_index hands out the tensor of a (nx, batch, device) again only
-    while it is unmodified: an in-place edit drops the tag and the next call
-    builds a fresh, correct edge index."""
-    from hybridflux.graph_constructor import chain_edge_index, chain_tag
-    a = chain_edge_index(7, 3)
-    assert chain_edge_index(7, 3) is a and chain_tag(a) == (3, 7)
+    """The public chain_edge_index returns a fresh tensor per call (a caller may
+    edit it in place); the package's shared_chain_edge_index hands out the
+    tensor of a (nx, batch, device) again only while it is unmodified: an
+    in-place edit drops the tag and the next call builds a fresh, correct one."""
+    from hybridflux.graph_constructor import chain_edge_index, chain_tag, shared_chain_edge_index
+    p = chain_edge_index(7, 3)
+    q = chain_edge_index(7, 3)
+    assert p is not q and chain_tag(p) == (3, 7) and torch.equal(p, O.chain_edges(7, 3))
+    p[0, 0] = 5
+    assert torch.equal(q, O.chain_edges(7, 3)) and chain_tag(q) == (3, 7)
+    a = shared_chain_edge_index(7, 3)
+    assert shared_chain_edge_index(7, 3) is a and chain_tag(a) == (3, 7)
     assert torch.equal(a, O.chain_edges(7, 3))
-    a[0, 0] = 5  # a caller edits its copy in place
+    a[0, 0] = 5  # a caller edits the shared tensor in place
     assert chain_tag(a) is None
-    b = chain_edge_index(7, 3)
+    b = shared_chain_edge_index(7, 3)
     assert b is not a and chain_tag(b) == (3, 7) and torch.equal(b, O.chain_edges(7, 3))
-    assert chain_edge_index(7, 4) is not b  # another batch size, another tensor
+    assert shared_chain_edge_index(7, 4) is not b  # another batch size, another tensor
 
 
 def test_cpu_inputs_raise_no_fallback():

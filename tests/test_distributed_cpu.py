@@ -167,3 +167,58 @@ def test_bench_group_setup_times_out_without_peer():
     res = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT")]
     assert res and "joined" not in res[0], (p.stdout[-1000:], p.stderr[-2000:])
     assert float(res[0].split()[-1]) < 60, res
+
+
+BENCH_RANK_SCRIPT = r"""
+import json, os, sys, time
+sys.path.insert(0, {root!r}); sys.argv = ["bench.py"]
+import torch, torch.distributed as dist
+import bench
+from hybridflux.rollout import COLLECTIVES, gather_ic_rows_packed, reset_collective_stats, shard_bounds
+world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+bench.init_group("gloo", world, torch.device("cpu"))
+n_total, T = {n_total}, {T}
+lo, hi = shard_bounds(n_total, world, rank)
+# the shapes bench.py gathers: metric series [b, T+1, 4] and summaries [b, 8]
+met = torch.arange(lo * (T + 1) * 4, hi * (T + 1) * 4, dtype=torch.float32).reshape(-1, T + 1, 4)
+summ = torch.arange(lo * 8, hi * 8, dtype=torch.float32).reshape(-1, 8)
+reset_collective_stats()
+g_met, g_summ = gather_ic_rows_packed([met, summ], n_total)
+coll = dict(COLLECTIVES)
+ranks = bench.rank_report(0.5 + 0.25 * rank, hi - lo)
+assert torch.equal(g_met, torch.arange(n_total * (T + 1) * 4, dtype=torch.float32).reshape(n_total, T + 1, 4))
+if rank == 0:
+    print(json.dumps({{"collective": bench.collective_entry(coll, world, 0.0), "ranks": ranks}}), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_bench_four_rank_gloo_line_checks_itself(tmp_path):
+    """4 gloo ranks started torchrun-style (as the driver
+    starts bench.py) run bench.py's own end-of-rollout exchange and reporting
+    (gather_ic_rows_packed, bench.rank_report, bench.collective_entry) on the
+    shapes of a 4 x 1024-IC job: rank 0's record says world_size 4, ONE call,
+    4 x the per-rank payload received, and every rank's wall and IC count.
+    (The GPU twin, tests/test_gpu_distributed.py::test_bench_self_launches_ranks,
+    runs the whole bench.py with 4 ranks on one GPU.)"""
+    import json
+    import subprocess
+    import sys
+    n_total, T = 4096, 4
+    script = tmp_path / "rank.py"
+    script.write_text(BENCH_RANK_SCRIPT.format(root=ROOT, n_total=n_total, T=T))
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "gnn-plasma-flux_amd") + os.pathsep + ROOT)
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(script)],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    c = d["collective"]
+    payload = (n_total // 4) * ((T + 1) * 4 + 8) * 4
+    assert c["backend"] == "gloo" and c["world_size"] == 4 and c["calls"] == 1
+    assert c["bytes_sent_per_rank"] == payload and c["bytes_received_per_rank"] == 4 * payload
+    r = d["ranks"]
+    assert r["ics_per_rank"] == [1024] * 4
+    assert r["wall_s_per_rank"] == [0.5, 0.75, 1.0, 1.25] and r["wall_s_max"] == 1.25 and r["wall_s_min"] == 0.5

@@ -67,17 +67,25 @@ def test_two_ranks_equal_one_rank_bitwise(tmp_path):
 
 @pytest.mark.timeout(400)
 def test_bench_self_launches_ranks():
-    """`python bench.py --gpus 2` without a launcher starts 2 ranks itself."""
-    p = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-              "--steps", "4", "--warmup", "2", "--no-cpu-baseline", "--no-other-configs", "--also", ""], 300)
+    """`python bench.py --gpus 4` without a launcher starts 4 ranks itself (gloo,
+    sharing this box's one GPU); rank 0's line checks itself: world_size 4, ONE
+    packed exchange moving 4 x the per-rank payload, and every rank's wall
+    time and IC count."""
+    p = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--dist-backend", "gloo",
+              "--steps", "4", "--warmup", "2", "--ics-per-gpu", "1024", "--no-cpu-baseline", "--no-other-configs",
+              "--also", ""], 300)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_ics"] == 8192 and d["config"]["ics_per_gpu"] == 4096
+    assert d["n_gpus"] == 4 and d["config"]["global_ics"] == 4096 and d["config"]["ics_per_gpu"] == 1024
     assert d["finite_fraction"] == 1.0 and d["value"] > 0
     c = d["config"]["collective"]
-    assert c["backend"] == "gloo" and c["world_size"] == 2 and c["calls"] == 1  # metrics + summaries packed
-    assert c["bytes_received_per_rank"] == 2 * c["bytes_sent_per_rank"] == 2 * 4096 * (5 * 4 + 8) * 4
+    assert c["backend"] == "gloo" and c["world_size"] == 4 and c["calls"] == 1  # metrics + summaries packed
+    assert c["bytes_received_per_rank"] == 4 * c["bytes_sent_per_rank"] == 4 * 1024 * (5 * 4 + 8) * 4
+    r = d["config"]["ranks"]
+    assert r["ics_per_rank"] == [1024] * 4 and len(r["wall_s_per_rank"]) == 4
+    assert r["wall_s_min"] <= r["wall_s_max"] and abs(d["ms_per_step"] - r["wall_s_max"] / 4 * 1e3) < 1e-3
+    assert abs(d["value"] - 4096 * 4 / r["wall_s_max"]) <= 1e-6 * d["value"] + 0.1
 
 
 N_CASES = 3  # dist_rollout_worker.CASES

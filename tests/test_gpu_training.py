@@ -515,3 +515,128 @@ def test_loss_terms_any_nx(hf, nx):
     assert abs(out[0][0] - out[1][0]) <= 2e-6 * abs(out[1][0])
     assert abs(out[0][1] - out[1][1]) <= 2e-6 * abs(out[1][1])
     torch.testing.assert_close(out[0][2], out[1][2], rtol=1e-5, atol=1e-10)
+
+
+def _rollout_cfgs(hf):
+    k5 = dict(hf.ABLATION_CONFIGS["full"], rollout_steps=5)  # energies reach forwards 1 and 2
+    return {"full": hf.ABLATION_CONFIGS["full"], "rollout_only": hf.ABLATION_CONFIGS["rollout_only"], "full_k5": k5}
+
+
+@pytest.mark.parametrize("cfg_name", ["full", "rollout_only", "full_k5"])
+def test_rollout_term_without_redundant_forwards_bitwise(hf, cfg_name):
+    """The rollout energy term with only the forwards that reach an energy
+    (ablation_loss rollout='reuse': forward 0 is the main forward, reused;
+    none more for the reference's rollout_steps = 3; forwards 1..K-3 untaped
+    otherwise) equals the reference's literal loop of rollout_steps taped
+    forwards (train_ablation.py:172-206, rollout='literal') bit for bit: loss,
+    flux loss and every parameter gradient, on 48 samples."""
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import ablation_loss
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=3, steps_per_ic=16, out_path=None, device=DEV)
+    st, ft, sn = (torch.as_tensor(a, device=DEV) for a in (st, ft, sn))
+    solver = hf.BaselineSolver(64, device=DEV)
+    xd = torch.as_tensor(x, device=DEV)
+    cfg = _rollout_cfgs(hf)[cfg_name]
+    m = _w1_model(hf)
+    out = []
+    for mode in ("literal", "reuse"):
+        m.zero_grad()
+        loss, fl = ablation_loss(m, st, ft, sn, xd, solver.dt, solver.dx, cfg, solver.grid, fused=False,
+                                 rollout=mode)
+        loss.backward()
+        out.append((loss.item(), fl.item(), {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}))
+    assert out[0][0] == out[1][0] and out[0][1] == out[1][1]
+    for k in out[0][2]:
+        assert np.array_equal(out[0][2][k], out[1][2][k]), k
+
+
+@pytest.mark.parametrize("cfg_name", ["full", "rollout_only", "full_k5"])
+def test_fused_rollout_term_vs_literal(hf, cfg_name):
+    """hf_ablation_loss_ex (the rollout energy term formed in the loss pass from
+    the main forward's flux, K <= 3; for K = 5 the term from the reuse form's
+    two untaped forwards) against the literal 3-forward torch loss: loss within
+    2e-6 relative (the kernels' fixed-order sums vs torch's reductions), the
+    gradients (the term has none) as the single-step comparison's."""
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import ablation_loss
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=3, steps_per_ic=16, out_path=None, device=DEV)
+    st, ft, sn = (torch.as_tensor(a, device=DEV) for a in (st, ft, sn))
+    solver = hf.BaselineSolver(64, device=DEV)
+    xd = torch.as_tensor(x, device=DEV)
+    cfg = _rollout_cfgs(hf)[cfg_name]
+    m = _w1_model(hf)
+    out = []
+    for fused in (True, False):
+        m.zero_grad()
+        loss, fl = ablation_loss(m, st, ft, sn, xd, solver.dt, solver.dx, cfg, solver.grid, fused=fused,
+                                 rollout="literal")
+        loss.backward()
+        out.append((loss.item(), fl.item(), {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}))
+    assert abs(out[0][0] - out[1][0]) <= 2e-6 * abs(out[1][0])
+    assert abs(out[0][1] - out[1][1]) <= 2e-6 * abs(out[1][1])
+    for k in out[0][2]:
+        grads_close(out[0][2][k], out[1][2][k], 1e-5)
+    # the term is really there: the same loss without it differs
+    base = dict(cfg, lambda_energy_multi=0.0)
+    with torch.no_grad():
+        l0, _ = ablation_loss(m, st, ft, sn, xd, solver.dt, solver.dx, base, solver.grid)
+    assert l0.item() != out[0][0]
+
+
+def test_flat_adam_invalidates_packed_inference_weights(hf):
+    """FlatAdam writes the parameters through a HIP kernel; it bumps their
+    version counters, so a no-grad forward after an optimizer step (eager or a
+    replayed HIP graph) uses the new weights, not the packed copy made before
+    (ADVICE r05)."""
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import FlatAdam, FluxDataset, GraphedStep, train_steps
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=2, steps_per_ic=16, out_path=None, device=DEV)
+    data = FluxDataset(st, ft, sn, DEV)
+    solver = hf.BaselineSolver(64, device=DEV)
+    xd = torch.as_tensor(x, device=DEV)
+    cfg = hf.ABLATION_CONFIGS["physics"]
+    nf, ei = hf.build_chain_graph_batch(data.state_t[:4], xd)
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        m = hf.FluxGNN(4, 128, 4).to(DEV).flatten_parameters_()
+        opt = FlatAdam(m.parameters(), lr=1e-3)
+        gs = GraphedStep(m, opt, data, 8, xd, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
+        if graphed:  # 3 eager warmup steps, the capture and a replay
+            train_steps(m, opt, data, torch.arange(32, device=DEV) % len(data), 8, xd, solver.dt, solver.dx, cfg,
+                        solver.grid, graphed=gs)
+            assert gs.graph is not None
+        with torch.no_grad():
+            before = m(nf, ei).clone()  # packs the current weights
+        # one more step: eager FlatAdam, or a replay of the captured step only
+        train_steps(m, opt, data, torch.arange(8, device=DEV) % len(data), 8, xd, solver.dt, solver.dx, cfg,
+                    solver.grid, graphed=gs)
+        with torch.no_grad():
+            after = m(nf, ei)
+            fresh = hf.FluxGNN(4, 128, 4).to(DEV)
+            fresh.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
+            want = fresh(nf, ei)
+        assert not torch.equal(before, after)
+        assert torch.equal(after, want)
+
+
+def test_dataset_batch_rejects_out_of_range_indices(hf):
+    """FluxDataset.batch raises IndexError outside [-N, N), as the reference's
+    dataset indexing does (the device gather would clamp); train_steps checks
+    a pass's order once."""
+    from hybridflux.training import FluxDataset, train_steps
+    g = torch.Generator().manual_seed(2)
+    N, nx = 5, 64
+    data = FluxDataset(torch.randn(N, 3, nx, generator=g).numpy(), torch.randn(N, nx, generator=g).numpy(),
+                       torch.randn(N, 3, nx, generator=g).numpy(), DEV)
+    x = torch.linspace(0, 1, nx, device=DEV)
+    data.batch(torch.tensor([-N, N - 1], device=DEV), x)
+    for bad in ([N], [-N - 1], [0, 7]):
+        with pytest.raises(IndexError):
+            data.batch(torch.tensor(bad, device=DEV), x)
+        with pytest.raises(IndexError):
+            data.batch(torch.tensor(bad, device=DEV))
+    m = hf.FluxGNN(4, 128, 4).to(DEV)
+    solver = hf.BaselineSolver(nx, device=DEV)
+    with pytest.raises(IndexError):
+        train_steps(m, torch.optim.Adam(m.parameters()), data, torch.tensor([0, 9], device=DEV), 2, x, solver.dt,
+                    solver.dx, hf.ABLATION_CONFIGS["physics"], solver.grid)

@@ -26,20 +26,10 @@ sys.path.insert(0, ROOT)
 
 
 def flop_per_sample(cfg_name, nx=64, H=128, L=4, F=4):
-    """Algorithmic FLOPs of one sample's FluxGNN forward + backward in the
-    training step (P/Q-split readout, as the inference count of SURVEY.md 8d):
-    forward 329,216 per cell (input 2FH, layers L*2*2H*H, readout 2*H*2H +
-    2 edges * 2H), backward = data gradients (layers L*2*2H*H, readout 2*2H*H)
-    + weight gradients (the same GEMM sizes, plus the input layer's 2FH).  The
-    'full' and 'rollout_only' configs run the model on rollout_steps more
-    states per sample, each with its backward.  The loss terms' elementwise FV
-    updates and the detached Poisson solves are not counted."""
-    from hybridflux.config import ABLATION_CONFIGS
-    fwd = 2 * F * H + L * 2 * 2 * H * H + 2 * H * 2 * H + 2 * 2 * H
-    bwd = (L * 2 * 2 * H * H + 2 * 2 * H * H) * 2 + 2 * F * H
-    cfg = ABLATION_CONFIGS[cfg_name]
-    evals = 1 + (cfg["rollout_steps"] if cfg["lambda_energy_multi"] > 0 else 0)
-    return evals * (fwd + bwd) * nx
+    """hybridflux.training.train_flop_per_sample (the algorithmic count: the
+    rollout term's redundant forwards are not counted)."""
+    from hybridflux.training import train_flop_per_sample
+    return train_flop_per_sample(cfg_name, nx, H, L, F)
 
 
 def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False, fused_adam=False, warm_s=0.3):
