@@ -468,6 +468,11 @@ struct CoreBF16 {
   // MFMAs of readout unit U of one output tile: fragment i = 2*(kb - 2U) + (P|Q), kb = 2U, 2U+1.
   template <int MT, int U>
   static __device__ __forceinline__ void ro_mfma(const u4 (&w)[4], const Acts<MT> &X, f4 (&P)[MT], f4 (&Q)[MT]) {
+#ifdef HF_DIAG_NOROMFMA  // timing diagnostic only: results are wrong (readout fragments read, no readout MFMA)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(w[i]));
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kb = 2 * U + (i >> 1);
@@ -646,7 +651,12 @@ struct CoreBF16 {
         const f4 bias = ldf4(S.bin + 16 * nt + g4);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
+#ifdef HF_DIAG_NOINMFMA  // timing diagnostic only: results are wrong (no input-layer MFMA)
+          asm volatile("" ::"v"(aw), "v"(bx[mt]));
+          const f4 h = relu4(bias);
+#else
           const f4 h = relu4(mma(aw, bx[mt], bias));
+#endif
           X.h[mt][kb][2 * t] = pk_bf16(h[0], h[1]);
           X.h[mt][kb][2 * t + 1] = pk_bf16(h[2], h[3]);
           if (kb == kKB - 1) h67[mt][t] = h;
