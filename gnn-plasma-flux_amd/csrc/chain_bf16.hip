@@ -753,6 +753,9 @@ __global__ __launch_bounds__(64 * Core::kNW, 1) void chain_flux_sw_kernel(ChainW
   Seam sm{lds4 + kBaseF4 + Seam::slot(R.wave, 0), lds4 + kBaseF4 + Seam::slot((R.wave + NW - 1) % NW, 1),
           lds4 + kBaseF4 + Seam::slot((R.wave + 1) % NW, 0), 0};
   __syncthreads();  // small weights staged (no DMA in flight yet)
+#ifdef HF_EXP_PRIO_HI  // experiment: static issue priority 1 for the second-dispatched half (waves 4-7)
+  if (R.wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   R.prime(R.chunks - 1);  // the pass starts two units before chunk 0 (Core::pos)
   typename Core::Feed F;
   Core::begin(R, F);
