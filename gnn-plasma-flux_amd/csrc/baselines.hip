@@ -259,12 +259,33 @@ struct PinnRows {
 // bias comes from LDS too (copied there once: a global bias load would be sunk
 // into the store's branch and waited for there behind the next layer's
 // k-blocks, vmcnt being in order).
-template <int K, int NTILES, int ACT, int KBN, int NT>
+// SPLIT (the last layer when its NTILES = 1.5 kPinnWaves tiles, the reference's
+// PINN(192, 256): 12 tiles over 8 waves): instead of a second, clamped tile
+// that waves 4-7 computed and dropped (a third of their MFMAs), wave w takes
+// its own tile w whole (j = 0) and half the k-blocks of remainder tile
+// kPinnWaves + w % R (j = 1, R = NTILES - kPinnWaves): waves R.. the first
+// half, waves 0..R-1 the second, so every wave issues 1.5 tiles of MFMAs.  A
+// first-half wave publishes its partial sums in LDS (sp) as soon as its half is
+// done, then a flag word (release, workgroup scope); the second-half wave adds
+// them (acquire on the flag, tag = step + 1) in its epilogue:
+// out = state + ((lo + hi) + b).
+struct PinnSplit {
+  f4v *sp;     // [R][64] partial sums of the first halves
+  int *flag;   // [R] step tag of the partial in sp
+  int tag;     // this step's tag (t + 1)
+};
+template <int K, int NTILES, int ACT, int KBN, int NT, bool SPLIT = false>
 __device__ __forceinline__ void pinn_layer(const PinnRows<NT> &wrow, const float *bias, const float *in, float *out,
                                            int wave, int lane, f4v (&wq)[kPinnAhead][NT],
-                                           const PinnRows<NT> &nrow) {
+                                           const PinnRows<NT> &nrow, const PinnSplit &spl = PinnSplit{}) {
   constexpr int KB = K / 16, P = kPinnAhead;
   static_assert(KB % P == 0 && KBN >= P - 1, "a layer's k-blocks fill whole rounds of the ring");
+  static_assert(!SPLIT || (ACT == 1 && NT == 2 && 2 * (NTILES - kPinnWaves) == kPinnWaves && KB % 2 == 0),
+                "split last layer: 1.5 tiles per wave");
+  constexpr int R = NTILES - kPinnWaves;
+  // SPLIT: j = 1 runs k-blocks [k1lo, k1lo + KB/2) of this wave (wave-uniform)
+  const int k1lo = SPLIT ? (wave >= R ? 0 : KB / 2) : 0;
+  auto on1 = [&](int kb) { return !SPLIT || (kb >= k1lo && kb < k1lo + KB / 2); };
   f4v acc[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
@@ -276,23 +297,42 @@ __device__ __forceinline__ void pinn_layer(const PinnRows<NT> &wrow, const float
     const int s = c + kAhead;  // slot s % P held k-block c - 1, consumed last iteration
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      if (s < KB)
-        wq[s % P][j] = *reinterpret_cast<const f4v *>(wrow.p[j] + 256 * s);
-      else
+      if (s < KB) {
+        if (j == 0 || on1(s)) wq[s % P][j] = *reinterpret_cast<const f4v *>(wrow.p[j] + 256 * s);
+      } else {
         wq[s % P][j] = *reinterpret_cast<const f4v *>(nrow.p[j] + 256 * (s - KB));
+      }
     }
     f4v bn = bv;
     if (c + 1 < KB) bn = *reinterpret_cast<const f4v *>(in + (c + 1) * 256 + lane * 4);
+    const bool use1 = on1(c);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j], 0, 0, 0);
+      for (int j = 0; j < NT; ++j)
+        if (j == 0 || use1) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(wq[c % P][j][e], bv[e], acc[j], 0, 0, 0);
     bv = bn;
+    if constexpr (SPLIT) {
+      if (c == KB / 2 - 1 && wave >= R) {  // the first half of remainder tile kPinnWaves + wave % R is done
+        spl.sp[(wave - R) * 64 + lane] = acc[1];
+        __hip_atomic_store(spl.flag + (wave - R), spl.tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
+  }
+  if constexpr (SPLIT) {
+    if (wave < R) {  // remainder tile kPinnWaves + wave: lo (published) + hi (acc[1])
+      while (__hip_atomic_load(spl.flag + wave, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != spl.tag)
+        __builtin_amdgcn_s_sleep(1);
+      const f4v lo = spl.sp[wave * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[1][i] = __fadd_rn(lo[i], acc[1][i]);
+    }
   }
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    const int t = wave + kPinnWaves * j;
+    const int t = SPLIT && j == 1 ? kPinnWaves + wave % R : wave + kPinnWaves * j;
+    if (SPLIT && j == 1 && wave >= R) break;  // (its half went to the second-half wave)
     if (NTILES % kPinnWaves != 0 && t >= NTILES) break;
     float *o = out + t * 256 + lane * 4;
     const f4v bq = *reinterpret_cast<const f4v *>(bias + 16 * t + 4 * (lane >> 4));
@@ -328,6 +368,14 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
   __shared__ f4v s_state4[D * kPinnIcs / 4];
   __shared__ f4v s_act4[2][H * kPinnIcs / 4];
   __shared__ f4v s_bias4[kMaxChainLayers * H / 4];  // layer l's bias at l * H
+  // the split last layer's partial sums and flags (PinnSplit)
+#ifdef HF_EXP_PINN_NOSPLIT  // A/B: the clamped spare tile of round 5
+  constexpr bool kSplit = false;
+#else
+  constexpr bool kSplit = 2 * (D / 16 - kPinnWaves) == kPinnWaves && NT == 2 && (H / 16) % 2 == 0;
+#endif
+  __shared__ f4v s_part[kSplit ? (D / 16 - kPinnWaves) * 64 : 1];
+  __shared__ int s_flag[kSplit ? D / 16 - kPinnWaves : 1];
   float *s_state = reinterpret_cast<float *>(s_state4);
   float *const act0 = reinterpret_cast<float *>(s_act4[0]), *const act1 = reinterpret_cast<float *>(s_act4[1]);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -342,6 +390,7 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
     if (traj && b0 + n < B) traj[b * ldt + d] = v;
   }
   const int L = w.L;
+  if (kSplit && tid < D / 16 - kPinnWaves) s_flag[tid] = 0;
   float *const s_bias = reinterpret_cast<float *>(s_bias4);
   for (int l = 0; l < L; ++l)
     for (int i = tid; i < (l == L - 1 ? D : H); i += NTH) s_bias[l * H + i] = w.b[l][i];
@@ -352,7 +401,8 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
     PinnRows<NT> r;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      const int t = wave + kPinnWaves * j;
+      int t = wave + kPinnWaves * j;
+      if (kSplit && j == 1 && l == L - 1 && l > 0) t = kPinnWaves + wave % (D / 16 - kPinnWaves);  // PinnSplit
       r.p[j] = w.wp[l] + ((int64_t)(t < tiles ? t : tiles - 1) * kb * 64 + lane) * 4;
     }
     return r;
@@ -373,8 +423,12 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
                                        row(l + 1));
       __syncthreads();
     }
-    pinn_layer<H, D / 16, 1, D / 16, NT>(row(L - 1), s_bias + (L - 1) * H, (L & 1) ? act1 : act0, s_state, wave, lane, wq,
-                                     row(0));
+    if constexpr (kSplit)
+      pinn_layer<H, D / 16, 1, D / 16, NT, true>(row(L - 1), s_bias + (L - 1) * H, (L & 1) ? act1 : act0, s_state, wave,
+                                                 lane, wq, row(0), PinnSplit{s_part, s_flag, t + 1});
+    else
+      pinn_layer<H, D / 16, 1, D / 16, NT>(row(L - 1), s_bias + (L - 1) * H, (L & 1) ? act1 : act0, s_state, wave, lane,
+                                           wq, row(0));
     __syncthreads();
     if (traj) {
       for (int idx = tid; idx < kPinnIcs * D; idx += NTH) {

@@ -754,6 +754,13 @@ hipError_t run_steps(const hf_model *m, const float *state0, float *state_final,
       ld_dst = S;
     }
     if (m) e = hf::launch_chain_flux(m->chain, nullptr, cur, ld_cur, x, B, nx, nullptr, F, s);
+#ifdef HF_DIAG_NOFVSTEP  // timing diagnostic only: results are wrong (hybrid steps launch no FV kernel)
+    if (m) {
+      cur = dst;
+      ld_cur = ld_dst;
+      continue;
+    }
+#endif
     if (e == hipSuccess)
       e = hf::launch_fv_step(cur, ld_cur, dst, ld_dst, F, pc, B, nx, c, dt, nu, dx2,
                              flux_traj ? flux_traj + (int64_t)t * nx : nullptr, (int64_t)T * nx,

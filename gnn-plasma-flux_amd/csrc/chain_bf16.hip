@@ -561,11 +561,13 @@ struct CoreBF16 {
   static __device__ __forceinline__ void readout(const ChainW &W, const Small &S, R_t &R, Feed &F, Acts<MT> &X,
                                                  Pair<MT> &pend, float *park, int lane, int g4, float (&ffwd)[MT],
                                                  float (&fbwd)[MT], Seam &sm) {
+#ifndef HF_DIAG_NOPARK
     wave_lds_sync();
 #pragma unroll
     for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) X.h[mt][kb] = __builtin_bit_cast(u4, ldf4(park_at(park, kb, mt, lane)));
+#endif
     float pf[MT], pb[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) pf[mt] = pb[mt] = 0.f;
@@ -680,10 +682,12 @@ struct CoreBF16 {
         // no update layer: hand the readout the input layer's output the way
         // a last layer would (k-blocks 0..2 parked, tiles 6, 7 pending with a
         // zero aggregation term; ReLU is idempotent)
+#ifndef HF_DIAG_NOPARK  // timing diagnostic only (L = 0): results are wrong (no park round trip)
 #pragma unroll
         for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) *reinterpret_cast<u4 *>(park_at(park, kb, mt, lane)) = X.h[mt][kb];
+#endif
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           pend.a[mt][0] = h67[mt][0];
