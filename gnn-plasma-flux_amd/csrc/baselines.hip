@@ -587,16 +587,45 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
   }
   for (int i = tid; i < NX; i += NTH) s_x[i] = x[i];
   __syncthreads();
+#ifndef HF_PURE_MFMA_IO
+#define HF_PURE_MFMA_IO 1
+#endif
   for (int t = 0; t < T; ++t) {
     // input_mlp: h = tanh(W_in [n, u, E, x] + b_in)
-    for (int idx = tid; idx < H * NX; idx += NTH) {
-      const int f = idx / NX, c = idx - f * NX;
-      const float *wi = w.w_in + f * 4;
-      float v = __fmul_rn(wi[0], s_st[c]);
-      v = __fmaf_rn(wi[1], s_st[NX + c], v);
-      v = __fmaf_rn(wi[2], s_st[2 * NX + c], v);
-      v = __fmaf_rn(wi[3], s_x[c], v);
-      act[pure_act_idx<NC>(f, c)] = tanh_fast(__fadd_rn(v, w.b_in[f]));
+    if (HF_PURE_MFMA_IO) {
+      // on the matrix core: one v_mfma_f32_16x16x4f32 per cell group, A = rows
+      // 16u .. 16u+15 of W_in (lane: row lane & 15, input lane >> 4), B = the
+      // group's [n, u, E, x] (lane: input lane >> 4 of cell NC (lane & 15) + g);
+      // its output tile is the activation layout's (feature 16u + 4 (lane >> 4)
+      // + i of cell column lane & 15).  The f32 MFMA's sum is an fmaf chain over
+      // the 4 inputs (MI355X_MICROARCH.md), as the VALU form's; + b_in, tanh pairs.
+      const float a = w.w_in[(16 * u + (lane & 15)) * 4 + (lane >> 4)];
+      f4v bi;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bi[i] = w.b_in[16 * u + q4 + i];
+#pragma unroll
+      for (int g = 0; g < NC; ++g) {
+        const int cell = NC * (lane & 15) + g, k = lane >> 4;
+        const float bf = k < 3 ? s_st[k * NX + cell] : s_x[cell];
+        const f4v z = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bf, f4v{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        f4v h;
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const hf_f2 th = tanh_fast2(hf_f2{__fadd_rn(z[i], bi[i]), __fadd_rn(z[i + 1], bi[i + 1])});
+          h[i] = th.x, h[i + 1] = th.y;
+        }
+        *reinterpret_cast<f4v *>(act + ((u * NC + g) * 64 + lane) * 4) = h;
+      }
+    } else {
+      for (int idx = tid; idx < H * NX; idx += NTH) {
+        const int f = idx / NX, c = idx - f * NX;
+        const float *wi = w.w_in + f * 4;
+        float v = __fmul_rn(wi[0], s_st[c]);
+        v = __fmaf_rn(wi[1], s_st[NX + c], v);
+        v = __fmaf_rn(wi[2], s_st[2 * NX + c], v);
+        v = __fmaf_rn(wi[3], s_x[c], v);
+        act[pure_act_idx<NC>(f, c)] = tanh_fast(__fadd_rn(v, w.b_in[f]));
+      }
     }
     __syncthreads();
     for (int l = 0; l < w.L; ++l) {
@@ -666,7 +695,30 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
       act2 = tmp;
     }
     // output_mlp.2 and the update: state += W_o2 o + b_o2
-    if (tid < 3 * NX) {
+    if (HF_PURE_MFMA_IO) {
+      // on the matrix core: wave g < NC takes cell group g, A = the 3 rows of
+      // W_o2 (rows 3..15 zero; the packed weights' k order), B = o as stored:
+      // H/16 k-blocks x 4 MFMA steps; channel ch of cell NC c + g lands in lane
+      // c, element ch
+      if (u < NC) {
+        const int g = u, row = lane & 15;
+        f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < H / 16; ++kb) {
+          const f4v av = row < 3 ? *reinterpret_cast<const f4v *>(w.w_o2 + row * H + 16 * kb + q4)
+                                 : f4v{0.f, 0.f, 0.f, 0.f};
+          const f4v bv = *reinterpret_cast<const f4v *>(act + ((kb * NC + g) * 64 + lane) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[e], acc, 0, 0, 0);
+        }
+        if (lane < 16) {
+          const int cell = NC * lane + g;
+#pragma unroll
+          for (int ch = 0; ch < 3; ++ch)
+            s_st[ch * NX + cell] = __fadd_rn(s_st[ch * NX + cell], __fadd_rn(acc[ch], w.b_o2[ch]));
+        }
+      }
+    } else if (tid < 3 * NX) {
       const int ch = tid / NX, c = tid - ch * NX;
       const float *wo = w.w_o2 + ch * H;
       float v = 0.f;
