@@ -293,24 +293,16 @@ struct EpiMsg {
 // views, unsplit views): no clamps or zeroed rows, and each thread's row
 // handles are stepped by kKC per stage instead of recomputed (the stencil's
 // cell index without a division).
-template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM, bool EX = false>
-__global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi epi, int64_t I, int64_t J, int64_t R,
-                                                       int64_t rsplit, float *bias_part) {
-  static_assert(!EX || (ARM && BRM), "exact form: both operands run along the reduction");
-  // (a block epilogue parks a 128 x 65 tile in each operand's two buffers)
-  constexpr int kBufF = (Epi::kBlock && 2 * kTileF < kBM * 65) ? (kBM * 65 + 1) / 2 : kTileF;
-  __shared__ float sA[2][kBufF];
-  __shared__ float sB[2][kBufF];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wi = wave >> 1, wj = wave & 1, h = lane >> 5;
 #ifndef HF_TG_XCD
 #define HF_TG_XCD 1
 #endif
-  // HF_TG_XCD (measured +0.8 % on the training step, profiles/r05_train_tgemm_xcd_prio_ab.txt):
-  // pairs of consecutive tiles (x fastest) on one XCD.  Blocks b and
-  // b + 8 share an XCD (MI355X_MICROARCH.md, workgroup dispatch); consecutive
-  // tiles of a weight-gradient split read the same rows (the two column tiles
-  // of [h ; agg h], or the P and Q halves against h[L]).
-  unsigned bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+// HF_TG_XCD (measured +0.8 % on the training step, profiles/r05_train_tgemm_xcd_prio_ab.txt):
+// pairs of consecutive tiles (x fastest) on one XCD.  Blocks b and
+// b + 8 share an XCD (MI355X_MICROARCH.md, workgroup dispatch); consecutive
+// tiles of a weight-gradient split read the same rows (the two column tiles
+// of [h ; agg h], or the P and Q halves against h[L]).
+__device__ __forceinline__ void tg_block(unsigned &bx, unsigned &by, unsigned &bz) {
+  bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if (HF_TG_XCD) {
     const unsigned gx = gridDim.x, gy = gridDim.y, T = gx * gy * gridDim.z;
     unsigned L = bx + gx * (by + gy * bz);
@@ -319,6 +311,19 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
     by = (L / gx) % gy;
     bz = L / (gx * gy);
   }
+}
+
+// One output tile (bx, by) of split bz: the body of tgemm_kernel and of
+// tgemm_batch_kernel.
+template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM, bool EX = false>
+__device__ __forceinline__ void tgemm_tile(LA ga, LB gb, Epi epi, int64_t I, int64_t J, int64_t R, int64_t rsplit,
+                                           float *bias_part, unsigned bx, unsigned by, unsigned bz) {
+  static_assert(!EX || (ARM && BRM), "exact form: both operands run along the reduction");
+  // (a block epilogue parks a 128 x 65 tile in each operand's two buffers)
+  constexpr int kBufF = (Epi::kBlock && 2 * kTileF < kBM * 65) ? (kBM * 65 + 1) / 2 : kTileF;
+  __shared__ float sA[2][kBufF];
+  __shared__ float sB[2][kBufF];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wi = wave >> 1, wj = wave & 1, h = lane >> 5;
   const int64_t i0 = (int64_t)bx * kBM, j0 = (int64_t)by * kBN;
   const int64_t rb = (int64_t)bz * rsplit;
   if constexpr (std::is_same<Epi, EpiPart>::value) epi.z = bz;
@@ -520,6 +525,39 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
   }
 }
 
+template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM, bool EX = false>
+__global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi epi, int64_t I, int64_t J, int64_t R,
+                                                       int64_t rsplit, float *bias_part) {
+  unsigned bx, by, bz;
+  tg_block(bx, by, bz);
+  tgemm_tile<LA, ARM, LB, BRM, Epi, COLSUM, EX>(ga, gb, epi, I, J, R, rsplit, bias_part, bx, by, bz);
+}
+
+// NB independent GEMMs of one shape in ONE launch (the layers' weight
+// gradients, each from its own operands into its own partials): grid z =
+// problem * S + split.  One launch keeps the machine full across the
+// problems' tails, which a launch per problem drains (each is about one wave
+// of workgroups).  Every tile's arithmetic is tgemm_kernel's.
+constexpr int kTgMaxBatch = 8;
+template <class LA, class LB, class Epi>
+struct TgBatch {
+  LA a[kTgMaxBatch];
+  LB b[kTgMaxBatch];
+  Epi e[kTgMaxBatch];
+  float *bias_part[kTgMaxBatch];
+  int n;      // problems
+  int64_t S;  // splits per problem
+};
+template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM, bool EX = false>
+__global__ __launch_bounds__(256, HF_TG_WG) void tgemm_batch_kernel(TgBatch<LA, LB, Epi> bt, int64_t I, int64_t J,
+                                                             int64_t R, int64_t rsplit) {
+  unsigned bx, by, bz;
+  tg_block(bx, by, bz);
+  const unsigned pb = bz / (unsigned)bt.S, sz = bz - pb * (unsigned)bt.S;
+  tgemm_tile<LA, ARM, LB, BRM, Epi, COLSUM, EX>(bt.a[pb], bt.b[pb], bt.e[pb], I, J, R, rsplit, bt.bias_part[pb], bx, by,
+                                                sz);
+}
+
 #ifndef HF_TG_EXACT
 #define HF_TG_EXACT 1
 #endif
@@ -543,6 +581,30 @@ hipError_t tgemm(const LA &ga, const LB &gb, const Epi &epi, int64_t I, int64_t 
   }
   hipLaunchKernelGGL((tgemm_kernel<LA, ARM, LB, BRM, Epi, COLSUM>), grid, dim3(256), 0, s, ga, gb, epi, I, J, R,
                      rsplit > 0 ? rsplit : kKC, bias_part);
+  return hipGetLastError();
+}
+// The NB = bt.n problems of bt in one launch (both operands along the
+// reduction, EpiPart-style split partials): the exact kernel when every
+// problem's shapes allow it, as tgemm.
+template <class LA, class LB, class Epi, bool COLSUM>
+hipError_t tgemm_batch(TgBatch<LA, LB, Epi> bt, int64_t I, int64_t J, int64_t R, int splits, hipStream_t s) {
+  if (I <= 0 || J <= 0 || bt.n <= 0) return hipSuccess;
+  if (bt.n > kTgMaxBatch) return hipErrorInvalidValue;
+  bool exact = HF_TG_EXACT && R > 0 && I % kBM == 0 && J % kBN == 0 && R % kKC == 0;
+  for (int p = 0; p < bt.n; ++p) {
+    if (!bt.a[p].fits32() || !bt.b[p].fits32()) return hipErrorInvalidValue;
+    exact = exact && bt.a[p].exact_ok(R) && bt.b[p].exact_ok(R);
+  }
+  int64_t rsplit = (R + splits - 1) / splits;
+  rsplit = (rsplit + kKC - 1) / kKC * kKC;
+  bt.S = R > 0 ? (R + rsplit - 1) / rsplit : 1;
+  dim3 grid((unsigned)((I + kBM - 1) / kBM), (unsigned)((J + kBN - 1) / kBN), (unsigned)(bt.S * bt.n));
+  if (exact)
+    hipLaunchKernelGGL((tgemm_batch_kernel<LA, true, LB, true, Epi, COLSUM, true>), grid, dim3(256), 0, s, bt, I, J, R,
+                       rsplit);
+  else
+    hipLaunchKernelGGL((tgemm_batch_kernel<LA, true, LB, true, Epi, COLSUM>), grid, dim3(256), 0, s, bt, I, J, R,
+                       rsplit > 0 ? rsplit : kKC);
   return hipGetLastError();
 }
 // number of splits tgemm makes of R for a requested count

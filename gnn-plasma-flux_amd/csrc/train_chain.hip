@@ -749,6 +749,11 @@ FusedTape fused_tape(const GraphW &w, int64_t N, const ChainTape &t) {
 }
 bool fused_chain(const GraphW &w, int nx, int64_t N) { return HF_TRAIN_FUSED && chain_train_fused_ok(w, nx) && N % nx == 0; }
 
+// 1: the fused path's update-layer weight-gradient GEMMs (independent once the
+// fused backward pass has every layer's g) run as ONE launch (tgemm_batch)
+#ifndef HF_TRAIN_WG_BATCH
+#define HF_TRAIN_WG_BATCH 1
+#endif
 int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   const int64_t H = w.hidden;
   size_t b = al256(sizeof(float) * N * 2 * H);  // dPQ
@@ -758,8 +763,11 @@ int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   b += al256(sizeof(float) * S * 2 * H);        // bias partials
   b += al256(sizeof(float) * kEdgeBlocks * (H + 1));
   b += al256(sizeof(float) * kInputSplits * H * (w.in_dim + 1));
-  if (fused_width(w))  // fused backward: g[0..L] side by side + the transposed weights
+  if (fused_width(w)) {  // fused backward: g[0..L] side by side + the transposed weights
     b += (w.layers + 1) * al256(sizeof(float) * N * H) + al256((size_t)chain_train_bwd_pack_bytes(w.layers));
+    // + every update layer's weight-gradient partials (the layers' GEMMs in one launch)
+    if (HF_TRAIN_WG_BATCH) b += w.layers * (al256(sizeof(float) * S * 2 * H * H) + al256(sizeof(float) * S * 2 * H));
+  }
   return (int64_t)b;
 }
 
@@ -819,6 +827,11 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   const int64_t gstride = (int64_t)(al256(sizeof(float) * N * H) / 4);
   float *G = fused ? take((L + 1) * al256(sizeof(float) * N * H)) : nullptr;
   void *bpack = fused ? static_cast<void *>(take((size_t)chain_train_bwd_pack_bytes(L))) : nullptr;
+  const bool wg_batch = fused && HF_TRAIN_WG_BATCH && L >= 1 && L <= kTgMaxBatch;
+  const int64_t lpstride = (int64_t)(al256(sizeof(float) * S * 2 * H * H) / 4),
+                lbstride = (int64_t)(al256(sizeof(float) * S * 2 * H) / 4);
+  float *lpart = wg_batch ? take(L * al256(sizeof(float) * S * 2 * H * H)) : nullptr;
+  float *lbpart = wg_batch ? take(L * al256(sizeof(float) * S * 2 * H)) : nullptr;
   hipError_t e;
   auto reduce = [&](int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff, int64_t nbias,
                     float *bias) {
@@ -859,7 +872,22 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   if (fused && (e = launch_chain_train_bwd_fused(w, N / nx, nx, G, gstride, fused_tape(w, N, t).mbits, bpack,
                                                  fold ? dPQ : nullptr, s)))
     return e;
-  for (int l = L - 1; l >= 0; --l) {  // update layers, last to first                      (:53-60)
+  if (wg_batch) {  // dW_l, db_l of every update layer: one launch, then the layers' reductions
+    TgBatch<VPlain, VStencil, EpiPart> bt{};
+    bt.n = L;
+    for (int l = 0; l < L; ++l) {
+      bt.a[l] = VPlain{G + (l + 1) * gstride, H, N, kNoSplit, 0, H};
+      bt.b[l] = VStencil{t.h[l], N, H, nx};
+      bt.e[l] = EpiPart{lpart + l * lpstride, H, 2LL * H};
+      bt.bias_part[l] = lbpart + l * lbstride;
+    }
+    if ((e = tgemm_batch<VPlain, VStencil, EpiPart, true>(bt, H, 2 * H, N, kWgradSplits, s))) return e;
+    for (int l = L - 1; l >= 0; --l)
+      launch_part_reduce(lpart + l * lpstride, (int)S, H, 2 * H, const_cast<float *>(g.w_l + l * g.lsw), kNoSplit,
+                         2LL * H, 0, lbpart + l * lbstride, H, const_cast<float *>(g.b_l + l * g.lsb), s);
+    if ((e = hipGetLastError())) return e;
+  }
+  for (int l = L - 1; l >= 0 && !wg_batch; --l) {  // update layers, last to first                      (:53-60)
     // dW_l[o][k] = sum_m delta[m][o] [h[l] ; agg h[l]][m][k], db_l = column sums of delta
     {
       const VPlain A{fused ? G + (l + 1) * gstride : dl[cur], H, N, kNoSplit, 0, H};
