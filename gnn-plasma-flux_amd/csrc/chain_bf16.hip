@@ -635,6 +635,16 @@ struct CoreBF16 {
   template <int MT>
   static __device__ __forceinline__ void input(const Small &S, int lane, const float (&feat)[MT], Acts<MT> &X,
                                                f4 (&h67)[MT][2]) {
+#ifdef HF_DIAG_NOINPUT  // timing diagnostic only: results are wrong (no input layer: the features' bits as h)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const unsigned v = __float_as_uint(feat[mt]);
+#pragma unroll
+      for (int kb = 0; kb < kKB; ++kb) X.h[mt][kb] = u4{v, v + kb, v, v};
+      h67[mt][0] = h67[mt][1] = f4{feat[mt], feat[mt], feat[mt], feat[mt]};
+    }
+    return;
+#endif
     const int g4 = 4 * (lane >> 4);
     u4 bx[MT];
 #pragma unroll

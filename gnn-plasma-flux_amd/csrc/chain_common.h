@@ -708,6 +708,105 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_fw
   R.drain();
 }
 
+// The readout's backward in the backward pass (train_chain.hip
+// launch_chain_backward, fused path): from the forward's P/Q tape (P = W_a h +
+// b_e, Q = W_b h, [N][P | Q]) and the flux gradient g ([B][2nx]: g_f, g_b),
+// with z_f(i) = P_i + Q_{i+1}, z_b(i) = P_{i+1} + Q_i (src/flux_gnn.py:62-66),
+//   dP_i = g_f(i) w2 [z_f(i) > 0] + g_b(i-1) w2 [z_b(i-1) > 0]
+//   dQ_i = g_b(i) w2 [z_b(i) > 0] + g_f(i-1) w2 [z_f(i-1) > 0]
+// in the lane layout (neighbours one m-tile over, or a row rotation at the
+// seam), the sums and products of edge_backward_kernel bit for bit, stored to
+// dpq ([N][dP | dQ], the readout weight gradient's operand and this pass's B
+// operand), and this IC's dw2 = sum g_f ReLU(z_f) + g_b ReLU(z_b), db2 = sum
+// g_f + g_b to part[b][0..H] (a fixed-order row reduction).  Replaces the
+// separate edge_backward_h128_kernel pass over P/Q and dP/dQ.
+struct EdgeFold {
+  const float *pq;     // nullptr: no fold (the pass reads dpq as written by the edge kernel)
+  const float *gflux;  // [B][2nx]
+  const float *w2;     // [kH]
+  float *dpq;          // [N][2 kH]
+  float *part;         // [B][kH + 1]
+};
+template <int MT>
+__device__ __forceinline__ void edge_fold_ic(const EdgeFold &E, int64_t b, bool live, int lane) {
+  constexpr int nx = 16 * MT;
+  const int j = lane & 15, g4 = 4 * (lane >> 4);
+  const float *src = E.pq + b * nx * 2 * kH + g4;
+  float *dst = E.dpq + b * nx * 2 * kH + g4;
+  float gf[MT], gb[MT], gfl[MT], gbl[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    gf[mt] = E.gflux[b * 2 * nx + cell_of<MT>(mt, j)];
+    gb[mt] = E.gflux[b * 2 * nx + nx + cell_of<MT>(mt, j)];
+  }
+  left_nb<MT>(gf, gfl);
+  left_nb<MT>(gb, gbl);
+  float dw[kNT][4];
+#pragma unroll
+  for (int nt = 0; nt < kNT; ++nt) {
+    f4 P4[MT], Q4[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      P4[mt] = ldf4(src + (int64_t)cell_of<MT>(mt, j) * 2 * kH + 16 * nt);
+      Q4[mt] = ldf4(src + (int64_t)cell_of<MT>(mt, j) * 2 * kH + kH + 16 * nt);
+    }
+    const f4 w = ldf4(E.w2 + 16 * nt + g4);
+    f4 dP4[MT], dQ4[MT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float P[MT], Q[MT], Pr[MT], Pl[MT], Qr[MT], Ql[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) P[mt] = P4[mt][r], Q[mt] = Q4[mt][r];
+      right_nb<MT>(P, Pr);
+      left_nb<MT>(P, Pl);
+      right_nb<MT>(Q, Qr);
+      left_nb<MT>(Q, Ql);
+      float acc = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float zf = __fadd_rn(P[mt], Qr[mt]), zbp = __fadd_rn(P[mt], Ql[mt]);
+        const float zb = __fadd_rn(Pr[mt], Q[mt]), zfp = __fadd_rn(Pl[mt], Q[mt]);
+        dP4[mt][r] = __fadd_rn(zf > 0.f ? __fmul_rn(gf[mt], w[r]) : 0.f, zbp > 0.f ? __fmul_rn(gbl[mt], w[r]) : 0.f);
+        dQ4[mt][r] = __fadd_rn(zb > 0.f ? __fmul_rn(gb[mt], w[r]) : 0.f, zfp > 0.f ? __fmul_rn(gfl[mt], w[r]) : 0.f);
+        acc = fmaf(gf[mt], zf > 0.f ? zf : 0.f, acc);
+        acc = fmaf(gb[mt], zb > 0.f ? zb : 0.f, acc);
+      }
+      dw[nt][r] = acc;
+    }
+    if (live) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        *reinterpret_cast<f4 *>(dst + (int64_t)cell_of<MT>(mt, j) * 2 * kH + 16 * nt) = dP4[mt];
+        *reinterpret_cast<f4 *>(dst + (int64_t)cell_of<MT>(mt, j) * 2 * kH + kH + 16 * nt) = dQ4[mt];
+      }
+    }
+  }
+  float db = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) db = __fadd_rn(db, __fadd_rn(gf[mt], gb[mt]));
+  // sums over the row's 16 lanes (its 16 MT cells), in the same order in every lane
+  auto row_sum = [](float v) {
+    v = __fadd_rn(v, dpp_zero<0x128>(v));  // row_ror:8
+    v = __fadd_rn(v, dpp_zero<0x124>(v));  // row_ror:4
+    v = __fadd_rn(v, dpp_zero<0x122>(v));  // row_ror:2
+    return __fadd_rn(v, dpp_zero<kRowRor1>(v));
+  };
+#pragma unroll
+  for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dw[nt][r] = row_sum(dw[nt][r]);
+  db = row_sum(db);
+  if (live && j == 0) {
+    float *o = E.part + b * (kH + 1);
+#pragma unroll
+    for (int nt = 0; nt < kNT; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[16 * nt + g4 + r] = dw[nt][r];
+    if (g4 == 0) o[kH] = db;
+  }
+  __threadfence_block();  // this wave's dP / dQ stores complete before it reads them back
+}
+
 // Fused data gradient of the update layers (train_chain.hip
 // launch_chain_backward): from g[L] = ReLU'(h[L]) * dh[L] (the readout's
 // gradient, global) to g[l] = ReLU'(h[l]) * (W_a^T g[l+1] + W_b^T agg g[l+1])
@@ -719,7 +818,7 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_fw
 template <class Core, int MT>
 __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bwd_kernel(
     ChainW W, int64_t items, float *g0, int64_t gstride, const unsigned *__restrict__ mbits,
-    const float *__restrict__ dPQ) {
+    const float *__restrict__ dPQ, EdgeFold EF) {
   constexpr int nx = 16 * MT;
   __shared__ f4 lds4[Core::kSlots * Core::kChunkFloats / 4];
   float *lds = reinterpret_cast<float *>(lds4);
@@ -743,6 +842,7 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bw
     f4 g[MT][kNT];
     if (dPQ) {
       // g[L] = ReLU'(h[L]) * (W_a^T dP + W_b^T dQ): a layer pass with B = [dP ; dQ]
+      if (EF.pq) edge_fold_ic<MT>(EF, b, live, lane);  // dP / dQ of this IC into dPQ (= EF.dpq) first
       SecondHalf<MT> X;
       const float *src = dPQ + b * nx * 2 * kH + g4;
 #pragma unroll

@@ -502,9 +502,9 @@ hipError_t train_fwd_launch(const ChainW &cw, const float *b2p, const float *nf,
 }
 template <int MT>
 hipError_t train_bwd_launch(const ChainW &cw, int64_t B, float *g0, int64_t gstride, const unsigned *mbits,
-                            const float *dPQ, hipStream_t s) {
+                            const float *dPQ, const EdgeFold &ef, hipStream_t s) {
   hipLaunchKernelGGL((chain_train_bwd_kernel<CoreF32, MT>), dim3((unsigned)train_blocks<MT>(B)),
-                     dim3(64 * CoreF32::kNW), 0, s, cw, B, g0, gstride, mbits, dPQ);
+                     dim3(64 * CoreF32::kNW), 0, s, cw, B, g0, gstride, mbits, dPQ, ef);
   return hipGetLastError();
 }
 }  // namespace
@@ -517,7 +517,10 @@ int64_t chain_train_mask_bytes(int layers, int64_t N) { return (int64_t)(layers 
 int64_t chain_train_bwd_pack_bytes(int layers) { return (int64_t)16 * (layers + 1) * chain_chunk_bytes(kPrecF32); }
 
 hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, float *g0, int64_t gstride,
-                                        const unsigned *mbits, void *pack, const float *dPQ, hipStream_t s) {
+                                        const unsigned *mbits, void *pack, const float *dPQ, hipStream_t s,
+                                        const float *pq, const float *gflux, const float *w2, float *epart) {
+  // pq != nullptr: the readout's backward from the P/Q tape in this pass (EdgeFold), writing dPQ
+  const EdgeFold ef{pq, gflux, w2, const_cast<float *>(dPQ), epart};
   const int L = w.layers;
   if (B <= 0 || (L == 0 && !dPQ)) return hipSuccess;
   float *stream = static_cast<float *>(pack);
@@ -529,10 +532,10 @@ hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, floa
   cw.layers = L;
   cw.prec = kPrecF32;
   switch (nx) {
-    case 16: return train_bwd_launch<1>(cw, B, g0, gstride, mbits, dPQ, s);
-    case 32: return train_bwd_launch<2>(cw, B, g0, gstride, mbits, dPQ, s);
-    case 48: return train_bwd_launch<3>(cw, B, g0, gstride, mbits, dPQ, s);
-    case 64: return train_bwd_launch<4>(cw, B, g0, gstride, mbits, dPQ, s);
+    case 16: return train_bwd_launch<1>(cw, B, g0, gstride, mbits, dPQ, ef, s);
+    case 32: return train_bwd_launch<2>(cw, B, g0, gstride, mbits, dPQ, ef, s);
+    case 48: return train_bwd_launch<3>(cw, B, g0, gstride, mbits, dPQ, ef, s);
+    case 64: return train_bwd_launch<4>(cw, B, g0, gstride, mbits, dPQ, ef, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -245,7 +245,9 @@ int64_t chain_train_bwd_pack_bytes(int layers);
 hipError_t launch_chain_train_fwd_fused(const GraphW &w, const float *nf, int64_t B, int nx, float *fe, float *h0,
                                         int64_t hstride, float *pq, unsigned *mbits, void *pack, hipStream_t s);
 hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, float *g0, int64_t gstride,
-                                        const unsigned *mbits, void *pack, const float *dPQ, hipStream_t s);
+                                        const unsigned *mbits, void *pack, const float *dPQ, hipStream_t s,
+                                        const float *pq = nullptr, const float *gflux = nullptr,
+                                        const float *w2 = nullptr, float *epart = nullptr);
 // The ablation loss's single-step terms and d loss / d flux_edge (train_chain.hip).
 int64_t ablation_loss_ws_bytes(int B, int nx);
 hipError_t launch_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx,

@@ -749,6 +749,15 @@ FusedTape fused_tape(const GraphW &w, int64_t N, const ChainTape &t) {
 }
 bool fused_chain(const GraphW &w, int nx, int64_t N) { return HF_TRAIN_FUSED && chain_train_fused_ok(w, nx) && N % nx == 0; }
 
+// 1: the fused path forms the readout's backward (dP, dQ, dw2, db2) from the
+// P/Q tape inside the backward pass (EdgeFold) instead of edge_backward_h128_kernel
+#ifndef HF_TRAIN_EDGE_FOLD
+#define HF_TRAIN_EDGE_FOLD 1
+#endif
+// 1: the readout's data gradient is the fused backward pass's first pass
+#ifndef HF_TRAIN_RO_FOLD
+#define HF_TRAIN_RO_FOLD 1
+#endif
 // 1: the fused path's update-layer weight-gradient GEMMs (independent once the
 // fused backward pass has every layer's g) run as ONE launch (tgemm_batch)
 #ifndef HF_TRAIN_WG_BATCH
@@ -767,6 +776,8 @@ int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
     b += (w.layers + 1) * al256(sizeof(float) * N * H) + al256((size_t)chain_train_bwd_pack_bytes(w.layers));
     // + every update layer's weight-gradient partials (the layers' GEMMs in one launch)
     if (HF_TRAIN_WG_BATCH) b += w.layers * (al256(sizeof(float) * S * 2 * H * H) + al256(sizeof(float) * S * 2 * H));
+    // + the readout's per-IC dw2 / db2 partials of the folded edge backward (B <= N / 16)
+    if (HF_TRAIN_EDGE_FOLD) b += al256(sizeof(float) * (N / 16 + 1) * (H + 1));
   }
   return (int64_t)b;
 }
@@ -832,6 +843,9 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
                 lbstride = (int64_t)(al256(sizeof(float) * S * 2 * H) / 4);
   float *lpart = wg_batch ? take(L * al256(sizeof(float) * S * 2 * H * H)) : nullptr;
   float *lbpart = wg_batch ? take(L * al256(sizeof(float) * S * 2 * H)) : nullptr;
+  // the readout's backward folded into the backward pass (needs its readout pass: HF_TRAIN_RO_FOLD)
+  const bool efold = fused && HF_TRAIN_EDGE_FOLD && HF_TRAIN_RO_FOLD && H == 128;
+  float *efpart = efold ? take(sizeof(float) * (N / 16 + 1) * (H + 1)) : nullptr;
   hipError_t e;
   auto reduce = [&](int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff, int64_t nbias,
                     float *bias) {
@@ -839,28 +853,30 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
     return hipGetLastError();
   };
   // readout: dPQ, dw2, db2                                                          (:62-66)
-  if (H == 128)
+  if (efold) {
+    // (formed inside the backward pass below, then the readout weight gradient)
+  } else if (H == 128)
     hipLaunchKernelGGL(edge_backward_h128_kernel, dim3(kEdgeBlocks), dim3(256), 0, s, t.pq, N / nx, nx, w.w_2,
                        grad_flux, dPQ, epart);
   else
     hipLaunchKernelGGL(edge_backward_kernel, dim3(kEdgeBlocks), dim3(256), 0, s, t.pq, H, N, nx, w.w_2, grad_flux, dPQ,
                        epart);
-  hipLaunchKernelGGL(edge_partial_reduce_kernel, dim3((unsigned)(H + 1)), dim3(256), 0, s, epart,
-                     kEdgeBlocks, H, const_cast<float *>(g.w_2), const_cast<float *>(g.b_2));
+  if (!efold)
+    hipLaunchKernelGGL(edge_partial_reduce_kernel, dim3((unsigned)(H + 1)), dim3(256), 0, s, epart,
+                       kEdgeBlocks, H, const_cast<float *>(g.w_2), const_cast<float *>(g.b_2));
   // dW_e[c % H][(c / H) H + k] = sum_m dPQ[m][c] h[L][m][k]; db_e = column sums of dP
-  {
+  auto readout_wgrad = [&]() -> hipError_t {
     const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
     const VPlain B{t.h[L], H, N, kNoSplit, 0, H};
     if ((e = tgemm<VPlain, true, VPlain, true, EpiPart, true, true>(A, B, EpiPart{part, 2LL * H, H}, 2 * H, H, N,
                                                                kWgradSplits, s, bpart)))
       return e;
     if ((e = reduce(2 * H, H, const_cast<float *>(g.w_e), hsh, 2LL * H, H, H, const_cast<float *>(g.b_e)))) return e;
-  }
+    return hipSuccess;
+  };
+  if (!efold && (e = readout_wgrad())) return e;
   // dh[L] = [W_a ; W_b]^T dPQ, masked by ReLU'(h[L]) (fused: the first pass of chain_train_bwd_kernel)
   int cur = 0;
-#ifndef HF_TRAIN_RO_FOLD
-#define HF_TRAIN_RO_FOLD 1
-#endif
   const bool fold = fused && HF_TRAIN_RO_FOLD;
   if (!fold) {
     const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
@@ -870,8 +886,14 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   }
   // fused: every layer's data gradient in one IC-per-wave pass (chain_train_bwd_kernel)
   if (fused && (e = launch_chain_train_bwd_fused(w, N / nx, nx, G, gstride, fused_tape(w, N, t).mbits, bpack,
-                                                 fold ? dPQ : nullptr, s)))
+                                                 fold ? dPQ : nullptr, s, efold ? t.pq : nullptr, grad_flux,
+                                                 w.w_2, efpart)))
     return e;
+  if (efold) {  // dw2, db2 from the per-IC partials; then dW_e, db_e from the dPQ the pass wrote
+    hipLaunchKernelGGL(edge_partial_reduce_kernel, dim3((unsigned)(H + 1)), dim3(256), 0, s, efpart,
+                       (int)(N / nx), H, const_cast<float *>(g.w_2), const_cast<float *>(g.b_2));
+    if ((e = readout_wgrad())) return e;
+  }
   if (wg_batch) {  // dW_l, db_l of every update layer: one launch, then the layers' reductions
     TgBatch<VPlain, VStencil, EpiPart> bt{};
     bt.n = L;
