@@ -191,9 +191,15 @@ struct CoreBF16 {
     L = R = f4{0.f, 0.f, 0.f, 0.f};
     return;
 #endif
-    const int o = sm.par * (NW * 16) + ((Seam::lane_id() >> 4) << 1) + t;
+    const int l = Seam::lane_id(), o = sm.par * (NW * 16) + ((l >> 4) << 1) + t;
+#ifdef HF_EXP_SEAM1
+    // experiment: one read per tile: lanes j = 15 read the right wave's value,
+    // every other lane the left wave's (only j = 0 uses L, only j = 15 uses R)
+    L = R = ((l & 15) == 15 ? sm.rdr : sm.rdl)[o];
+#else
     L = sm.rdl[o];
     R = sm.rdr[o];
+#endif
   }
 
   struct Feed {

@@ -720,6 +720,9 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_fw
 // operand), and this IC's dw2 = sum g_f ReLU(z_f) + g_b ReLU(z_b), db2 = sum
 // g_f + g_b to part[b][0..H] (a fixed-order row reduction).  Replaces the
 // separate edge_backward_h128_kernel pass over P/Q and dP/dQ.
+#ifndef HF_TRAIN_EDGE_FOLD  // (train_chain.hip: measured and not kept; default off)
+#define HF_TRAIN_EDGE_FOLD 0
+#endif
 struct EdgeFold {
   const float *pq;     // nullptr: no fold (the pass reads dpq as written by the edge kernel)
   const float *gflux;  // [B][2nx]
@@ -842,7 +845,9 @@ __global__ __launch_bounds__(64 * Core::kNW, Core::kWGPerCU) void chain_train_bw
     f4 g[MT][kNT];
     if (dPQ) {
       // g[L] = ReLU'(h[L]) * (W_a^T dP + W_b^T dQ): a layer pass with B = [dP ; dQ]
+#if HF_TRAIN_EDGE_FOLD
       if (EF.pq) edge_fold_ic<MT>(EF, b, live, lane);  // dP / dQ of this IC into dPQ (= EF.dpq) first
+#endif
       SecondHalf<MT> X;
       const float *src = dPQ + b * nx * 2 * kH + g4;
 #pragma unroll

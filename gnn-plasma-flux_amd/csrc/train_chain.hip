@@ -750,9 +750,13 @@ FusedTape fused_tape(const GraphW &w, int64_t N, const ChainTape &t) {
 bool fused_chain(const GraphW &w, int nx, int64_t N) { return HF_TRAIN_FUSED && chain_train_fused_ok(w, nx) && N % nx == 0; }
 
 // 1: the fused path forms the readout's backward (dP, dQ, dw2, db2) from the
-// P/Q tape inside the backward pass (EdgeFold) instead of edge_backward_h128_kernel
+// P/Q tape inside the backward pass (EdgeFold) instead of edge_backward_h128_kernel.
+// Measured and not kept (round 6, profiles/r06_train_edgefold_ab.txt): the
+// backward pass grew 349 -> 414 us against the 48 + 5 us it saved (the pass
+// runs one wave per SIMD, so the P/Q loads' latency is exposed).  Default 0
+// (chain_common.h holds the same switch for the kernel side).
 #ifndef HF_TRAIN_EDGE_FOLD
-#define HF_TRAIN_EDGE_FOLD 1
+#define HF_TRAIN_EDGE_FOLD 0
 #endif
 // 1: the readout's data gradient is the fused backward pass's first pass
 #ifndef HF_TRAIN_RO_FOLD
