@@ -274,10 +274,35 @@ struct PinnSplit {
   int *flag;   // [R] step tag of the partial in sp
   int tag;     // this step's tag (t + 1)
 };
+// Barrier-free layer hand-off (HF_PINN_FLAGS): each output tile carries a
+// flag word in LDS that its wave sets (release, workgroup scope) to the
+// layer's tag (step * L + layer + 1, increasing) once the tile is stored; a
+// wave reads input k-block c only after flag c holds the producing layer's tag
+// (acquire).  Tiles are owned by one wave each, the activations cycle through
+// three buffers (a writer of layer l has consumed every tile of layer l-1, so
+// every wave is past layer l-2, the last reader of the buffer layer l
+// overwrites), so no workgroup barrier orders a step: a wave starts a layer on
+// the k-blocks that are ready while the slower waves finish theirs.  The last
+// layer's owner waves also store their new state rows to the trajectory.
+struct PinnSync {
+  const int *in_flag = nullptr;  // flags of the input tiles (nullptr: a barrier ordered them)
+  int in_tag = 0;
+  int *out_flag = nullptr;
+  int out_tag = 0;
+  float *traj = nullptr;  // ACT 1: row step + 1 of IC b0 (ICs ldt apart), or nullptr
+  int64_t ldt = 0;
+  int nic = 0;  // ICs of the workgroup that exist
+};
+__device__ __forceinline__ void pinn_wait(const int *f, int tag) {
+  // bounded: never reached in a correct run, but a lost producer ends in wrong values, not a hang
+  for (int it = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < tag && it < (1 << 20); ++it)
+    __builtin_amdgcn_s_sleep(1);
+}
 template <int K, int NTILES, int ACT, int KBN, int NT, bool SPLIT = false>
 __device__ __forceinline__ void pinn_layer(const PinnRows<NT> &wrow, const float *bias, const float *in, float *out,
                                            int wave, int lane, f4v (&wq)[kPinnAhead][NT],
-                                           const PinnRows<NT> &nrow, const PinnSplit &spl = PinnSplit{}) {
+                                           const PinnRows<NT> &nrow, const PinnSplit &spl = PinnSplit{},
+                                           const PinnSync &sy = PinnSync{}) {
   constexpr int KB = K / 16, P = kPinnAhead;
   static_assert(KB % P == 0 && KBN >= P - 1, "a layer's k-blocks fill whole rounds of the ring");
   static_assert(!SPLIT || (ACT == 1 && NT == 2 && 2 * (NTILES - kPinnWaves) == kPinnWaves && KB % 2 == 0),
@@ -289,6 +314,15 @@ __device__ __forceinline__ void pinn_layer(const PinnRows<NT> &wrow, const float
   f4v acc[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+  // flags: one read of all the input tiles' flags; only if some are not yet
+  // set does the wave wait per k-block
+  bool ready = true;
+  if (sy.in_flag) {
+    const int f = lane < KB ? __hip_atomic_load(sy.in_flag + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
+                            : sy.in_tag;
+    ready = __all(f >= sy.in_tag);
+    if (!ready) pinn_wait(sy.in_flag, sy.in_tag);
+  }
   f4v bv = *reinterpret_cast<const f4v *>(in + lane * 4);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -304,7 +338,10 @@ __device__ __forceinline__ void pinn_layer(const PinnRows<NT> &wrow, const float
       }
     }
     f4v bn = bv;
-    if (c + 1 < KB) bn = *reinterpret_cast<const f4v *>(in + (c + 1) * 256 + lane * 4);
+    if (c + 1 < KB) {
+      if (!ready) pinn_wait(sy.in_flag + c + 1, sy.in_tag);
+      bn = *reinterpret_cast<const f4v *>(in + (c + 1) * 256 + lane * 4);
+    }
     const bool use1 = on1(c);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -349,8 +386,12 @@ __device__ __forceinline__ void pinn_layer(const PinnRows<NT> &wrow, const float
       const f4v st = *reinterpret_cast<const f4v *>(o);
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = __fadd_rn(st[i], v[i]);
+      // the new state's features 16t + 4 (lane >> 4) .. +3 of IC lane & 15
+      if (sy.traj && (lane & 15) < sy.nic)
+        *reinterpret_cast<f4v *>(sy.traj + (lane & 15) * sy.ldt + 16 * t + 4 * (lane >> 4)) = v;
     }
     *reinterpret_cast<f4v *>(o) = v;
+    if (sy.out_flag) __hip_atomic_store(sy.out_flag + t, sy.out_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
 
@@ -366,7 +407,13 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
   static_assert(H >= D, "the widest layer sets the tiles per wave");
   constexpr int NTH = 64 * kPinnWaves;
   __shared__ f4v s_state4[D * kPinnIcs / 4];
-  __shared__ f4v s_act4[2][H * kPinnIcs / 4];
+#ifndef HF_PINN_FLAGS
+#define HF_PINN_FLAGS 1
+#endif
+  constexpr bool kFlags = HF_PINN_FLAGS;
+  __shared__ f4v s_act4[kFlags ? 3 : 2][H * kPinnIcs / 4];
+  __shared__ int s_fh[3][H / 16];  // PinnSync flags of the three activation buffers' tiles
+  __shared__ int s_fs[D / 16];     // ... and of the state's
   __shared__ f4v s_bias4[kMaxChainLayers * H / 4];  // layer l's bias at l * H
   // the split last layer's partial sums and flags (PinnSplit)
 #ifdef HF_EXP_PINN_NOSPLIT  // A/B: the clamped spare tile of round 5
@@ -391,6 +438,8 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
   }
   const int L = w.L;
   if (kSplit && tid < D / 16 - kPinnWaves) s_flag[tid] = 0;
+  if (tid < 3 * (H / 16)) s_fh[tid / (H / 16)][tid % (H / 16)] = 0;
+  if (tid < D / 16) s_fs[tid] = 0;
   float *const s_bias = reinterpret_cast<float *>(s_bias4);
   for (int l = 0; l < L; ++l)
     for (int i = tid; i < (l == L - 1 ? D : H); i += NTH) s_bias[l * H + i] = w.b[l][i];
@@ -415,7 +464,30 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
 #pragma unroll
       for (int j = 0; j < NT; ++j) wq[kb][j] = *reinterpret_cast<const f4v *>(r0.p[j] + 256 * kb);
   }
-  for (int t = 0; t < T; ++t) {
+  if constexpr (kFlags) {
+    float *const act2 = reinterpret_cast<float *>(s_act4[kFlags ? 2 : 0]);
+    auto hb = [&](int i) { return i == 0 ? act0 : (i == 1 ? act1 : act2); };
+    const int nic = B - b0 < kPinnIcs ? (int)(B - b0) : kPinnIcs;
+    for (int t = 0; t < T; ++t) {
+      const int G = t * L;  // tags: layer l of step t publishes G + l + 1
+      pinn_layer<D, H / 16, 0, H / 16, NT>(row(0), s_bias, s_state, hb(0), wave, lane, wq, row(1), PinnSplit{},
+                                           PinnSync{s_fs, G, s_fh[0], G + 1});
+      for (int l = 1; l < L - 1; ++l)
+        pinn_layer<H, H / 16, 0, H / 16, NT>(row(l), s_bias + l * H, hb((l - 1) % 3), hb(l % 3), wave, lane, wq,
+                                             row(l + 1), PinnSplit{},
+                                             PinnSync{s_fh[(l - 1) % 3], G + l, s_fh[l % 3], G + l + 1});
+      PinnSync sl{s_fh[(L - 2) % 3], G + L - 1, s_fs, G + L,
+                  traj ? traj + b0 * ldt + (int64_t)(t + 1) * D : nullptr, ldt, nic};
+      if constexpr (kSplit)
+        pinn_layer<H, D / 16, 1, D / 16, NT, true>(row(L - 1), s_bias + (L - 1) * H, hb((L - 2) % 3), s_state, wave,
+                                                   lane, wq, row(0), PinnSplit{s_part, s_flag, t + 1}, sl);
+      else
+        pinn_layer<H, D / 16, 1, D / 16, NT>(row(L - 1), s_bias + (L - 1) * H, hb((L - 2) % 3), s_state, wave, lane,
+                                             wq, row(0), PinnSplit{}, sl);
+    }
+    __syncthreads();  // every wave's last state tiles stored
+  }
+  for (int t = 0; t < (kFlags ? 0 : T); ++t) {
     pinn_layer<D, H / 16, 0, H / 16, NT>(row(0), s_bias, s_state, act0, wave, lane, wq, row(1));
     __syncthreads();
     for (int l = 1; l < L - 1; ++l) {
