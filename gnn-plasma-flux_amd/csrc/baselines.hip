@@ -407,8 +407,12 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
   static_assert(H >= D, "the widest layer sets the tiles per wave");
   constexpr int NTH = 64 * kPinnWaves;
   __shared__ f4v s_state4[D * kPinnIcs / 4];
+// HF_PINN_FLAGS=1: the barrier-free hand-off (PinnSync).  Measured and not
+// kept: correct (tests/test_gpu_baselines.py) but 12 % slower than the
+// barriers (profiles/r06_models_ab.txt, run 3): without a barrier the older
+// wave of each SIMD pair runs ahead and then waits on the younger one's tiles.
 #ifndef HF_PINN_FLAGS
-#define HF_PINN_FLAGS 1
+#define HF_PINN_FLAGS 0
 #endif
   constexpr bool kFlags = HF_PINN_FLAGS;
   __shared__ f4v s_act4[kFlags ? 3 : 2][H * kPinnIcs / 4];
