@@ -441,6 +441,9 @@ __global__ __launch_bounds__(64 * kPinnWaves, 1) void pinn_run_kernel(PinnW w, c
     if (traj && b0 + n < B) traj[b * ldt + d] = v;
   }
   const int L = w.L;
+#ifdef HF_EXP_PINN_PRIO  // experiment: static issue priority 1 for the second-dispatched half (waves 4-7)
+  if (wave >= kPinnWaves / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   if (kSplit && tid < D / 16 - kPinnWaves) s_flag[tid] = 0;
   if (tid < 3 * (H / 16)) s_fh[tid / (H / 16)][tid % (H / 16)] = 0;
   if (tid < D / 16) s_fs[tid] = 0;
@@ -662,6 +665,9 @@ __global__ __launch_bounds__(64 * (H / 16), HF_PURE_WG) void pure_run_kernel(Pur
     if (traj) traj[b * ldt + i] = v;
   }
   for (int i = tid; i < NX; i += NTH) s_x[i] = x[i];
+#ifdef HF_EXP_PURE_PRIO  // experiment: static issue priority 1 for the second-dispatched half
+  if (u >= H / 32) __builtin_amdgcn_s_setprio(1);
+#endif
   __syncthreads();
 #ifndef HF_PURE_MFMA_IO
 #define HF_PURE_MFMA_IO 1
