@@ -518,11 +518,14 @@ def test_loss_terms_any_nx(hf, nx):
 
 
 def _rollout_cfgs(hf):
-    k5 = dict(hf.ABLATION_CONFIGS["full"], rollout_steps=5)  # energies reach forwards 1 and 2
-    return {"full": hf.ABLATION_CONFIGS["full"], "rollout_only": hf.ABLATION_CONFIGS["rollout_only"], "full_k5": k5}
+    full = hf.ABLATION_CONFIGS["full"]
+    return {"full": full, "rollout_only": hf.ABLATION_CONFIGS["rollout_only"],
+            "full_k1": dict(full, rollout_steps=1),   # energies [e_0]: the term is 0
+            "full_k2": dict(full, rollout_steps=2),   # e_0, e_1 (u_1 from the sample's E)
+            "full_k5": dict(full, rollout_steps=5)}   # energies reach forwards 1 and 2
 
 
-@pytest.mark.parametrize("cfg_name", ["full", "rollout_only", "full_k5"])
+@pytest.mark.parametrize("cfg_name", ["full", "rollout_only", "full_k1", "full_k2", "full_k5"])
 def test_rollout_term_without_redundant_forwards_bitwise(hf, cfg_name):
     """The rollout energy term with only the forwards that reach an energy
     (ablation_loss rollout='reuse': forward 0 is the main forward, reused;
@@ -550,7 +553,7 @@ def test_rollout_term_without_redundant_forwards_bitwise(hf, cfg_name):
         assert np.array_equal(out[0][2][k], out[1][2][k]), k
 
 
-@pytest.mark.parametrize("cfg_name", ["full", "rollout_only", "full_k5"])
+@pytest.mark.parametrize("cfg_name", ["full", "rollout_only", "full_k1", "full_k2", "full_k5"])
 def test_fused_rollout_term_vs_literal(hf, cfg_name):
     """hf_ablation_loss_ex (the rollout energy term formed in the loss pass from
     the main forward's flux, K <= 3; for K = 5 the term from the reuse form's
@@ -576,11 +579,14 @@ def test_fused_rollout_term_vs_literal(hf, cfg_name):
     assert abs(out[0][1] - out[1][1]) <= 2e-6 * abs(out[1][1])
     for k in out[0][2]:
         grads_close(out[0][2][k], out[1][2][k], 1e-5)
-    # the term is really there: the same loss without it differs
+    # the term is really there (K >= 2): the same loss without it differs; K = 1 adds exactly 0
     base = dict(cfg, lambda_energy_multi=0.0)
     with torch.no_grad():
         l0, _ = ablation_loss(m, st, ft, sn, xd, solver.dt, solver.dx, base, solver.grid)
-    assert l0.item() != out[0][0]
+    if cfg["rollout_steps"] >= 2:
+        assert l0.item() != out[0][0]
+    else:
+        assert l0.item() == out[0][0]
 
 
 def test_flat_adam_invalidates_packed_inference_weights(hf):
