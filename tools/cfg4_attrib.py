@@ -33,8 +33,12 @@ LABELS = {
 
 def main(tag, tl=None):
     rows = {}
-    for f in glob.glob(os.path.join(ROOT, "gpurun_out", f"ab_cfg4tl_{tag}_*.json")):
-        m = re.match(rf"ab_cfg4tl_{re.escape(tag)}_(.+)_(\d+)\.json$", os.path.basename(f))
+    # tools/gpu_ab.sh cfg4tl names its outputs ab_cfg4tl_<tag>_*, tools/gpu_cfg4_timeline.sh tl_<tag>_*
+    files = glob.glob(os.path.join(ROOT, "gpurun_out", f"ab_cfg4tl_{tag}_*.json")) + \
+        [f for f in glob.glob(os.path.join(ROOT, "gpurun_out", f"tl_{tag}_*.json"))
+         if re.match(rf"tl_{re.escape(tag)}_lib.+_\d+\.json$", os.path.basename(f))]
+    for f in files:
+        m = re.match(rf"(?:ab_cfg4tl|tl)_{re.escape(tag)}_(.+)_(\d+)\.json$", os.path.basename(f))
         if not m:
             continue
         d = json.load(open(f))
