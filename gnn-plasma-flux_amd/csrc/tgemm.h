@@ -47,6 +47,13 @@ constexpr bool kDiagNoEpi = true;
 #else
 constexpr bool kDiagNoEpi = false;
 #endif
+#ifndef HF_TG_FRAG_AHEAD
+#define HF_TG_FRAG_AHEAD 1
+#endif
+#ifndef HF_TG_PAIR_LOOP
+#define HF_TG_PAIR_LOOP 1
+#endif
+constexpr bool kFragAhead = HF_TG_FRAG_AHEAD, kPairLoop = HF_TG_PAIR_LOOP;
 constexpr int kBM = 128, kBN = 128, kKC = HF_TG_KC;  // reduction chunk per stage (32; 16: a build knob)
 constexpr int kNQ = kBM * kKC / 4 / 256;             // float4 per thread per operand per stage
 constexpr int kIMSh = kKC == 32 ? 3 : 2;             // log2(float4 per [i][r] row)
@@ -313,6 +320,21 @@ __device__ __forceinline__ void tg_block(unsigned &bx, unsigned &by, unsigned &b
   }
 }
 
+// HF_TG_STAGGER > 0 (a build knob): a workgroup whose waves hold an odd wave
+// slot on their SIMDs (the second workgroup of a CU, HW_REG_HW_ID.WAVE_ID)
+// starts s_sleep(HF_TG_STAGGER) x 64 cycles late, so that the two workgroups
+// sharing each SIMD reach their LDS stores and barriers at different times
+// (MI355X_MICROARCH.md, "two waves that run the same program")
+#ifndef HF_TG_STAGGER
+#define HF_TG_STAGGER 0
+#endif
+__device__ __forceinline__ void tg_stagger() {
+  if constexpr (HF_TG_STAGGER > 0) {
+    const unsigned slot = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4);  // HW_ID[3:0]
+    if (slot & 1) __builtin_amdgcn_s_sleep(HF_TG_STAGGER);
+  }
+}
+
 // One output tile (bx, by) of split bz: the body of tgemm_kernel and of
 // tgemm_batch_kernel.
 template <class LA, bool ARM, class LB, bool BRM, class Epi, bool COLSUM, bool EX = false>
@@ -427,9 +449,8 @@ __device__ __forceinline__ void tgemm_tile(LA ga, LB gb, Epi epi, int64_t I, int
       gload(0, r0 + kKC);
     }
     const float *A = sA[cur], *B = sB[cur];
-#pragma unroll
-    for (int g = 0; g < kKC / 8; ++g) {
-      float av[2][4], bv[2][4];
+    // fragments of group g (8 reduction rows): av[x][s] / bv[x][s] for MFMA step s
+    auto frag = [&](int g, float (&av)[2][4], float (&bv)[2][4]) {
 #pragma unroll
       for (int x = 0; x < 2; ++x) {
         const int il = 64 * wi + 32 * x + (lane & 31), jl = 64 * wj + 32 * x + (lane & 31);
@@ -450,22 +471,58 @@ __device__ __forceinline__ void tgemm_tile(LA ga, LB gb, Epi epi, int64_t I, int
           for (int s = 0; s < 4; ++s) bv[x][s] = v[s];
         }
       }
+    };
+    auto mfma16 = [&](const float (&av)[2][4], const float (&bv)[2][4]) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
           for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][s], bv[b][s], acc[a][b], 0, 0, 0);
+    };
+    if constexpr (kFragAhead) {
+      // group g + 1's fragments are read while group g's 16 MFMAs run: the
+      // wave keeps its own MFMA pipe fed instead of waiting one LDS latency
+      // per MFMA step for the other wave of its SIMD to cover it
+      float av[2][2][4], bv[2][2][4];
+      frag(0, av[0], bv[0]);
+#pragma unroll
+      for (int g = 0; g < kKC / 8; ++g) {
+        if (g + 1 < kKC / 8) frag(g + 1, av[(g + 1) & 1], bv[(g + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);  // the next group's ds_reads stay ahead of this group's MFMAs
+        mfma16(av[g & 1], bv[g & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < kKC / 8; ++g) {
+        float av[2][4], bv[2][4];
+        frag(g, av, bv);
+        mfma16(av, bv);
+      }
     }
     if (!kDiagNoLs && r0 + kKC < re) lstore(cur ^ 1, (cur ^ 1) % kDepth, r0 + kKC);
     if (!kDiagNoBar) __syncthreads();
   };
-  for (int64_t r0 = rb; r0 < re;) {
-    stage(std::integral_constant<int, 0>{}, r0);
-    r0 += kKC;
-    if (r0 >= re) break;
-    stage(std::integral_constant<int, 1>{}, r0);
-    r0 += kKC;
+  if (kPairLoop) {
+    // stage pairs, then an odd last stage: no exit from between the two
+    // parities, whose accumulators the compiler otherwise copied to the exit's
+    // registers every pair (64 VGPRs and 32 moves behind an MFMA drain)
+    const int nst = rb < re ? (int)((re - rb + kKC - 1) / kKC) : 0;
+    int k = 0;
+    for (; k + 2 <= nst; k += 2) {
+      stage(std::integral_constant<int, 0>{}, rb + (int64_t)k * kKC);
+      stage(std::integral_constant<int, 1>{}, rb + (int64_t)(k + 1) * kKC);
+    }
+    if (k < nst) stage(std::integral_constant<int, 0>{}, rb + (int64_t)k * kKC);
+  } else {
+    for (int64_t r0 = rb; r0 < re;) {
+      stage(std::integral_constant<int, 0>{}, r0);
+      r0 += kKC;
+      if (r0 >= re) break;
+      stage(std::integral_constant<int, 1>{}, r0);
+      r0 += kKC;
+    }
   }
   if constexpr (Epi::kBlock) {
     static_assert(kBM * EpiMsg::kS <= 2 * kBufF, "a parked P or Q tile fits one operand's two buffers");
@@ -530,6 +587,7 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_kernel(LA ga, LB gb, Epi 
                                                        int64_t rsplit, float *bias_part) {
   unsigned bx, by, bz;
   tg_block(bx, by, bz);
+  tg_stagger();
   tgemm_tile<LA, ARM, LB, BRM, Epi, COLSUM, EX>(ga, gb, epi, I, J, R, rsplit, bias_part, bx, by, bz);
 }
 
@@ -553,6 +611,7 @@ __global__ __launch_bounds__(256, HF_TG_WG) void tgemm_batch_kernel(TgBatch<LA, 
                                                              int64_t R, int64_t rsplit) {
   unsigned bx, by, bz;
   tg_block(bx, by, bz);
+  tg_stagger();
   const unsigned pb = bz / (unsigned)bt.S, sz = bz - pb * (unsigned)bt.S;
   tgemm_tile<LA, ARM, LB, BRM, Epi, COLSUM, EX>(bt.a[pb], bt.b[pb], bt.e[pb], I, J, R, rsplit, bt.bias_part[pb], bx, by,
                                                 sz);

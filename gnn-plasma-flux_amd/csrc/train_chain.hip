@@ -92,8 +92,15 @@ static_assert(kPrSlices == 8 || kPrSlices == 16, "slices: a power of two, 32 x s
 __global__ __launch_bounds__(32 * kPrSlices) void part_reduce4_kernel(const float *__restrict__ part, int S, int64_t I,
                                                                       int64_t J, float *out, int ish, int64_t ld,
                                                                       int64_t hoff, const float *__restrict__ bias_part,
-                                                                      int64_t nbias, float *bias) {
+                                                                      int64_t nbias, float *bias, int64_t part_ps = 0,
+                                                                      int64_t out_ps = 0, int64_t bpart_ps = 0,
+                                                                      int64_t bias_ps = 0) {
   __shared__ f4 s_q[kPrSlices][32];
+  // problem blockIdx.y (batched reductions): each pointer advanced by its stride
+  part += blockIdx.y * part_ps;
+  out += blockIdx.y * out_ps;
+  bias_part += blockIdx.y * bpart_ps;
+  if (bias) bias += blockIdx.y * bias_ps;
   const int c = threadIdx.x & 31, q = threadIdx.x >> 5;
   const int64_t n4 = I * J / 4, wblocks = (n4 + 31) / 32;
   const bool wb = blockIdx.x < wblocks;
@@ -137,6 +144,16 @@ __global__ __launch_bounds__(32 * kPrSlices) void part_reduce4_kernel(const floa
 inline unsigned part_reduce4_blocks(int64_t I, int64_t J, int64_t nbias) {
   return (unsigned)((I * J / 4 + 31) / 32 + (nbias / 4 + 31) / 32);
 }
+// NP problems of one shape at per-problem strides (float4 form only): one launch
+inline bool launch_part_reduce_batch(int NP, const float *part, int64_t part_ps, int S, int64_t I, int64_t J,
+                                     float *out, int64_t out_ps, int ish, int64_t ld, int64_t hoff,
+                                     const float *bias_part, int64_t bpart_ps, int64_t nbias, float *bias,
+                                     int64_t bias_ps, hipStream_t s) {
+  if (!(J % 4 == 0 && I % 4 == 0 && nbias % 4 == 0)) return false;
+  hipLaunchKernelGGL(part_reduce4_kernel, dim3(part_reduce4_blocks(I, J, nbias), (unsigned)NP), dim3(32 * kPrSlices), 0,
+                     s, part, S, I, J, out, ish, ld, hoff, bias_part, nbias, bias, part_ps, out_ps, bpart_ps, bias_ps);
+  return true;
+}
 // the float4 form where the shapes allow it
 #ifndef HF_PART_REDUCE4
 #define HF_PART_REDUCE4 1
@@ -145,7 +162,7 @@ inline void launch_part_reduce(const float *part, int S, int64_t I, int64_t J, f
                                int64_t hoff, const float *bias_part, int64_t nbias, float *bias, hipStream_t s) {
   if (HF_PART_REDUCE4 && J % 4 == 0 && I % 4 == 0 && nbias % 4 == 0)
     hipLaunchKernelGGL(part_reduce4_kernel, dim3(part_reduce4_blocks(I, J, nbias)), dim3(32 * kPrSlices), 0, s, part, S, I, J,
-                       out, ish, ld, hoff, bias_part, nbias, bias);
+                       out, ish, ld, hoff, bias_part, nbias, bias, 0, 0, 0, 0);
   else
     hipLaunchKernelGGL(part_reduce_kernel, dim3(part_reduce_blocks(I, J, nbias)), dim3(256), 0, s, part, S, I, J, out,
                        ish, ld, hoff, bias_part, nbias, bias);
@@ -692,7 +709,193 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const float *__restrict
 #define HF_WGRAD_SPLITS 256
 #endif
 constexpr int kWgradSplits = HF_WGRAD_SPLITS;
+// the update layers' weight-gradient GEMMs in one launch (HF_TRAIN_WG_BATCH):
+// L x 2 column tiles x these splits fill the CUs on their own, and fewer
+// splits write and re-read fewer partial tiles
+#ifndef HF_WGRAD_BATCH_SPLITS
+#define HF_WGRAD_BATCH_SPLITS 64
+#endif
+constexpr int kWgradBatchSplits = HF_WGRAD_BATCH_SPLITS;
+// 1: the layers' split reductions in one launch
+#ifndef HF_PR_BATCH
+#define HF_PR_BATCH 1
+#endif
 constexpr int kInputSplits = 1024;
+
+// The update layers' weight gradients on the chain (fused path: H = 128, chains
+// of nx % 32 == 0 cells), every layer in one launch, split-K over the cells m:
+//   part[z][o][k] = sum_{m in split z} G[m][o] [h ; agg h][m][k],  k < 2H
+//   bias_part[z][o] = sum_{m in split z} G[m][o]
+// (G = g[l+1], h = h[l]; src/flux_gnn.py:53-60), the layout and arithmetic of
+// tgemm's EpiPart / COLSUM partials, bit for bit: every output accumulates the
+// same products in the same order (stages of 32 cells, 8-cell groups, MFMA
+// steps), so that the reductions are unchanged.  What differs from tgemm_batch
+// over VStencil: ONE workgroup owns the whole 128 x 256 tile of a split, so
+// h's rows are staged once per stage instead of once per column tile, and they
+// are staged raw with the chain's two halo rows (the cell before the stage's
+// first, the cell after its last; a 32-cell stage never straddles chains when
+// nx % 32 == 0): the agg half is formed at fragment-read time as
+// (h[next] + h[prev]) * 0.5 from rows k + 2 and k of the staged block (the
+// value VStencil::combine forms), with no second load, no select and no
+// per-row neighbour offsets.  Waves: (wi, wj) = 64 outputs o x the self
+// (wj = 0) or the agg (wj = 1) half, 2 x 4 v_mfma_f32_32x32x2_f32 tiles.
+constexpr int kWsH = 128, kWsKC = 32, kWsStr = 136;  // LDS rows: 136 floats (tgemm's kStrRM)
+struct WgStencilBatch {
+  const float *g[kTgMaxBatch], *x[kTgMaxBatch];
+  float *part[kTgMaxBatch], *bpart[kTgMaxBatch];
+  int n, S;
+};
+#ifndef HF_WGS_SPLITS
+#define HF_WGS_SPLITS 128
+#endif
+constexpr int kWgsSplits = HF_WGS_SPLITS;
+#ifndef HF_WGS_FRAG_AHEAD
+#define HF_WGS_FRAG_AHEAD 0
+#endif
+constexpr bool kWsFragAhead = HF_WGS_FRAG_AHEAD;
+__global__ __launch_bounds__(256, 2) void wgrad_stencil_kernel(WgStencilBatch bt, int64_t N, int nx, int64_t rsplit) {
+  __shared__ float sA[2][kWsKC * kWsStr];
+  __shared__ float sB[2][(kWsKC + 2) * kWsStr];
+  __shared__ f4 s_cs[256];
+  tg_stagger();
+#ifdef HF_EXP_WGS_AGPR
+  asm volatile("" ::: "a0");  // (A/B: accumulators in AGPRs)
+#endif
+  const unsigned pb = blockIdx.x / (unsigned)bt.S, z = blockIdx.x - pb * (unsigned)bt.S;
+  const float *__restrict__ G = bt.g[pb];
+  const float *__restrict__ X = bt.x[pb];
+  const int t = threadIdx.x, lane = t & 63, h = lane >> 5, c4 = 4 * (t & 31);
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6), wi = wave >> 1, wj = wave & 1;
+  // (N * H < 2^31, host-checked: 32-bit cell arithmetic)
+  const int rb = (int)((int64_t)z * rsplit), re = (int)(rb + rsplit < N ? rb + rsplit : N);
+  const int nst = rb < re ? (re - rb) / kWsKC : 0;  // whole stages (host-checked)
+  f4 ra[4], rx[4], rh = f4{0.f, 0.f, 0.f, 0.f}, csum = f4{0.f, 0.f, 0.f, 0.f};
+  // the stage at r0: rows r0 + (t >> 5) + 8q of G and h, and (t < 64) the halo
+  // row of h: t < 32 the cell before r0 on its chain, else the cell after r0 + 31
+  auto gload = [&](int r0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned off = (unsigned)((r0 + (t >> 5) + 8 * q) * kWsH + c4);
+      ra[q] = *reinterpret_cast<const f4 *>(G + off);
+      rx[q] = *reinterpret_cast<const f4 *>(X + off);
+    }
+    if (t < 64) {
+      const int i0 = (int)((unsigned)r0 % (unsigned)nx);
+      const int hr = t < 32 ? (i0 == 0 ? r0 + nx - 1 : r0 - 1) : (i0 + kWsKC == nx ? r0 + kWsKC - nx : r0 + kWsKC);
+      rh = *reinterpret_cast<const f4 *>(X + (unsigned)(hr * kWsH + c4));
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (t >> 5) + 8 * q;
+      *reinterpret_cast<f4 *>(&sA[buf][row * kWsStr + c4]) = ra[q];
+      *reinterpret_cast<f4 *>(&sB[buf][(row + 1) * kWsStr + c4]) = rx[q];
+      csum += ra[q];
+    }
+    if (t < 64) *reinterpret_cast<f4 *>(&sB[buf][(t < 32 ? 0 : kWsKC + 1) * kWsStr + c4]) = rh;
+  };
+  // The whole pipeline for the wave's half (AGG: the agg half): one copy per
+  // half, so that neither the stage loop nor the accumulators cross a branch
+  // (the waves of both halves pass the same barriers).
+  auto run = [&](auto agg) {
+    constexpr bool AGG = decltype(agg)::value;
+    f16 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
+    if (nst > 0) {
+      gload(rb);
+      lstore(0);
+    }
+    __syncthreads();
+    auto stage = [&](auto parity, int k) {
+      constexpr int cur = decltype(parity)::value;
+      if (k + 1 < nst) gload(rb + (k + 1) * kWsKC);
+      const float *A = sA[cur], *B = sB[cur];
+      // fragments of group g (8 cells): av[x][s], bv[b][s] for MFMA step s
+      auto frag = [&](int g, float (&av)[2][4], float (&bv)[4][4]) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int r = 8 * g + 4 * h + s;
+#pragma unroll
+          for (int x = 0; x < 2; ++x) av[x][s] = A[r * kWsStr + 64 * wi + 32 * x + (lane & 31)];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            if constexpr (AGG)
+              bv[b][s] = (B[(r + 2) * kWsStr + 32 * b + (lane & 31)] + B[r * kWsStr + 32 * b + (lane & 31)]) * 0.5f;
+            else
+              bv[b][s] = B[(r + 1) * kWsStr + 32 * b + (lane & 31)];
+          }
+        }
+      };
+      auto mfma32 = [&](const float (&av)[2][4], const float (&bv)[4][4]) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][s], bv[b][s], acc[a][b], 0, 0, 0);
+      };
+      if constexpr (kWsFragAhead) {
+        // group g + 1's fragments are read (and formed) before group g's 32
+        // MFMAs issue: one LDS wait per group instead of one per MFMA step
+        float av[2][2][4], bv[2][4][4];
+        frag(0, av[0], bv[0]);
+#pragma unroll
+        for (int g = 0; g < kWsKC / 8; ++g) {
+          if (g + 1 < kWsKC / 8) frag(g + 1, av[(g + 1) & 1], bv[(g + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+          mfma32(av[g & 1], bv[g & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < kWsKC / 8; ++g) {
+          float av[2][4], bv[4][4];
+          frag(g, av, bv);
+          mfma32(av, bv);
+        }
+      }
+      if (k + 1 < nst) lstore(cur ^ 1);
+      __syncthreads();
+    };
+    int k = 0;
+    for (; k + 2 <= nst; k += 2) {
+      stage(std::integral_constant<int, 0>{}, k);
+      stage(std::integral_constant<int, 1>{}, k + 1);
+    }
+    if (k < nst) stage(std::integral_constant<int, 0>{}, k);
+    float *part = bt.part[pb] + (int64_t)z * kWsH * 2 * kWsH;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int j = (AGG ? kWsH : 0) + 32 * b + (lane & 31);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          part[(64 * wi + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3)) * (2 * kWsH) + j] = acc[a][b][v];
+    }
+  };
+  if (wj) run(std::true_type{});
+  else run(std::false_type{});
+  // thread t summed rows t >> 5 (+ 8q) of columns c4..c4+3: fold the 8 row groups in order (tgemm's COLSUM)
+  s_cs[t] = csum;
+  __syncthreads();
+  if (t < 32) {
+    f4 v = s_cs[t];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) v += s_cs[t + 32 * q];
+    *reinterpret_cast<f4 *>(bt.bpart[pb] + (int64_t)z * kWsH + 4 * t) = v;
+  }
+}
+// splits of N cells (whole stages)
+inline int64_t wgs_rsplit(int64_t N) { return ((N + kWgsSplits - 1) / kWgsSplits + kWsKC - 1) / kWsKC * kWsKC; }
+inline int64_t wgs_splits(int64_t N) { return (N + wgs_rsplit(N) - 1) / wgs_rsplit(N); }
 
 inline size_t al256(size_t v) { return (v + 255) & ~size_t(255); }
 
@@ -767,6 +970,10 @@ bool fused_chain(const GraphW &w, int nx, int64_t N) { return HF_TRAIN_FUSED && 
 #ifndef HF_TRAIN_WG_BATCH
 #define HF_TRAIN_WG_BATCH 1
 #endif
+// 1: those GEMMs on wgrad_stencil_kernel (H = 128, nx % 32 == 0)
+#ifndef HF_TRAIN_WGS
+#define HF_TRAIN_WGS 1
+#endif
 int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   const int64_t H = w.hidden;
   size_t b = al256(sizeof(float) * N * 2 * H);  // dPQ
@@ -779,7 +986,8 @@ int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   if (fused_width(w)) {  // fused backward: g[0..L] side by side + the transposed weights
     b += (w.layers + 1) * al256(sizeof(float) * N * H) + al256((size_t)chain_train_bwd_pack_bytes(w.layers));
     // + every update layer's weight-gradient partials (the layers' GEMMs in one launch)
-    if (HF_TRAIN_WG_BATCH) b += w.layers * (al256(sizeof(float) * S * 2 * H * H) + al256(sizeof(float) * S * 2 * H));
+    const int64_t SB = std::max(tgemm_splits(N, kWgradBatchSplits), wgs_splits(N));
+    if (HF_TRAIN_WG_BATCH) b += w.layers * (al256(sizeof(float) * SB * 2 * H * H) + al256(sizeof(float) * SB * 2 * H));
     // + the readout's per-IC dw2 / db2 partials of the folded edge backward (B <= N / 16)
     if (HF_TRAIN_EDGE_FOLD) b += al256(sizeof(float) * (N / 16 + 1) * (H + 1));
   }
@@ -843,10 +1051,14 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   float *G = fused ? take((L + 1) * al256(sizeof(float) * N * H)) : nullptr;
   void *bpack = fused ? static_cast<void *>(take((size_t)chain_train_bwd_pack_bytes(L))) : nullptr;
   const bool wg_batch = fused && HF_TRAIN_WG_BATCH && L >= 1 && L <= kTgMaxBatch;
-  const int64_t lpstride = (int64_t)(al256(sizeof(float) * S * 2 * H * H) / 4),
-                lbstride = (int64_t)(al256(sizeof(float) * S * 2 * H) / 4);
-  float *lpart = wg_batch ? take(L * al256(sizeof(float) * S * 2 * H * H)) : nullptr;
-  float *lbpart = wg_batch ? take(L * al256(sizeof(float) * S * 2 * H)) : nullptr;
+  // the layers' weight gradients: wgrad_stencil_kernel where its shapes hold, else tgemm_batch
+  const bool wgs = wg_batch && HF_TRAIN_WGS && H == kWsH && nx % kWsKC == 0 && N % kWsKC == 0 &&
+                   N * kWsH < (int64_t(1) << 31);
+  const int64_t SB = wgs ? wgs_splits(N) : tgemm_splits(N, kWgradBatchSplits);
+  const int64_t lpstride = (int64_t)(al256(sizeof(float) * SB * 2 * H * H) / 4),
+                lbstride = (int64_t)(al256(sizeof(float) * SB * 2 * H) / 4);
+  float *lpart = wg_batch ? take(L * al256(sizeof(float) * SB * 2 * H * H)) : nullptr;
+  float *lbpart = wg_batch ? take(L * al256(sizeof(float) * SB * 2 * H)) : nullptr;
   // the readout's backward folded into the backward pass (needs its readout pass: HF_TRAIN_RO_FOLD)
   const bool efold = fused && HF_TRAIN_EDGE_FOLD && HF_TRAIN_RO_FOLD && H == 128;
   float *efpart = efold ? take(sizeof(float) * (N / 16 + 1) * (H + 1)) : nullptr;
@@ -898,7 +1110,25 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
                        (int)(N / nx), H, const_cast<float *>(g.w_2), const_cast<float *>(g.b_2));
     if ((e = readout_wgrad())) return e;
   }
-  if (wg_batch) {  // dW_l, db_l of every update layer: one launch, then the layers' reductions
+  if (wgs) {  // dW_l, db_l of every update layer: one launch, then the layers' reductions
+    WgStencilBatch bt{};
+    bt.n = L;
+    bt.S = (int)SB;
+    for (int l = 0; l < L; ++l) {
+      bt.g[l] = G + (l + 1) * gstride;
+      bt.x[l] = t.h[l];
+      bt.part[l] = lpart + l * lpstride;
+      bt.bpart[l] = lbpart + l * lbstride;
+    }
+    hipLaunchKernelGGL(wgrad_stencil_kernel, dim3((unsigned)(SB * L)), dim3(256), 0, s, bt, N, nx, wgs_rsplit(N));
+    if (!(HF_PR_BATCH && launch_part_reduce_batch(L, lpart, lpstride, (int)SB, H, 2 * H, const_cast<float *>(g.w_l),
+                                                  g.lsw, kNoSplit, 2LL * H, 0, lbpart, lbstride, H,
+                                                  const_cast<float *>(g.b_l), g.lsb, s)))
+      for (int l = L - 1; l >= 0; --l)
+        launch_part_reduce(lpart + l * lpstride, (int)SB, H, 2 * H, const_cast<float *>(g.w_l + l * g.lsw), kNoSplit,
+                           2LL * H, 0, lbpart + l * lbstride, H, const_cast<float *>(g.b_l + l * g.lsb), s);
+    if ((e = hipGetLastError())) return e;
+  } else if (wg_batch) {  // the same with tgemm_batch over the stencil view
     TgBatch<VPlain, VStencil, EpiPart> bt{};
     bt.n = L;
     for (int l = 0; l < L; ++l) {
@@ -907,10 +1137,13 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
       bt.e[l] = EpiPart{lpart + l * lpstride, H, 2LL * H};
       bt.bias_part[l] = lbpart + l * lbstride;
     }
-    if ((e = tgemm_batch<VPlain, VStencil, EpiPart, true>(bt, H, 2 * H, N, kWgradSplits, s))) return e;
-    for (int l = L - 1; l >= 0; --l)
-      launch_part_reduce(lpart + l * lpstride, (int)S, H, 2 * H, const_cast<float *>(g.w_l + l * g.lsw), kNoSplit,
-                         2LL * H, 0, lbpart + l * lbstride, H, const_cast<float *>(g.b_l + l * g.lsb), s);
+    if ((e = tgemm_batch<VPlain, VStencil, EpiPart, true>(bt, H, 2 * H, N, kWgradBatchSplits, s))) return e;
+    if (!(HF_PR_BATCH && launch_part_reduce_batch(L, lpart, lpstride, (int)SB, H, 2 * H, const_cast<float *>(g.w_l),
+                                                  g.lsw, kNoSplit, 2LL * H, 0, lbpart, lbstride, H,
+                                                  const_cast<float *>(g.b_l), g.lsb, s)))
+      for (int l = L - 1; l >= 0; --l)
+        launch_part_reduce(lpart + l * lpstride, (int)SB, H, 2 * H, const_cast<float *>(g.w_l + l * g.lsw), kNoSplit,
+                           2LL * H, 0, lbpart + l * lbstride, H, const_cast<float *>(g.b_l + l * g.lsb), s);
     if ((e = hipGetLastError())) return e;
   }
   for (int l = L - 1; l >= 0 && !wg_batch; --l) {  // update layers, last to first                      (:53-60)

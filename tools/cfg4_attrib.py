@@ -6,7 +6,11 @@ repetitions; each row's cost is the drop from the row above, so the rows sum
 to the shipped figure by construction and the last row is what no switch
 removes.  Markdown on stdout.
 
-    python tools/cfg4_attrib.py TAG [timeline.json]
+    python tools/cfg4_attrib.py TAG [timeline.json [stripped_timeline.json]]
+
+stripped_timeline.json: the lane timeline of the last cumulative build
+(tools/cfg4_timeline.py under rocprofv3, HYBRIDFLUX_LIB = that build): what
+no switch removes, split into the kernels that still run and the gaps.
 """
 import glob
 import json
@@ -31,7 +35,7 @@ LABELS = {
 }
 
 
-def main(tag, tl=None):
+def main(tag, tl=None, strip=None):
     rows = {}
     # tools/gpu_ab.sh cfg4tl names its outputs ab_cfg4tl_<tag>_*, tools/gpu_cfg4_timeline.sh tl_<tag>_*
     files = glob.glob(os.path.join(ROOT, "gpurun_out", f"ab_cfg4tl_{tag}_*.json")) + \
@@ -68,6 +72,22 @@ def main(tag, tl=None):
         prev = a
     print(f"| left | what no switch removes | {prev['rand_L0']:.4f} | | {100 * prev['rand_L0'] / base['rand_L0']:.1f} % | "
           f"{prev['rand_L4']:.4f} | | {prev['W1_r2']:.4f} |")
+    if strip:
+        # the best (lowest L = 0) cumulative build: the trace was taken of it
+        best = min(order[1:], key=lambda k: avg[k]["rand_L0"])
+        r = {x["group"]: x for x in json.load(open(strip))["rows"]}["rand_L0"]
+        print(f"\nWhat no switch removes, from the kernel trace of `{best}` at L = 0 (ms per step; HIP-event "
+              f"step of that build {avg[best]['rand_L0']:.4f}):\n")
+        print("| piece | ms per step | share of the shipped L = 0 step |")
+        print("|---|---|---|")
+        for name, v in (("flux kernels' skeleton (grid dispatch, wave start, loop control and barriers with "
+                         "every piece removed; the three lanes' dispatches overlap)", r["flux_union_ms_per_step"]),
+                        ("other kernels exposed", r["exposed_other_ms_per_step"]),
+                        ("nothing running", r["idle_ms_per_step"])):
+            print(f"| {name} | {v:.4f} | {100 * v / base['rand_L0']:.1f} % |")
+        rest = avg[best]["rand_L0"] - r["span_ms_per_step"]
+        print(f"| unattributed (that build's HIP-event step less the traced span) | {rest:.4f} | "
+              f"{100 * rest / base['rand_L0']:.1f} % |")
     if tl:
         t = json.load(open(tl))
         print("\nLane timeline (rocprofv3 --kernel-trace of the same run, tools/cfg4_timeline.py analyze), ms per step:\n")
@@ -81,4 +101,4 @@ def main(tag, tl=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None, sys.argv[3] if len(sys.argv) > 3 else None)
