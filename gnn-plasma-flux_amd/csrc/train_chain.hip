@@ -534,16 +534,25 @@ __global__ __launch_bounds__(256) void loss_update_kernel(const float *__restric
 }
 
 // fixed-order block sum of 256 per-thread values (thread 0 returns it)
-__device__ __forceinline__ float block_sum256(float v, float *sh) {
-  sh[threadIdx.x] = v;
+// K block sums of 256 threads at once, each a fixed pairwise tree (t + w into
+// t for w = 128, 64, ..., 1), with 10 barriers for all K (one sum at a time
+// took 10 barriers per sum: 100 in a loss pass block)
+template <int K>
+__device__ __forceinline__ void block_sum256_multi(float (&v)[K], float (*sh)[256]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < K; ++k) sh[k][t] = v[k];
   __syncthreads();
   for (int w = 128; w >= 1; w >>= 1) {
-    if ((int)threadIdx.x < w) sh[threadIdx.x] = __fadd_rn(sh[threadIdx.x], sh[threadIdx.x + w]);
+    if (t < w) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) sh[k][t] = __fadd_rn(sh[k][t], sh[k][t + w]);
+    }
     __syncthreads();
   }
-  const float r = sh[0];
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = sh[k][0];
   __syncthreads();
-  return r;
 }
 
 // Per-sample sums part[b][0..6] = sum (F - F_t)^2, sum (n' - n'_t)^2,
@@ -557,7 +566,7 @@ __global__ __launch_bounds__(256) void loss_terms_kernel(const float *__restrict
                                                          const float *__restrict__ nn, const float *__restrict__ En,
                                                          int B, int nx, float c, float lam_s, float dt, int roll,
                                                          float *__restrict__ part, float *__restrict__ dfe) {
-  __shared__ float sh[256];
+  __shared__ float sh[kLossParts][256];
   const int b = blockIdx.x;
   const float *f = fe + (int64_t)b * 2 * nx, *n = st + (int64_t)b * 3 * nx, *F_t = ft + (int64_t)b * nx;
   const float *nt = sn + (int64_t)b * 3 * nx, *ut = nt + nx, *Et = nt + 2 * nx;
@@ -594,10 +603,9 @@ __global__ __launch_bounds__(256) void loss_terms_kernel(const float *__restrict
     dfe[(int64_t)b * 2 * nx + nx + i] = h;
   }
   const int np_ = roll >= 2 ? kLossParts : 7;
-  for (int k = 0; k < np_; ++k) {
-    const float v = block_sum256(s[k], sh);
-    if (threadIdx.x == 0) part[(int64_t)b * kLossParts + k] = v;
-  }
+  block_sum256_multi(s, sh);
+  if (threadIdx.x == 0)
+    for (int k = 0; k < np_; ++k) part[(int64_t)b * kLossParts + k] = s[k];
 }
 
 // loss_update_kernel + the detached Poisson solve (poisson_kernel's circulant
@@ -613,7 +621,7 @@ __global__ __launch_bounds__(256) void loss_step_kernel(const float *__restrict_
                                                         float *__restrict__ dfe) {
   extern __shared__ double s_cd[];  // c [nx] (double), then rho' [nx], n' [nx] (float)
   float *s_rho = reinterpret_cast<float *>(s_cd + nx), *s_np = s_rho + nx;
-  __shared__ float sh[256];
+  __shared__ float sh[kLossParts][256];
   const int b = blockIdx.x;
   const float *f = fe + (int64_t)b * 2 * nx, *n = st + (int64_t)b * 3 * nx, *F_t = ft + (int64_t)b * nx;
   const float *nt = sn + (int64_t)b * 3 * nx, *ut = nt + nx, *Et = nt + 2 * nx;
@@ -656,10 +664,9 @@ __global__ __launch_bounds__(256) void loss_step_kernel(const float *__restrict_
     dfe[(int64_t)b * 2 * nx + nx + i] = h;
   }
   const int np_ = roll >= 2 ? kLossParts : 7;
-  for (int k = 0; k < np_; ++k) {
-    const float v = block_sum256(sacc[k], sh);
-    if (threadIdx.x == 0) part[(int64_t)b * kLossParts + k] = v;
-  }
+  block_sum256_multi(sacc, sh);
+  if (threadIdx.x == 0)
+    for (int k = 0; k < np_; ++k) part[(int64_t)b * kLossParts + k] = sacc[k];
 }
 
 // loss = flux MSE + lam_s state MSE + lam_p Poisson MSE + lam_c charge + lam_e energy
@@ -669,28 +676,46 @@ __global__ __launch_bounds__(256) void loss_step_kernel(const float *__restrict_
 __global__ __launch_bounds__(256) void loss_final_kernel(const float *__restrict__ part, int B, int nx, float dx,
                                                          float lam_s, float lam_p, float lam_c, float lam_e,
                                                          float lam_m, int roll, float *loss, float *flux_loss) {
-  __shared__ float sh[256];
+  __shared__ float sh[6][256];
   float a[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const float *p = part + (int64_t)b * kLossParts;
-    if (roll >= 2) {  // energies e_k = 0.5 mean(u_k^2) (:181); k = 0 adds (e_0 - e_0)^2 = 0
-      const float e0 = __fmul_rn(0.5f, __fdiv_rn(p[7], (float)nx));
-      for (int k = 1; k < roll; ++k) {
-        const float d = __fsub_rn(__fmul_rn(0.5f, __fdiv_rn(p[7 + k], (float)nx)), e0);
-        a[5] = fmaf(d, d, a[5]);
-      }
-    }
-    a[0] = __fadd_rn(a[0], p[0]);
-    a[1] = __fadd_rn(a[1], p[1]);
-    a[2] = __fadd_rn(a[2], p[2]);
-    const float dq = __fsub_rn(__fmul_rn(p[4], dx), __fmul_rn(p[3], dx));          // charge_next - charge_t
-    a[3] = fmaf(dq, dq, a[3]);
-    const float de = __fsub_rn(__fmul_rn(0.5f, __fdiv_rn(p[5], (float)nx)), __fmul_rn(0.5f, __fdiv_rn(p[6], (float)nx)));
-    a[4] = fmaf(de, de, a[4]);
-  }
-  float t[6];
+  // 8 samples per round: every part of the 8 is loaded before the first one's
+  // sums (a sample at a time waited out one load latency each: 9 us at B = 2000);
+  // the sums run in the same sample order
+  constexpr int kU = 8;
+  for (int b0 = threadIdx.x; b0 < B; b0 += kU * blockDim.x) {
+    float q[kU][kLossParts];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) t[k] = block_sum256(a[k], sh);
+    for (int u = 0; u < kU; ++u) {
+      const int b = b0 + u * (int)blockDim.x;
+      const float *p = part + (int64_t)(b < B ? b : 0) * kLossParts;
+#pragma unroll
+      for (int k = 0; k < kLossParts; ++k) q[u][k] = p[k];  // (parts past those written are not used)
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (b0 + u * (int)blockDim.x >= B) break;
+      const float *p = q[u];
+      if (roll >= 2) {  // energies e_k = 0.5 mean(u_k^2) (:181); k = 0 adds (e_0 - e_0)^2 = 0
+        const float e0 = __fmul_rn(0.5f, __fdiv_rn(p[7], (float)nx));
+#pragma unroll
+        for (int k = 1; k < kLossMaxRollout; ++k) {
+          if (k >= roll) break;
+          const float d = __fsub_rn(__fmul_rn(0.5f, __fdiv_rn(p[7 + k], (float)nx)), e0);
+          a[5] = fmaf(d, d, a[5]);
+        }
+      }
+      a[0] = __fadd_rn(a[0], p[0]);
+      a[1] = __fadd_rn(a[1], p[1]);
+      a[2] = __fadd_rn(a[2], p[2]);
+      const float dq = __fsub_rn(__fmul_rn(p[4], dx), __fmul_rn(p[3], dx));  // charge_next - charge_t
+      a[3] = fmaf(dq, dq, a[3]);
+      const float de =
+          __fsub_rn(__fmul_rn(0.5f, __fdiv_rn(p[5], (float)nx)), __fmul_rn(0.5f, __fdiv_rn(p[6], (float)nx)));
+      a[4] = fmaf(de, de, a[4]);
+    }
+  }
+  float t[6] = {a[0], a[1], a[2], a[3], a[4], a[5]};
+  block_sum256_multi(t, sh);
   if (threadIdx.x == 0) {
     const float N = (float)B * (float)nx;
     const float fl = __fdiv_rn(t[0], N);
@@ -720,7 +745,10 @@ constexpr int kWgradBatchSplits = HF_WGRAD_BATCH_SPLITS;
 #ifndef HF_PR_BATCH
 #define HF_PR_BATCH 1
 #endif
-constexpr int kInputSplits = 1024;
+#ifndef HF_INPUT_SPLITS
+#define HF_INPUT_SPLITS 512
+#endif
+constexpr int kInputSplits = HF_INPUT_SPLITS;  // the input layer's weight-gradient splits
 
 // The update layers' weight gradients on the chain (fused path: H = 128, chains
 // of nx % 32 == 0 cells), every layer in one launch, split-K over the cells m:
@@ -758,9 +786,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_stencil_kernel(WgStencilBatch bt
   __shared__ float sB[2][(kWsKC + 2) * kWsStr];
   __shared__ f4 s_cs[256];
   tg_stagger();
-#ifdef HF_EXP_WGS_AGPR
-  asm volatile("" ::: "a0");  // (A/B: accumulators in AGPRs)
-#endif
   const unsigned pb = blockIdx.x / (unsigned)bt.S, z = blockIdx.x - pb * (unsigned)bt.S;
   const float *__restrict__ G = bt.g[pb];
   const float *__restrict__ X = bt.x[pb];

@@ -292,6 +292,49 @@ class FlatAdam(torch.optim.Optimizer):
         return loss
 
 
+def direct_step(model, opt, st, ft, sn, nf, x, dt, dx, cfg, grid):
+    """One step of the reference trainer's loop (ablation_loss ->
+    loss.backward() -> optimizer.step(), train_ablation.py:107-210) without
+    autograd where it reduces to three HIP passes and the optimizer launch:
+    FluxGNN with flat parameters (flatten_parameters_), FlatAdam over exactly
+    those parameters, the one-pass loss (rollout_steps <= 3), and the batch's
+    chain node features nf (FluxDataset.batch with x).  The forward
+    (hf_graph_forward_train), the loss and its flux gradient
+    (hf_ablation_loss_ex), the backward (hf_graph_backward) with that gradient
+    as the incoming one -- autograd's seed is 1 and _StepLoss.backward's
+    product dfe * 1 is dfe exactly -- and FlatAdam on the gradient buffer: the
+    same parameters bit for bit as the autograd step, without its seed fill,
+    gradient product and bookkeeping launches.  Parameter hooks are not run.
+    Returns (loss, flux_loss) detached, or None when the case does not apply
+    (the caller then takes the autograd step)."""
+    from .flux_gnn import _flat_view
+    if type(model) is not FluxGNN or not isinstance(opt, FlatAdam) or nf is None or not torch.is_grad_enabled():
+        return None
+    params = list(model.parameters())
+    if len(opt.param_groups) != 1 or [id(q) for q in opt.param_groups[0]["params"]] != [id(q) for q in params] \
+            or not all(q.requires_grad for q in params):
+        return None
+    dev = st.device
+    flat = _flat_view(params, dev)
+    K = cfg["rollout_steps"] if _has_rollout(cfg) else 0
+    if flat is None or K > engine.LOSS_MAX_ROLLOUT or abs(dt / dx - grid.dt / grid.dx) > 1e-12 * abs(dt / dx):
+        return None
+    B, _, nx = st.shape
+    dims = (model.input_dim, model.hidden_dim, model.num_layers)
+    flux, tape, nf_d, ei_d, chain_nx = engine.graph_forward_train(flat, dims, nf.detach(),
+                                                                  shared_chain_edge_index(nx, B, dev))
+    lam = (cfg["lambda_state"], cfg["lambda_poisson"], cfg["lambda_charge"], cfg["lambda_energy_one"],
+           cfg["lambda_energy_multi"])
+    loss, flux_loss, dfe = engine.ablation_loss_terms(grid, flux.reshape(B, 2 * nx), st, ft, sn, lam, K, dt)
+    gp, _ = engine.graph_backward(flat, dims, nf_d, ei_d, chain_nx, tape, dfe.reshape(-1), False)
+    o = 0
+    for q in params:
+        q.grad = gp[o:o + q.numel()].view_as(q)
+        o += q.numel()
+    opt.step()
+    return loss.detach(), flux_loss.detach()
+
+
 class GraphedStep:
     """One optimizer step of the reference trainer's loop (ablation_loss ->
     backward -> optimizer step, train_ablation.py:107-210) on a fixed batch
@@ -303,8 +346,9 @@ class GraphedStep:
     The warmup steps that precede the capture are ordinary eager steps on the
     first batches, so a pass makes exactly the eager loop's updates."""
 
-    def __init__(self, model, opt, data, batch_size, x, dt, dx, cfg, grid):
+    def __init__(self, model, opt, data, batch_size, x, dt, dx, cfg, grid, direct=True):
         self.args = (model, opt, data, x, dt, dx, cfg, grid)
+        self.direct = direct  # direct_step where it applies
         dev = data.state_t.device
         self.idx = torch.zeros(batch_size, dtype=torch.long, device=dev)
         self.graph = None
@@ -313,6 +357,10 @@ class GraphedStep:
     def _body(self):
         model, opt, data, x, dt, dx, cfg, grid = self.args
         st, ft, sn, nf = data.batch(self.idx, x, check=False)  # (train_steps checked the order)
+        if self.direct:
+            r = direct_step(model, opt, st, ft, sn, nf, x, dt, dx, cfg, grid)
+            if r is not None:
+                return r
         loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid, nf=nf)
         opt.zero_grad(set_to_none=True)
         loss.backward()
@@ -338,12 +386,14 @@ class GraphedStep:
         return self.out[0].clone(), self.out[1].clone()
 
 
-def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid, graphed=None, warmup=3):
+def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid, graphed=None, warmup=3, direct=True):
     """One pass over `order` (sample indices) in batches; returns (sum of
     losses, sum of flux losses) weighted by batch size, and the step count.
     graphed: a GraphedStep of this batch size (created by the caller and kept
     across passes); its first `warmup` steps run eagerly on a side stream, then
-    it is captured and every further full batch replays the graph."""
+    it is captured and every further full batch replays the graph.  direct:
+    eager steps take direct_step where it applies (the same parameters bit for
+    bit as the autograd step)."""
     tot, tot_flux, steps = 0.0, 0.0, 0
     losses = []
     data.check_indices(order)  # once per pass; the steps gather with check=False
@@ -364,11 +414,15 @@ def train_steps(model, opt, data, order, batch_size, x, dt, dx, cfg, grid, graph
                 loss, flux_loss = graphed(idx)
         else:
             st, ft, sn, nf = data.batch(idx, x, check=False)
-            loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid, nf=nf)
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-            loss, flux_loss = loss.detach(), flux_loss.detach()
+            r = direct_step(model, opt, st, ft, sn, nf, x, dt, dx, cfg, grid) if direct else None
+            if r is not None:
+                loss, flux_loss = r
+            else:
+                loss, flux_loss = ablation_loss(model, st, ft, sn, x, dt, dx, cfg, grid, nf=nf)
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+                loss, flux_loss = loss.detach(), flux_loss.detach()
         losses.append((loss, flux_loss, len(idx)))
         steps += 1
     for l, f, n in losses:  # one host sync per pass, not per step

@@ -348,6 +348,42 @@ def test_graphed_steps_equal_eager(hf):
         assert np.abs(res[0][1][k] - res[1][1][k]).max() <= 1e-6, k
 
 
+@pytest.mark.parametrize("cfg_name", ["physics", "full", "full_k5"])
+def test_direct_step_equals_autograd_step(hf, cfg_name):
+    """train_steps' direct_step (forward, one-pass loss, backward with the
+    loss's flux gradient as the incoming one, FlatAdam: no autograd) makes the
+    autograd step's updates bit for bit: losses and every parameter after 8
+    batches of 16, eager and graph-replayed.  'full_k5' (rollout_steps 5: the
+    energies need model forwards) takes the autograd step in both arms."""
+    from hybridflux.datagen import generate_dataset
+    from hybridflux.training import FlatAdam, FluxDataset, GraphedStep, direct_step, train_steps
+    st, ft, sn, x, dt, dx, nu = generate_dataset(num_initial_conditions=4, steps_per_ic=32, out_path=None, device=DEV)
+    data = FluxDataset(st, ft, sn, DEV)
+    solver = hf.BaselineSolver(64, device=DEV)
+    xd = torch.as_tensor(x, device=DEV)
+    cfg = dict(hf.ABLATION_CONFIGS["full"], rollout_steps=5) if cfg_name == "full_k5" else hf.ABLATION_CONFIGS[cfg_name]
+    order = torch.randperm(len(data), generator=torch.Generator().manual_seed(6))[:128].to(DEV)
+    res = []
+    arms = ((False, False), (True, False)) + (((True, True),) if cfg_name != "full_k5" else ())
+    for direct, graphed in arms:  # (K = 5's energies take a host value: not capturable)
+        torch.manual_seed(0)
+        m = hf.FluxGNN(4, 128, 4).to(DEV).flatten_parameters_()
+        opt = FlatAdam(m.parameters(), lr=1e-3)
+        gs = GraphedStep(m, opt, data, 16, xd, solver.dt, solver.dx, cfg, solver.grid, direct=direct) if graphed else None
+        tot, _, steps = train_steps(m, opt, data, order, 16, xd, solver.dt, solver.dx, cfg, solver.grid, graphed=gs,
+                                    direct=direct)
+        assert steps == 8 and (gs is None or gs.graph is not None)
+        res.append((tot, {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}))
+    # the direct step applies exactly where documented
+    b_st, b_ft, b_sn, nf = data.batch(order[:16], xd)
+    r = direct_step(m, opt, b_st, b_ft, b_sn, nf, xd, solver.dt, solver.dx, cfg, solver.grid)
+    assert (r is None) == (cfg_name == "full_k5")
+    for tot, sd in res[1:]:
+        assert tot == res[0][0]
+        for k in sd:
+            assert np.array_equal(sd[k].view(np.uint32), res[0][1][k].view(np.uint32)), k
+
+
 @pytest.mark.parametrize("cfg_name", ["baseline", "physics", "full"])
 def test_fused_step_loss_equals_torch_terms(hf, cfg_name):
     """hf_ablation_loss (the loss's single-step terms in one HIP pass, with its

@@ -51,11 +51,13 @@ def gpu_rate(hf, cfg_name, batch, steps, warmup, data, x, solver, graphed=False,
                torch.optim.Adam(m.parameters(), lr=1e-3))
     cfg = hf.ABLATION_CONFIGS[cfg_name]
     gen = torch.Generator().manual_seed(1)
-    gs = GraphedStep(m, opt, data, batch, x, solver.dt, solver.dx, cfg, solver.grid) if graphed else None
+    gs = GraphedStep(m, opt, data, batch, x, solver.dt, solver.dx, cfg, solver.grid,
+                     direct=not os.environ.get("HF_AB_NO_DIRECT")) if graphed else None
 
     def run(n):
         order = torch.randint(0, len(data), (n * batch,), generator=gen).to("cuda")
-        return train_steps(m, opt, data, order, batch, x, solver.dt, solver.dx, cfg, solver.grid, graphed=gs)
+        return train_steps(m, opt, data, order, batch, x, solver.dt, solver.dx, cfg, solver.grid, graphed=gs,
+                           direct=not os.environ.get("HF_AB_NO_DIRECT"))  # A/B switch: the autograd step
 
     run(warmup + (4 if graphed else 0))  # graphed: 3 eager warmup steps, the capture, then replays
     torch.cuda.synchronize()

@@ -69,6 +69,7 @@ for rep in $reps; do
     if [ $MODE = trainks ]; then
       db=$(find /tmp/ab_trainks_${TAG}_$n -name "*.db" | head -1)
       python3 tools/rocpd_summary.py "$db" > $o.md && grep -E "${PAT:-kernel}" $o.md | cut -d'|' -f2,3,5 | sed "s/^/$n /"
+      python3 tools/train_timeline.py "$db" > $o.timeline.md || exit 9
     fi
   done
 done
