@@ -252,7 +252,9 @@ def train_line(dev, batch=2000, steps=20, cfg_name="physics", warm_s=0.3, more=(
     eager with its single-kernel fused=True Adam (the same update), replaying
     the captured step (hybridflux.training.GraphedStep, fused capturable
     Adam), and eager / replayed with hybridflux's FlatAdam (the same update in
-    one launch over the parameter buffer); each warmed for warm_s, then `steps`
+    one launch over the parameter buffer; with it train_steps takes
+    hybridflux.training.direct_step, the autograd step's parameters bit for bit
+    without autograd's launches); each warmed for warm_s, then `steps`
     steps timed with HIP events + the wall clock.  Then the configs of `more`
     (the rollout-loss ablations 'full' and 'rollout_only', half of the
     reference's checkpoints) in the best mode.  FLOPs per sample: FluxGNN

@@ -434,8 +434,8 @@ __device__ __forceinline__ int kperm_dev(int s, int lane) { return 16 * (s >> 2)
 // optimizer changes them every step, so the host pack is no option.  One
 // thread per packed float: the stream's nstream floats, then the small arrays
 // (win [2][64][4], b_in, b_l[L], b_e, w2).
-__global__ void pack_chain_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream, float *__restrict__ small) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void pack_chain_f32_at(const GraphW &w, float *__restrict__ stream, int64_t nstream,
+                                                  float *__restrict__ small, int64_t idx) {
   const int L = w.layers;
   if (idx < nstream) {
     const int c = (int)(idx >> 11), rem = (int)(idx & 2047), j = rem >> 8, lane = (rem >> 2) & 63, cc = rem & 3;
@@ -470,13 +470,16 @@ __global__ void pack_chain_f32_kernel(GraphW w, float *__restrict__ stream, int6
   }
   small[i] = v;
 }
+__global__ void pack_chain_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream, float *__restrict__ small) {
+  pack_chain_f32_at(w, stream, nstream, small, (int64_t)blockIdx.x * 256 + threadIdx.x);
+}
 
 // The update layers' transposed weights for chain_train_bwd_kernel, in the
 // f32 stream format, layers L-1 .. 0: A(n, k) = W_l[k][n] (k < H: W_a^T) or
 // W_l[k - H][H + n] / 2 (W_b^T with the mean's 1/deg).
 // ro: the readout's [W_a^T | W_b^T] of edge_mlp.0 first (16 chunks, no 1/deg).
-__global__ void pack_chain_bwd_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream, int ro) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void pack_chain_bwd_f32_at(const GraphW &w, float *__restrict__ stream, int64_t nstream,
+                                                      int ro, int64_t idx) {
   if (idx >= nstream) return;
   const int c = (int)(idx >> 11), rem = (int)(idx & 2047), j = rem >> 8, lane = (rem >> 2) & 63, cc = rem & 3;
   const bool readout = ro && c < 16;
@@ -485,6 +488,19 @@ __global__ void pack_chain_bwd_f32_kernel(GraphW w, float *__restrict__ stream, 
   const float *W = readout ? w.w_e : w.w_l + l * w.lsw;
   const float half = readout ? 1.f : 0.5f;
   stream[idx] = s < kKS ? W[(int64_t)k * 2 * kH + n] : half * W[(int64_t)k * 2 * kH + kH + n];
+}
+__global__ void pack_chain_bwd_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream, int ro) {
+  pack_chain_bwd_f32_at(w, stream, nstream, ro, (int64_t)blockIdx.x * 256 + threadIdx.x);
+}
+// Both packs in one launch (the training forward packs the backward's
+// transposed stream too: the parameters do not change between the two passes
+// of a step): threads [0, ftotal) the forward's, then the backward's.
+__global__ void pack_chain_train_f32_kernel(GraphW w, float *__restrict__ stream, int64_t nstream,
+                                            float *__restrict__ small, int64_t ftotal, float *__restrict__ bstream,
+                                            int64_t nbstream, int ro) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx < ftotal) pack_chain_f32_at(w, stream, nstream, small, idx);
+  else pack_chain_bwd_f32_at(w, bstream, nbstream, ro, idx - ftotal);
 }
 
 template <int MT>
@@ -518,15 +534,17 @@ int64_t chain_train_bwd_pack_bytes(int layers) { return (int64_t)16 * (layers + 
 
 hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, float *g0, int64_t gstride,
                                         const unsigned *mbits, void *pack, const float *dPQ, hipStream_t s,
-                                        const float *pq, const float *gflux, const float *w2, float *epart) {
+                                        const float *pq, const float *gflux, const float *w2, float *epart,
+                                        bool prepacked) {
   // pq != nullptr: the readout's backward from the P/Q tape in this pass (EdgeFold), writing dPQ
   const EdgeFold ef{pq, gflux, w2, const_cast<float *>(dPQ), epart};
   const int L = w.layers;
   if (B <= 0 || (L == 0 && !dPQ)) return hipSuccess;
   float *stream = static_cast<float *>(pack);
   const int64_t nstream = (int64_t)16 * (L + (dPQ ? 1 : 0)) * 2048;
-  hipLaunchKernelGGL(pack_chain_bwd_f32_kernel, dim3((unsigned)(nstream / 256)), dim3(256), 0, s, w, stream, nstream,
-                     dPQ ? 1 : 0);
+  if (!prepacked)
+    hipLaunchKernelGGL(pack_chain_bwd_f32_kernel, dim3((unsigned)(nstream / 256)), dim3(256), 0, s, w, stream, nstream,
+                       dPQ ? 1 : 0);
   ChainW cw{};
   cw.stream = stream;
   cw.layers = L;
@@ -546,15 +564,22 @@ bool chain_train_fused_ok(const GraphW &w, int nx) {
 }
 
 hipError_t launch_chain_train_fwd_fused(const GraphW &w, const float *nf, int64_t B, int nx, float *fe, float *h0,
-                                        int64_t hstride, float *pq, unsigned *mbits, void *pack, hipStream_t s) {
+                                        int64_t hstride, float *pq, unsigned *mbits, void *pack, hipStream_t s,
+                                        void *bpack, int ro) {
   if (B <= 0) return hipSuccess;
   const int L = w.layers;
   float *stream = static_cast<float *>(pack);
   const int64_t nstream = (int64_t)chain_chunks(L, kPrecF32) * chain_chunk_bytes(kPrecF32) / 4;
   float *small = stream + nstream;
   const int64_t total = nstream + 512 + kH * (3 + L);
-  hipLaunchKernelGGL(pack_chain_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, w, stream, nstream,
-                     small);
+  if (bpack) {  // + the backward's stream (launch_chain_train_bwd_fused with prepacked)
+    const int64_t nb = (int64_t)16 * (L + (ro ? 1 : 0)) * 2048;
+    hipLaunchKernelGGL(pack_chain_train_f32_kernel, dim3((unsigned)((total + nb + 255) / 256)), dim3(256), 0, s, w,
+                       stream, nstream, small, total, static_cast<float *>(bpack), nb, ro);
+  } else {
+    hipLaunchKernelGGL(pack_chain_f32_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, w, stream,
+                       nstream, small);
+  }
   ChainW cw{};
   cw.stream = stream;
   cw.win = small;

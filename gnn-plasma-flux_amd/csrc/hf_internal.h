@@ -242,12 +242,16 @@ bool chain_train_fused_ok(const GraphW &w, int nx);
 int64_t chain_train_pack_bytes(int layers);
 int64_t chain_train_mask_bytes(int layers, int64_t N);
 int64_t chain_train_bwd_pack_bytes(int layers);
+// bpack (forward): also pack the backward's stream there (chain_train_bwd_pack_bytes(L);
+// ro: with the readout's [W_a^T | W_b^T] first, as the backward's dPQ form needs),
+// in the same launch; the backward then takes it with prepacked.
 hipError_t launch_chain_train_fwd_fused(const GraphW &w, const float *nf, int64_t B, int nx, float *fe, float *h0,
-                                        int64_t hstride, float *pq, unsigned *mbits, void *pack, hipStream_t s);
+                                        int64_t hstride, float *pq, unsigned *mbits, void *pack, hipStream_t s,
+                                        void *bpack = nullptr, int ro = 0);
 hipError_t launch_chain_train_bwd_fused(const GraphW &w, int64_t B, int nx, float *g0, int64_t gstride,
                                         const unsigned *mbits, void *pack, const float *dPQ, hipStream_t s,
                                         const float *pq = nullptr, const float *gflux = nullptr,
-                                        const float *w2 = nullptr, float *epart = nullptr);
+                                        const float *w2 = nullptr, float *epart = nullptr, bool prepacked = false);
 // The ablation loss's single-step terms and d loss / d flux_edge (train_chain.hip).
 int64_t ablation_loss_ws_bytes(int B, int nx);
 hipError_t launch_ablation_loss(const float *fe, const float *st, const float *ft, const float *sn, int B, int nx,

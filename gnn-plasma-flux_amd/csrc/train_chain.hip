@@ -89,22 +89,21 @@ inline unsigned part_reduce_blocks(int64_t I, int64_t J, int64_t nbias) {
 #endif
 constexpr int kPrSlices = HF_PR_SLICES;
 static_assert(kPrSlices == 8 || kPrSlices == 16, "slices: a power of two, 32 x slices threads");
-__global__ __launch_bounds__(32 * kPrSlices) void part_reduce4_kernel(const float *__restrict__ part, int S, int64_t I,
-                                                                      int64_t J, float *out, int ish, int64_t ld,
-                                                                      int64_t hoff, const float *__restrict__ bias_part,
-                                                                      int64_t nbias, float *bias, int64_t part_ps = 0,
-                                                                      int64_t out_ps = 0, int64_t bpart_ps = 0,
-                                                                      int64_t bias_ps = 0) {
-  __shared__ f4 s_q[kPrSlices][32];
-  // problem blockIdx.y (batched reductions): each pointer advanced by its stride
-  part += blockIdx.y * part_ps;
-  out += blockIdx.y * out_ps;
-  bias_part += blockIdx.y * bpart_ps;
-  if (bias) bias += blockIdx.y * bias_ps;
+__device__ __forceinline__ void part_reduce4_block(f4 (*s_q)[32], unsigned bx, unsigned by,
+                                                   const float *__restrict__ part, int S, int64_t I, int64_t J,
+                                                   float *out, int ish, int64_t ld, int64_t hoff,
+                                                   const float *__restrict__ bias_part, int64_t nbias, float *bias,
+                                                   int64_t part_ps, int64_t out_ps, int64_t bpart_ps,
+                                                   int64_t bias_ps) {
+  // problem by (batched reductions): each pointer advanced by its stride
+  part += by * part_ps;
+  out += by * out_ps;
+  bias_part += by * bpart_ps;
+  if (bias) bias += by * bias_ps;
   const int c = threadIdx.x & 31, q = threadIdx.x >> 5;
   const int64_t n4 = I * J / 4, wblocks = (n4 + 31) / 32;
-  const bool wb = blockIdx.x < wblocks;
-  const int64_t t = (wb ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - wblocks) * 32 + c;  // float4 index
+  const bool wb = bx < wblocks;
+  const int64_t t = (wb ? (int64_t)bx : (int64_t)bx - wblocks) * 32 + c;  // float4 index
   const bool ok = t < (wb ? n4 : (bias ? nbias / 4 : 0));
   const f4 *src = reinterpret_cast<const f4 *>(wb ? part : bias_part);
   const int64_t per = wb ? n4 : I / 4;  // float4s per split
@@ -141,6 +140,16 @@ __global__ __launch_bounds__(32 * kPrSlices) void part_reduce4_kernel(const floa
     }
   }
 }
+__global__ __launch_bounds__(32 * kPrSlices) void part_reduce4_kernel(const float *__restrict__ part, int S, int64_t I,
+                                                                      int64_t J, float *out, int ish, int64_t ld,
+                                                                      int64_t hoff, const float *__restrict__ bias_part,
+                                                                      int64_t nbias, float *bias, int64_t part_ps = 0,
+                                                                      int64_t out_ps = 0, int64_t bpart_ps = 0,
+                                                                      int64_t bias_ps = 0) {
+  __shared__ f4 s_q[kPrSlices][32];
+  part_reduce4_block(s_q, blockIdx.x, blockIdx.y, part, S, I, J, out, ish, ld, hoff, bias_part, nbias, bias, part_ps,
+                     out_ps, bpart_ps, bias_ps);
+}
 inline unsigned part_reduce4_blocks(int64_t I, int64_t J, int64_t nbias) {
   return (unsigned)((I * J / 4 + 31) / 32 + (nbias / 4 + 31) / 32);
 }
@@ -154,6 +163,58 @@ inline bool launch_part_reduce_batch(int NP, const float *part, int64_t part_ps,
                      s, part, S, I, J, out, ish, ld, hoff, bias_part, nbias, bias, part_ps, out_ps, bpart_ps, bias_ps);
   return true;
 }
+// Every split reduction of the fused backward in ONE launch, after the last
+// weight-gradient pass: the readout's dw2 / db2 (edge_partial_reduce_block,
+// blocks [0, eblocks)), then the part_reduce4 problems of the jobs in order
+// (the readout's dW_e, the update layers', the input layer's), each block's
+// arithmetic that of the kernel it replaces (bit for bit).  Four launches
+// (and their drains) become one.
+struct PrJob {
+  const float *part, *bpart;
+  float *out, *bias;
+  int64_t I, J, ld, hoff, nbias, part_ps, out_ps, bpart_ps, bias_ps;
+  int S, ish;
+  unsigned blocks, np;  // blocks per problem, problems
+};
+constexpr int kMaxPrJobs = 3;
+__device__ void edge_partial_reduce_block(float *s_v, int c, const float *__restrict__ partial, int nb, int H,
+                                          float *gw2, float *gb2);
+struct PrJobs {
+  PrJob j[kMaxPrJobs];
+  int n;
+  const float *epart;
+  float *gw2, *gb2;
+  int enb, eH;
+  unsigned eblocks;
+};
+__global__ __launch_bounds__(32 * kPrSlices) void final_reduce_kernel(PrJobs J) {
+  __shared__ f4 s_q[kPrSlices][32];
+  unsigned b = blockIdx.x;
+  if (b < J.eblocks) {
+    edge_partial_reduce_block(reinterpret_cast<float *>(&s_q[0][0]), (int)b, J.epart, J.enb, J.eH, J.gw2, J.gb2);
+    return;
+  }
+  b -= J.eblocks;
+  for (int k = 0; k < J.n; ++k) {
+    const PrJob &q = J.j[k];
+    if (b < q.blocks * q.np) {
+      const unsigned by = b / q.blocks;
+      part_reduce4_block(s_q, b - by * q.blocks, by, q.part, q.S, q.I, q.J, q.out, q.ish, q.ld, q.hoff, q.bpart,
+                         q.nbias, q.bias, q.part_ps, q.out_ps, q.bpart_ps, q.bias_ps);
+      return;
+    }
+    b -= q.blocks * q.np;
+  }
+}
+static_assert(32 * kPrSlices >= 256, "the edge reduction's 256 threads");
+inline PrJob pr_job(const float *part, int S, int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff,
+                    const float *bpart, int64_t nbias, float *bias, unsigned np = 1, int64_t part_ps = 0,
+                    int64_t out_ps = 0, int64_t bpart_ps = 0, int64_t bias_ps = 0) {
+  return PrJob{part,    bpart,   out, bias, I, J, ld, hoff, nbias, part_ps, out_ps, bpart_ps, bias_ps,
+               S,       ish,     part_reduce4_blocks(I, J, nbias), np};
+}
+inline bool pr_job_ok(int64_t I, int64_t J, int64_t nbias) { return J % 4 == 0 && I % 4 == 0 && nbias % 4 == 0; }
+
 // the float4 form where the shapes allow it
 #ifndef HF_PART_REDUCE4
 #define HF_PART_REDUCE4 1
@@ -365,13 +426,14 @@ __global__ __launch_bounds__(256) void edge_backward_h128_kernel(const float *__
 
 // gw2[c] = sum_b partial[b][c] (c < H), gb2 = sum_b partial[b][H]: block c,
 // thread k sums blocks k, k + 256, ... in order, then a fixed-order LDS tree.
-__global__ __launch_bounds__(256) void edge_partial_reduce_kernel(const float *__restrict__ partial, int nb, int H,
-                                                                  float *gw2, float *gb2) {
-  __shared__ float s_v[256];
-  const int c = blockIdx.x, k = threadIdx.x;
+// (block c; threads >= 256 of a wider block only pass the barriers)
+__device__ void edge_partial_reduce_block(float *s_v, int c, const float *__restrict__ partial, int nb, int H,
+                                          float *gw2, float *gb2) {
+  const int k = threadIdx.x;
   float v = 0.f;
-  for (int b = k; b < nb; b += 256) v = __fadd_rn(v, partial[(int64_t)b * (H + 1) + c]);
-  s_v[k] = v;
+  if (k < 256)
+    for (int b = k; b < nb; b += 256) v = __fadd_rn(v, partial[(int64_t)b * (H + 1) + c]);
+  if (k < 256) s_v[k] = v;
   __syncthreads();
   for (int w = 128; w >= 1; w >>= 1) {
     if (k < w) s_v[k] = __fadd_rn(s_v[k], s_v[k + w]);
@@ -381,6 +443,11 @@ __global__ __launch_bounds__(256) void edge_partial_reduce_kernel(const float *_
     if (c < H) gw2[c] = s_v[0];
     else *gb2 = s_v[0];
   }
+}
+__global__ __launch_bounds__(256) void edge_partial_reduce_kernel(const float *__restrict__ partial, int nb, int H,
+                                                                  float *gw2, float *gb2) {
+  __shared__ float s_v[256];
+  edge_partial_reduce_block(s_v, blockIdx.x, partial, nb, H, gw2, gb2);
 }
 
 // Input-layer weight gradient partials: part[s][o][c] = sum_{m in split} d[m][o] nf[m][c],
@@ -964,16 +1031,21 @@ bool fused_width(const GraphW &w) { return HF_TRAIN_FUSED && chain_train_fused_o
 int64_t chain_tape_bytes(const GraphW &w, int64_t N) {
   return (int64_t)((w.layers + 1) * al256(sizeof(float) * N * w.hidden) + al256(sizeof(float) * N * 2 * w.hidden) +
                    (fused_width(w) ? al256((size_t)chain_train_pack_bytes(w.layers)) +
-                                         al256((size_t)chain_train_mask_bytes(w.layers, N))
+                                         al256((size_t)chain_train_mask_bytes(w.layers, N)) +
+                                         al256((size_t)chain_train_bwd_pack_bytes(w.layers))
                                    : 0));
 }
+// the fused forward's packed weights, ReLU' bits, and the backward's packed
+// transposed weights (written by the forward's pack launch)
 struct FusedTape {
   void *pack;
   unsigned *mbits;
+  void *bpack;
 };
 FusedTape fused_tape(const GraphW &w, int64_t N, const ChainTape &t) {
   char *p = reinterpret_cast<char *>(t.pq) + al256(sizeof(float) * N * 2 * w.hidden);
-  return FusedTape{p, reinterpret_cast<unsigned *>(p + al256((size_t)chain_train_pack_bytes(w.layers)))};
+  char *m = p + al256((size_t)chain_train_pack_bytes(w.layers));
+  return FusedTape{p, reinterpret_cast<unsigned *>(m), m + al256((size_t)chain_train_mask_bytes(w.layers, N))};
 }
 bool fused_chain(const GraphW &w, int nx, int64_t N) { return HF_TRAIN_FUSED && chain_train_fused_ok(w, nx) && N % nx == 0; }
 
@@ -999,6 +1071,10 @@ bool fused_chain(const GraphW &w, int nx, int64_t N) { return HF_TRAIN_FUSED && 
 #ifndef HF_TRAIN_WGS
 #define HF_TRAIN_WGS 1
 #endif
+// 1: on that path, every split reduction in one launch (final_reduce_kernel)
+#ifndef HF_FINAL_REDUCE
+#define HF_FINAL_REDUCE 1
+#endif
 int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   const int64_t H = w.hidden;
   size_t b = al256(sizeof(float) * N * 2 * H);  // dPQ
@@ -1009,7 +1085,7 @@ int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   b += al256(sizeof(float) * kEdgeBlocks * (H + 1));
   b += al256(sizeof(float) * kInputSplits * H * (w.in_dim + 1));
   if (fused_width(w)) {  // fused backward: g[0..L] side by side + the transposed weights
-    b += (w.layers + 1) * al256(sizeof(float) * N * H) + al256((size_t)chain_train_bwd_pack_bytes(w.layers));
+    b += (w.layers + 1) * al256(sizeof(float) * N * H);
     // + every update layer's weight-gradient partials (the layers' GEMMs in one launch)
     const int64_t SB = std::max(tgemm_splits(N, kWgradBatchSplits), wgs_splits(N));
     if (HF_TRAIN_WG_BATCH) b += w.layers * (al256(sizeof(float) * SB * 2 * H * H) + al256(sizeof(float) * SB * 2 * H));
@@ -1026,7 +1102,7 @@ hipError_t launch_chain_forward_train(const GraphW &w, const float *nf, int64_t 
   if (fused_chain(w, nx, N)) {  // (N = B * nx on a tagged chain)
     const FusedTape f = fused_tape(w, N, t);
     return launch_chain_train_fwd_fused(w, nf, N / nx, nx, flux, t.h[0], (int64_t)(al256(sizeof(float) * N * H) / 4),
-                                        t.pq, f.mbits, f.pack, s);
+                                        t.pq, f.mbits, f.pack, s, f.bpack, HF_TRAIN_RO_FOLD);
   }
 #define HF_IN_FWD(FF)                                                                                      \
   hipLaunchKernelGGL(input_forward_kernel<FF>, dim3((unsigned)((N * (H / 4) + 255) / 256)), dim3(256), 0, s, nf, \
@@ -1074,7 +1150,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   const bool fused = fused_chain(w, nx, N);
   const int64_t gstride = (int64_t)(al256(sizeof(float) * N * H) / 4);
   float *G = fused ? take((L + 1) * al256(sizeof(float) * N * H)) : nullptr;
-  void *bpack = fused ? static_cast<void *>(take((size_t)chain_train_bwd_pack_bytes(L))) : nullptr;
+  void *bpack = fused ? fused_tape(w, N, t).bpack : nullptr;  // (packed by the forward)
   const bool wg_batch = fused && HF_TRAIN_WG_BATCH && L >= 1 && L <= kTgMaxBatch;
   // the layers' weight gradients: wgrad_stencil_kernel where its shapes hold, else tgemm_batch
   const bool wgs = wg_batch && HF_TRAIN_WGS && H == kWsH && nx % kWsKC == 0 && N % kWsKC == 0 &&
@@ -1088,8 +1164,16 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   const bool efold = fused && HF_TRAIN_EDGE_FOLD && HF_TRAIN_RO_FOLD && H == 128;
   float *efpart = efold ? take(sizeof(float) * (N / 16 + 1) * (H + 1)) : nullptr;
   hipError_t e;
+  // the fast path's split reductions all in one launch at the end (final_reduce_kernel)
+  const bool one_reduce = HF_FINAL_REDUCE && wgs && !efold && pr_job_ok(2 * H, H, H) && pr_job_ok(H, 2 * H, H) &&
+                          pr_job_ok(H, F, H);
+  PrJobs jobs{};
   auto reduce = [&](int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff, int64_t nbias,
                     float *bias) {
+    if (one_reduce) {
+      jobs.j[jobs.n++] = pr_job(part, (int)S, I, J, out, ish, ld, hoff, bpart, nbias, bias);
+      return hipSuccess;
+    }
     launch_part_reduce(part, (int)S, I, J, out, ish, ld, hoff, bpart, nbias, bias, s);
     return hipGetLastError();
   };
@@ -1102,9 +1186,17 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   else
     hipLaunchKernelGGL(edge_backward_kernel, dim3(kEdgeBlocks), dim3(256), 0, s, t.pq, H, N, nx, w.w_2, grad_flux, dPQ,
                        epart);
-  if (!efold)
+  if (one_reduce) {
+    jobs.epart = epart;
+    jobs.enb = kEdgeBlocks;
+    jobs.eH = H;
+    jobs.gw2 = const_cast<float *>(g.w_2);
+    jobs.gb2 = const_cast<float *>(g.b_2);
+    jobs.eblocks = (unsigned)(H + 1);
+  } else if (!efold) {
     hipLaunchKernelGGL(edge_partial_reduce_kernel, dim3((unsigned)(H + 1)), dim3(256), 0, s, epart,
                        kEdgeBlocks, H, const_cast<float *>(g.w_2), const_cast<float *>(g.b_2));
+  }
   // dW_e[c % H][(c / H) H + k] = sum_m dPQ[m][c] h[L][m][k]; db_e = column sums of dP
   auto readout_wgrad = [&]() -> hipError_t {
     const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
@@ -1128,7 +1220,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   // fused: every layer's data gradient in one IC-per-wave pass (chain_train_bwd_kernel)
   if (fused && (e = launch_chain_train_bwd_fused(w, N / nx, nx, G, gstride, fused_tape(w, N, t).mbits, bpack,
                                                  fold ? dPQ : nullptr, s, efold ? t.pq : nullptr, grad_flux,
-                                                 w.w_2, efpart)))
+                                                 w.w_2, efpart, true)))
     return e;
   if (efold) {  // dw2, db2 from the per-IC partials; then dW_e, db_e from the dPQ the pass wrote
     hipLaunchKernelGGL(edge_partial_reduce_kernel, dim3((unsigned)(H + 1)), dim3(256), 0, s, efpart,
@@ -1146,7 +1238,10 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
       bt.bpart[l] = lbpart + l * lbstride;
     }
     hipLaunchKernelGGL(wgrad_stencil_kernel, dim3((unsigned)(SB * L)), dim3(256), 0, s, bt, N, nx, wgs_rsplit(N));
-    if (!(HF_PR_BATCH && launch_part_reduce_batch(L, lpart, lpstride, (int)SB, H, 2 * H, const_cast<float *>(g.w_l),
+    if (one_reduce)
+      jobs.j[jobs.n++] = pr_job(lpart, (int)SB, H, 2 * H, const_cast<float *>(g.w_l), kNoSplit, 2LL * H, 0, lbpart, H,
+                                const_cast<float *>(g.b_l), (unsigned)L, lpstride, g.lsw, lbstride, g.lsb);
+    else if (!(HF_PR_BATCH && launch_part_reduce_batch(L, lpart, lpstride, (int)SB, H, 2 * H, const_cast<float *>(g.w_l),
                                                   g.lsw, kNoSplit, 2LL * H, 0, lbpart, lbstride, H,
                                                   const_cast<float *>(g.b_l), g.lsb, s)))
       for (int l = L - 1; l >= 0; --l)
@@ -1208,8 +1303,16 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   else
     HF_INPUT_DISPATCH(F, HF_IN_WG)
 #undef HF_IN_WG
-  launch_part_reduce(ipart, nsp, (int64_t)H, (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F, (int64_t)0,
-                     ipb, (int64_t)H, const_cast<float *>(g.b_in), s);
+  if (one_reduce) {
+    jobs.j[jobs.n++] = pr_job(ipart, nsp, (int64_t)H, (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F,
+                              (int64_t)0, ipb, (int64_t)H, const_cast<float *>(g.b_in));
+    unsigned nb = jobs.eblocks;
+    for (int k = 0; k < jobs.n; ++k) nb += jobs.j[k].blocks * jobs.j[k].np;
+    hipLaunchKernelGGL(final_reduce_kernel, dim3(nb), dim3(32 * kPrSlices), 0, s, jobs);
+  } else {
+    launch_part_reduce(ipart, nsp, (int64_t)H, (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F,
+                       (int64_t)0, ipb, (int64_t)H, const_cast<float *>(g.b_in), s);
+  }
   if (grad_nf)
     hipLaunchKernelGGL(input_dgrad_kernel, dim3((unsigned)((N * F + 255) / 256)), dim3(256), 0, s, d0, w.w_in, F, H, N,
                        grad_nf);
