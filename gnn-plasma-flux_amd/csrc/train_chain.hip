@@ -494,14 +494,12 @@ __global__ __launch_bounds__(256) void input_wgrad_kernel(const float *__restric
 // feature quad o4 = t & 31) sums rows m0 + k, m0 + k + 8, ... for features
 // 4 o4 .. +3 (one float4 of d, one of nf per row), then the 8 row lanes are
 // added in order through LDS.
-__global__ __launch_bounds__(256) void input_wgrad_h128f4_kernel(const float *__restrict__ d,
-                                                                 const float *__restrict__ nf, int64_t N,
-                                                                 int64_t rows, float *__restrict__ part,
-                                                                 float *__restrict__ bpart) {
+__device__ __forceinline__ void input_wgrad_h128f4_block(float (*s_w)[128][5], unsigned bx, const float *__restrict__ d,
+                                                         const float *__restrict__ nf, int64_t N, int64_t rows,
+                                                         float *__restrict__ part, float *__restrict__ bpart) {
   constexpr int H = 128, F = 4;
-  __shared__ float s_w[8][H][F + 1];
   const int k = threadIdx.x >> 5, o4 = threadIdx.x & 31;
-  const int64_t m0 = (int64_t)blockIdx.x * rows;
+  const int64_t m0 = (int64_t)bx * rows;
   const int64_t m1 = m0 + rows < N ? m0 + rows : N;
   f4 w[F], bs = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -529,9 +527,16 @@ __global__ __launch_bounds__(256) void input_wgrad_h128f4_kernel(const float *__
     float v = s_w[0][o][c];
 #pragma unroll
     for (int kk = 1; kk < 8; ++kk) v = __fadd_rn(v, s_w[kk][o][c]);
-    if (c < F) part[((int64_t)blockIdx.x * H + o) * F + c] = v;
-    else bpart[(int64_t)blockIdx.x * H + o] = v;
+    if (c < F) part[((int64_t)bx * H + o) * F + c] = v;
+    else bpart[(int64_t)bx * H + o] = v;
   }
+}
+__global__ __launch_bounds__(256) void input_wgrad_h128f4_kernel(const float *__restrict__ d,
+                                                                 const float *__restrict__ nf, int64_t N,
+                                                                 int64_t rows, float *__restrict__ part,
+                                                                 float *__restrict__ bpart) {
+  __shared__ float s_w[8][128][5];
+  input_wgrad_h128f4_block(s_w, blockIdx.x, d, nf, N, rows, part, bpart);
 }
 
 // the kernels above for in_dim F = 1..8
@@ -839,6 +844,13 @@ struct WgStencilBatch {
   const float *g[kTgMaxBatch], *x[kTgMaxBatch];
   float *part[kTgMaxBatch], *bpart[kTgMaxBatch];
   int n, S;
+  // blocks [n S, n S + in_blocks): the input layer's weight-gradient partials
+  // (input_wgrad_h128f4_block, F = 4), which then fill the CUs the layers'
+  // workgroups leave as they finish instead of following them
+  const float *in_d, *in_nf;
+  float *in_part, *in_bpart;
+  int64_t in_rows;
+  int in_blocks;
 };
 #ifndef HF_WGS_SPLITS
 #define HF_WGS_SPLITS 128
@@ -852,6 +864,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_stencil_kernel(WgStencilBatch bt
   __shared__ float sA[2][kWsKC * kWsStr];
   __shared__ float sB[2][(kWsKC + 2) * kWsStr];
   __shared__ f4 s_cs[256];
+  static_assert(sizeof(sA) >= sizeof(float) * 8 * 128 * 5, "the input job's LDS");
+  if (blockIdx.x >= (unsigned)(bt.n * bt.S)) {
+    input_wgrad_h128f4_block(reinterpret_cast<float (*)[128][5]>(&sA[0][0]), blockIdx.x - bt.n * bt.S, bt.in_d,
+                             bt.in_nf, N, bt.in_rows, bt.in_part, bt.in_bpart);
+    return;
+  }
   tg_stagger();
   const unsigned pb = blockIdx.x / (unsigned)bt.S, z = blockIdx.x - pb * (unsigned)bt.S;
   const float *__restrict__ G = bt.g[pb];
@@ -985,6 +1003,126 @@ __global__ __launch_bounds__(256, 2) void wgrad_stencil_kernel(WgStencilBatch bt
     *reinterpret_cast<f4 *>(bt.bpart[pb] + (int64_t)z * kWsH + 4 * t) = v;
   }
 }
+// The readout's weight gradient (fused path, H = 128):
+//   part[z][c][k] = sum_{m in split z} dPQ[m][c] h[L][m][k]  (c < 2H, k < H)
+//   bias_part[z][c] = sum_{m in split z} dPQ[m][c]
+// tgemm's EpiPart / COLSUM layout and arithmetic bit for bit (the same MFMA
+// operands and order per output; the column sums in tgemm's thread order:
+// rows of one residue mod 8 in increasing order, then the 8 residues in
+// order), but ONE workgroup owns the whole 256 x 128 tile of a split, so that
+// h[L]'s rows are staged once instead of once per 128-row tile.  Stages of
+// 16 cells (the 256-wide dPQ rows would not leave room for two workgroups per
+// CU at 32): wave w = outputs c in [64w, 64w + 64) x all 128 k.
+constexpr int kWrKC = 16, kWrStrA = 2 * kWsH + 8;
+#ifndef HF_WGR_SPLITS
+#define HF_WGR_SPLITS 512
+#endif
+constexpr int kWgrSplits = HF_WGR_SPLITS;
+__global__ __launch_bounds__(256, 2) void wgrad_readout_kernel(const float *__restrict__ dPQ,
+                                                               const float *__restrict__ X, int64_t N, int64_t rsplit,
+                                                               float *__restrict__ part, float *__restrict__ bpart) {
+  __shared__ float sA[2][kWrKC * kWrStrA];
+  __shared__ float sB[2][kWrKC * kWsStr];
+  __shared__ f4 s_cs[8][64];
+  const unsigned z = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, h = lane >> 5, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int rb = (int)((int64_t)z * rsplit), re = (int)(rb + rsplit < N ? rb + rsplit : N);
+  const int nst = rb < re ? (re - rb) / kWrKC : 0;  // whole stages (host-checked)
+  // loads of a stage at r0: A (dPQ) rows r0 + (t >> 5) + 8u, float4 columns (t & 31) + 32p (u, p < 2);
+  // B (h) rows r0 + (t >> 5) + 8u, float4 column t & 31 (the column sums' thread order: residue t >> 5)
+  f4 ra[2][2], rx[2], cs[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  const int g8 = t >> 5, c4 = 4 * (t & 31);
+  auto gload = [&](int r0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + g8 + 8 * u;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) ra[u][p] = *reinterpret_cast<const f4 *>(dPQ + (unsigned)(r * 2 * kWsH + 128 * p + c4));
+      rx[u] = *reinterpret_cast<const f4 *>(X + (unsigned)(r * kWsH + c4));
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = g8 + 8 * u;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        *reinterpret_cast<f4 *>(&sA[buf][row * kWrStrA + 128 * p + c4]) = ra[u][p];
+        cs[p] += ra[u][p];
+      }
+      *reinterpret_cast<f4 *>(&sB[buf][row * kWsStr + c4]) = rx[u];
+    }
+  };
+  f16 acc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[a][b][v] = 0.f;
+  if (nst > 0) {
+    gload(rb);
+    lstore(0);
+  }
+  __syncthreads();
+  auto stage = [&](auto parity, int k) {
+    constexpr int cur = decltype(parity)::value;
+    if (k + 1 < nst) gload(rb + (k + 1) * kWrKC);
+    const float *A = sA[cur], *B = sB[cur];
+#pragma unroll
+    for (int g = 0; g < kWrKC / 8; ++g) {
+      float av[2][4], bv[4][4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int r = 8 * g + 4 * h + s;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) av[x][s] = A[r * kWrStrA + 64 * wave + 32 * x + (lane & 31)];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) bv[b][s] = B[r * kWsStr + 32 * b + (lane & 31)];
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a][s], bv[b][s], acc[a][b], 0, 0, 0);
+    }
+    if (k + 1 < nst) lstore(cur ^ 1);
+    __syncthreads();
+  };
+  int k = 0;
+  for (; k + 2 <= nst; k += 2) {
+    stage(std::integral_constant<int, 0>{}, k);
+    stage(std::integral_constant<int, 1>{}, k + 1);
+  }
+  if (k < nst) stage(std::integral_constant<int, 0>{}, k);
+  float *pz = part + (int64_t)z * 2 * kWsH * kWsH;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int j = 32 * b + (lane & 31);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        pz[(64 * wave + 32 * a + 8 * (v >> 2) + 4 * h + (v & 3)) * kWsH + j] = acc[a][b][v];
+  }
+  // column sums: thread (g8, column quad) holds rows of residue g8; fold the 8 residues in order
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    s_cs[g8][(t & 31) + 32 * p] = cs[p];
+  }
+  __syncthreads();
+  if (t < 64) {
+    f4 v = s_cs[0][t];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) v += s_cs[q][t];
+    *reinterpret_cast<f4 *>(bpart + (int64_t)z * 2 * kWsH + 4 * (t & 31) + 128 * (t >> 5)) = v;
+  }
+}
+inline int64_t wgr_rsplit(int64_t N) { return ((N + kWgrSplits - 1) / kWgrSplits + kWsKC - 1) / kWsKC * kWsKC; }
+inline int64_t wgr_splits(int64_t N) { return (N + wgr_rsplit(N) - 1) / wgr_rsplit(N); }
+
 // splits of N cells (whole stages)
 inline int64_t wgs_rsplit(int64_t N) { return ((N + kWgsSplits - 1) / kWgsSplits + kWsKC - 1) / kWsKC * kWsKC; }
 inline int64_t wgs_splits(int64_t N) { return (N + wgs_rsplit(N) - 1) / wgs_rsplit(N); }
@@ -1071,15 +1209,30 @@ bool fused_chain(const GraphW &w, int nx, int64_t N) { return HF_TRAIN_FUSED && 
 #ifndef HF_TRAIN_WGS
 #define HF_TRAIN_WGS 1
 #endif
+// 1: the readout's weight gradient on wgrad_readout_kernel (fused path, H = 128).
+// Measured and not kept (profiles/r06_train_wgs_ab.txt): 80.6 us at 500 splits
+// against tgemm's 76.4 us at 250, and the final reduction 21 -> 28 us (bitwise
+// equal gradients at 250 splits, where it fills only half the CUs)
+#ifndef HF_TRAIN_WGR
+#define HF_TRAIN_WGR 0
+#endif
 // 1: on that path, every split reduction in one launch (final_reduce_kernel)
 #ifndef HF_FINAL_REDUCE
 #define HF_FINAL_REDUCE 1
+#endif
+// 1: the float4 input-layer weight gradient (H = 128, F = 4)
+#ifndef HF_INPUT_WGRAD4
+#define HF_INPUT_WGRAD4 1
+#endif
+// 1: on the stencil path, that gradient's blocks on the stencil kernel's launch
+#ifndef HF_INPUT_IN_WGS
+#define HF_INPUT_IN_WGS 1
 #endif
 int64_t chain_backward_ws_bytes(const GraphW &w, int64_t N) {
   const int64_t H = w.hidden;
   size_t b = al256(sizeof(float) * N * 2 * H);  // dPQ
   b += 2 * al256(sizeof(float) * N * H);        // deltas
-  const int64_t S = tgemm_splits(N, kWgradSplits);
+  const int64_t S = std::max(tgemm_splits(N, kWgradSplits), wgr_splits(N));
   b += al256(sizeof(float) * S * 2 * H * H);    // weight-gradient partials (largest: 2H x H or H x 2H)
   b += al256(sizeof(float) * S * 2 * H);        // bias partials
   b += al256(sizeof(float) * kEdgeBlocks * (H + 1));
@@ -1140,10 +1293,11 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
     return r;
   };
   const int64_t S = tgemm_splits(N, kWgradSplits);
+  const int64_t Sp = std::max(S, wgr_splits(N));  // (the partial buffers' splits, as chain_backward_ws_bytes)
   float *dPQ = take(sizeof(float) * N * 2 * H);
   float *dl[2] = {take(sizeof(float) * N * H), take(sizeof(float) * N * H)};
-  float *part = take(sizeof(float) * S * 2 * H * H);
-  float *bpart = take(sizeof(float) * S * 2 * H);
+  float *part = take(sizeof(float) * Sp * 2 * H * H);
+  float *bpart = take(sizeof(float) * Sp * 2 * H);
   float *epart = take(sizeof(float) * kEdgeBlocks * (H + 1));
   float *ipart = take(sizeof(float) * kInputSplits * H * (F + 1));
   // fused (FluxGNN(4, 128) on nx <= 64): g[l] = G + l * gstride for every layer
@@ -1156,6 +1310,9 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   const bool wgs = wg_batch && HF_TRAIN_WGS && H == kWsH && nx % kWsKC == 0 && N % kWsKC == 0 &&
                    N * kWsH < (int64_t(1) << 31);
   const int64_t SB = wgs ? wgs_splits(N) : tgemm_splits(N, kWgradBatchSplits);
+  // the readout's weight gradient: wgrad_readout_kernel on the fused path at H = 128
+  const bool wgr = fused && HF_TRAIN_WGR && H == kWsH && N % kWsKC == 0 && N * 2 * kWsH < (int64_t(1) << 31);
+  const int64_t SR = wgr ? wgr_splits(N) : S;
   const int64_t lpstride = (int64_t)(al256(sizeof(float) * SB * 2 * H * H) / 4),
                 lbstride = (int64_t)(al256(sizeof(float) * SB * 2 * H) / 4);
   float *lpart = wg_batch ? take(L * al256(sizeof(float) * SB * 2 * H * H)) : nullptr;
@@ -1168,13 +1325,13 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   const bool one_reduce = HF_FINAL_REDUCE && wgs && !efold && pr_job_ok(2 * H, H, H) && pr_job_ok(H, 2 * H, H) &&
                           pr_job_ok(H, F, H);
   PrJobs jobs{};
-  auto reduce = [&](int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff, int64_t nbias,
-                    float *bias) {
+  auto reduce = [&](int64_t I, int64_t J, float *out, int ish, int64_t ld, int64_t hoff, int64_t nbias, float *bias,
+                    int splits) {
     if (one_reduce) {
-      jobs.j[jobs.n++] = pr_job(part, (int)S, I, J, out, ish, ld, hoff, bpart, nbias, bias);
+      jobs.j[jobs.n++] = pr_job(part, splits, I, J, out, ish, ld, hoff, bpart, nbias, bias);
       return hipSuccess;
     }
-    launch_part_reduce(part, (int)S, I, J, out, ish, ld, hoff, bpart, nbias, bias, s);
+    launch_part_reduce(part, splits, I, J, out, ish, ld, hoff, bpart, nbias, bias, s);
     return hipGetLastError();
   };
   // readout: dPQ, dw2, db2                                                          (:62-66)
@@ -1199,12 +1356,18 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   }
   // dW_e[c % H][(c / H) H + k] = sum_m dPQ[m][c] h[L][m][k]; db_e = column sums of dP
   auto readout_wgrad = [&]() -> hipError_t {
-    const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
-    const VPlain B{t.h[L], H, N, kNoSplit, 0, H};
-    if ((e = tgemm<VPlain, true, VPlain, true, EpiPart, true, true>(A, B, EpiPart{part, 2LL * H, H}, 2 * H, H, N,
-                                                               kWgradSplits, s, bpart)))
+    if (wgr) {
+      hipLaunchKernelGGL(wgrad_readout_kernel, dim3((unsigned)SR), dim3(256), 0, s, dPQ, t.h[L], N, wgr_rsplit(N), part,
+                         bpart);
+    } else {
+      const VPlain A{dPQ, 2LL * H, N, kNoSplit, 0, 2 * H};
+      const VPlain B{t.h[L], H, N, kNoSplit, 0, H};
+      if ((e = tgemm<VPlain, true, VPlain, true, EpiPart, true, true>(A, B, EpiPart{part, 2LL * H, H}, 2 * H, H, N,
+                                                                 kWgradSplits, s, bpart)))
+        return e;
+    }
+    if ((e = reduce(2 * H, H, const_cast<float *>(g.w_e), hsh, 2LL * H, H, H, const_cast<float *>(g.b_e), (int)SR)))
       return e;
-    if ((e = reduce(2 * H, H, const_cast<float *>(g.w_e), hsh, 2LL * H, H, H, const_cast<float *>(g.b_e)))) return e;
     return hipSuccess;
   };
   if (!efold && (e = readout_wgrad())) return e;
@@ -1227,6 +1390,11 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
                        (int)(N / nx), H, const_cast<float *>(g.w_2), const_cast<float *>(g.b_2));
     if ((e = readout_wgrad())) return e;
   }
+  // the input layer's weight-gradient splits
+  const int64_t in_rows = (N + kInputSplits - 1) / kInputSplits;
+  const int in_nsp = (int)((N + in_rows - 1) / in_rows);
+  // on the stencil kernel's launch (its blocks after the layers')
+  const bool in_fold = wgs && HF_INPUT_IN_WGS && HF_INPUT_WGRAD4 && H == 128 && F == 4;
   if (wgs) {  // dW_l, db_l of every update layer: one launch, then the layers' reductions
     WgStencilBatch bt{};
     bt.n = L;
@@ -1237,7 +1405,16 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
       bt.part[l] = lpart + l * lpstride;
       bt.bpart[l] = lbpart + l * lbstride;
     }
-    hipLaunchKernelGGL(wgrad_stencil_kernel, dim3((unsigned)(SB * L)), dim3(256), 0, s, bt, N, nx, wgs_rsplit(N));
+    if (in_fold) {  // + the input layer's weight-gradient partials (d = g[0])
+      bt.in_d = G;
+      bt.in_nf = nf;
+      bt.in_part = ipart;
+      bt.in_bpart = ipart + (int64_t)kInputSplits * H * F;
+      bt.in_rows = in_rows;
+      bt.in_blocks = in_nsp;
+    }
+    hipLaunchKernelGGL(wgrad_stencil_kernel, dim3((unsigned)(SB * L + bt.in_blocks)), dim3(256), 0, s, bt, N, nx,
+                       wgs_rsplit(N));
     if (one_reduce)
       jobs.j[jobs.n++] = pr_job(lpart, (int)SB, H, 2 * H, const_cast<float *>(g.w_l), kNoSplit, 2LL * H, 0, lbpart, H,
                                 const_cast<float *>(g.b_l), (unsigned)L, lpstride, g.lsw, lbstride, g.lsb);
@@ -1275,7 +1452,7 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
                                                                   kWgradSplits, s, bpart)))
         return e;
       if ((e = reduce(H, 2 * H, const_cast<float *>(g.w_l + l * g.lsw), kNoSplit, 2LL * H, 0, H,
-                      const_cast<float *>(g.b_l + l * g.lsb))))
+                      const_cast<float *>(g.b_l + l * g.lsb), (int)S)))
         return e;
     }
     // dh[l] = W_a^T delta + W_b^T agg(delta) (the aggregation's adjoint is itself on the
@@ -1290,18 +1467,18 @@ hipError_t launch_chain_backward(const GraphW &w, const float *nf, int64_t N, in
   }
   // input MLP                                                                        (:49)
   const float *d0 = fused ? G : dl[cur];
-  const int64_t rows = (N + kInputSplits - 1) / kInputSplits;
-  const int nsp = (int)((N + rows - 1) / rows);
+  const int64_t rows = in_rows;
+  const int nsp = in_nsp;
   float *ipb = ipart + (int64_t)kInputSplits * H * F;
 #define HF_IN_WG(FF) \
   hipLaunchKernelGGL(input_wgrad_kernel<FF>, dim3((unsigned)nsp), dim3(256), 0, s, d0, nf, H, N, rows, ipart, ipb)
-#ifndef HF_INPUT_WGRAD4
-#define HF_INPUT_WGRAD4 1
-#endif
-  if (HF_INPUT_WGRAD4 && H == 128 && F == 4)
+  if (in_fold) {
+    // (on the stencil kernel's launch above)
+  } else if (HF_INPUT_WGRAD4 && H == 128 && F == 4) {
     hipLaunchKernelGGL(input_wgrad_h128f4_kernel, dim3((unsigned)nsp), dim3(256), 0, s, d0, nf, N, rows, ipart, ipb);
-  else
+  } else {
     HF_INPUT_DISPATCH(F, HF_IN_WG)
+  }
 #undef HF_IN_WG
   if (one_reduce) {
     jobs.j[jobs.n++] = pr_job(ipart, nsp, (int64_t)H, (int64_t)F, const_cast<float *>(g.w_in), kNoSplit, (int64_t)F,
