@@ -2,7 +2,7 @@
 # PMC passes over the training bench at B = 2000 (tools/bench_train.py), one
 # counter set per pass: shader clock + MFMA busy; instruction mix / waits; LDS
 # bank conflicts + HBM fetch; HBM write + L2 requests.  Summaries for the
-# fused forward / backward passes and the weight-gradient GEMM.
+# fused forward / backward passes, the weight-gradient kernels and the final reduction.
 set -o pipefail
 cd "$(dirname "$0")/.."
 TAG=${1:-r05}
@@ -18,7 +18,7 @@ for P in "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES
   timeout -s KILL 150 rocprofv3 --pmc $P --kernel-trace -d /tmp/pmc_tr${i}_$TAG -o p -- $B \
     > gpurun_out/pmc_tr${i}_$TAG.log 2>&1 || exit $?
 done
-for K in "chain_train_fwd" "chain_train_bwd" "VPlain, true, hf::tg::VStencil, true" "tgemm_kernel"; do
+for K in "chain_train_fwd" "chain_train_bwd" "wgrad_stencil_kernel" "tgemm_kernel" "final_reduce_kernel"; do
   echo "== $K"
   python3 tools/pmc_summary.py "$K" /tmp/pmc_tr[1-4]_$TAG/*.db | grep -v dispatch=
 done > gpurun_out/pmc_train_$TAG.txt 2>&1
