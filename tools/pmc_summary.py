@@ -37,7 +37,8 @@ def main(sub, paths):
             if "SQ_VALU_MFMA_BUSY_CYCLES" in tot:
                 der.append(f"mfma_busy={tot['SQ_VALU_MFMA_BUSY_CYCLES'] / (4 * CUS * gui):.4f}")
         if "SQ_INSTS_MFMA" in tot and "SQ_INSTS_VALU" in tot:
-            der.append(f"nonmfma_valu_per_mfma={(tot['SQ_INSTS_VALU'] - tot['SQ_INSTS_MFMA']) / tot['SQ_INSTS_MFMA']:.3f}")
+            if tot['SQ_INSTS_MFMA'] > 0:
+                der.append(f"nonmfma_valu_per_mfma={(tot['SQ_INSTS_VALU'] - tot['SQ_INSTS_MFMA']) / tot['SQ_INSTS_MFMA']:.3f}")
         print(p.split("/")[-2], "TOTAL", f"dispatches={len(by)}", f"dur_us={tdur / 1e3:.1f}",
               " ".join(f"{k}={v:.6g}" for k, v in sorted(tot.items())), *der)
 
