@@ -38,7 +38,7 @@ elif mode == "diag4":
     print(n, rep, json.dumps(d))
 elif mode in ("train", "trainks"):
     g = d["gpu"]["2000"]
-    print(n, rep, g["eager_samples_per_s"], g["graphed_samples_per_s"], g["graphed_flat_adam_samples_per_s"],
+    print(n, rep, g["eager_samples_per_s"], g["graphed_samples_per_s"], g.get("eager_flat_adam_samples_per_s"), g["graphed_flat_adam_samples_per_s"],
           d["roofline"]["frac"])
 elif mode == "models":
     g = d["gpu"]
