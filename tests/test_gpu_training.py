@@ -106,7 +106,8 @@ def test_backward_deterministic_and_chain_batch_vs_oracle(hf):
                                                           (64, 4, 3, 16, False), (16, 3, 2, 8, False),
                                                           (8, 2, 1, 4, False), (64, 3, 2, 256, False),
                                                           (16, 5, 2, 128, False), (32, 9, 0, 128, False),
-                                                          (48, 7, 8, 128, False), (32, 11, 3, 128, False)])
+                                                          (48, 7, 8, 128, False), (32, 11, 3, 128, False),
+                                                          (64, 301, 4, 128, True)])
 def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden, kinkfree):
     """The chain training path (train_chain.hip: stencil-loader GEMMs, P/Q
     readout, split-K weight gradients) on tagged chains of any nx, layer count
@@ -128,7 +129,8 @@ def test_chain_training_path_vs_oracle(hf, nx, B, layers, hidden, kinkfree):
     and 100 at width 128 run the GEMM forward.  The update layers' weight
     gradients of the fused path run on wgrad_stencil_kernel for nx in {32, 64}
     (32-cell stages with the chain's halo rows: nx = 32 wraps at both ends of
-    every stage) and on tgemm_batch for nx in {16, 48}."""
+    every stage; 301 chains of 64 leave a last split of two stages) and on
+    tgemm_batch for nx in {16, 48}."""
     rng = np.random.default_rng(nx * 100 + layers)
     if kinkfree:
         u = lambda a, shape: rng.uniform(-a, a, shape)  # noqa: E731
